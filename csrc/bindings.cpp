@@ -1,0 +1,148 @@
+// xdot — torch operator bindings for the gfx950 kernels (registered as torch.ops.xdot.*).
+//
+// The kernels themselves live in *.hip translation units that do not include any torch
+// header (fast rebuilds); this file only validates arguments on the host, resolves the
+// current HIP stream and calls the C-ABI launchers.  Every launch is bounds-checked on
+// the host against the tensors' storage so a bad stride can never turn into a GPU fault.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace {
+
+int dt_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return xdot::DT_F32;
+    case at::kBFloat16: return xdot::DT_BF16;
+    case at::kHalf: return xdot::DT_F16;
+    default: TORCH_CHECK(false, "xdot: unsupported dtype ", t);
+  }
+  return -1;
+}
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+// elements addressable from t.data_ptr() to the end of its storage
+int64_t avail_elems(const at::Tensor& t) {
+  const int64_t bytes = (int64_t)t.storage().nbytes() - t.storage_offset() * (int64_t)t.element_size();
+  return bytes / (int64_t)t.element_size();
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+void check_launch(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "xdot: ", what, " launch failed: ", hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------------------------
+void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N,
+          int64_t K, int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb,
+          int64_t ldc, int64_t sA1, int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1,
+          int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "xdot.gemm: tensors must be on GPU");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "xdot.gemm: A/B dtype mismatch");
+  TORCH_CHECK(M >= 0 && N >= 0 && K >= 0 && nseg >= 1 && nb1 >= 1 && nb2 >= 1, "xdot.gemm: bad sizes");
+  if (M == 0 || N == 0) return;
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "xdot.gemm: dim too large");
+  TORCH_CHECK(nb1 * nb2 <= 65535, "xdot.gemm: too many batches");
+  // host-side bounds check of the furthest element each operand touches
+  auto last = [](int64_t b1, int64_t s1, int64_t b2, int64_t s2, int64_t ns, int64_t ss) {
+    return (b1 - 1) * s1 + (b2 - 1) * s2 + (ns - 1) * ss;
+  };
+  if (K > 0) {
+    const int64_t la = last(nb1, sA1, nb2, sA2, nseg, sAseg) + (a_mc ? (K - 1) * lda + (M - 1) : (M - 1) * lda + (K - 1));
+    const int64_t lb = last(nb1, sB1, nb2, sB2, nseg, sBseg) + (b_mc ? (K - 1) * ldb + (N - 1) : (N - 1) * ldb + (K - 1));
+    TORCH_CHECK(la < avail_elems(A), "xdot.gemm: A access out of bounds (", la, " >= ", avail_elems(A), ")");
+    TORCH_CHECK(lb < avail_elems(B), "xdot.gemm: B access out of bounds (", lb, " >= ", avail_elems(B), ")");
+  }
+  const int64_t lc = last(nb1, sC1, nb2, sC2, 1, 0) + (M - 1) * ldc + (N - 1);
+  TORCH_CHECK(lc < avail_elems(C), "xdot.gemm: C access out of bounds");
+
+  const int eps = 16 / (int)A.element_size();
+  auto mult = [&](int64_t v) { return v % eps == 0; };
+  bool vec = aligned16(A.data_ptr()) && aligned16(B.data_ptr()) && aligned16(C.data_ptr()) &&
+             mult(lda) && mult(ldb) && mult(sA1) && mult(sA2) && mult(sB1) && mult(sB2) &&
+             mult(sAseg) && mult(sBseg);
+  const int eo = 16 / (int)C.element_size();
+  vec = vec && (sC1 % eo == 0) && (sC2 % eo == 0);
+
+  xdot::GemmArgs g{};
+  g.A = A.data_ptr(); g.B = B.data_ptr(); g.C = C.data_ptr();
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.nseg = (int)nseg; g.nb2 = (int)nb2;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.sA1 = sA1; g.sA2 = sA2; g.sB1 = sB1; g.sB2 = sB2; g.sC1 = sC1; g.sC2 = sC2;
+  g.sAseg = sAseg; g.sBseg = sBseg; g.alpha = (float)alpha;
+  c10::DeviceGuard guard(A.device());
+  const int rc = xdot_gemm_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()),
+                                  dt_code(C.scalar_type()), a_mc, b_mc, vec, cur_stream(A));
+  TORCH_CHECK(rc == 0, "xdot.gemm: unsupported dtype combination ", A.scalar_type(), " -> ", C.scalar_type());
+  check_launch(hipGetLastError(), "gemm");
+}
+
+// ------------------------------------------------------------------------------------
+at::Tensor softmax_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& mask, double scale,
+                       int64_t mdiv, int64_t mmul, int64_t mmod) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "xdot.softmax_fwd: x must be a contiguous GPU tensor");
+  const int64_t T = x.size(-1);
+  const int64_t rows = T == 0 ? 0 : x.numel() / T;
+  auto y = at::empty_like(x);
+  xdot::smx::Args a{};
+  a.x = x.data_ptr(); a.out = y.data_ptr(); a.rows = rows; a.T = T; a.scale = (float)scale;
+  a.mdiv = mdiv; a.mmul = mmul; a.mmod = mmod; a.mask = nullptr;
+  bool vec = (T % 8 == 0) && aligned16(x.data_ptr()) && aligned16(y.data_ptr());
+  if (mask.has_value() && mask->defined()) {
+    const auto& m = *mask;
+    TORCH_CHECK(m.is_cuda() && m.is_contiguous() && m.scalar_type() == at::kBool, "xdot.softmax_fwd: mask must be contiguous bool on GPU");
+    TORCH_CHECK(m.size(-1) == T, "xdot.softmax_fwd: mask last dim mismatch");
+    TORCH_CHECK(mdiv > 0 && mmod > 0, "xdot.softmax_fwd: bad mask row map");
+    const int64_t mrows = m.numel() / T;
+    // furthest mask row touched
+    const int64_t lr = ((rows - 1) / mdiv) * mmul + std::min<int64_t>(rows - 1, mmod - 1);
+    TORCH_CHECK(rows == 0 || lr < mrows, "xdot.softmax_fwd: mask row map out of bounds");
+    a.mask = reinterpret_cast<const uint8_t*>(m.data_ptr());
+    vec = vec && ((reinterpret_cast<uintptr_t>(m.data_ptr()) & 7) == 0);
+  }
+  TORCH_CHECK(rows <= 0x7fffffff, "xdot.softmax_fwd: too many rows");
+  c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(xdot_softmax_fwd_launch(&a, dt_code(x.scalar_type()), vec, cur_stream(x)) == 0, "xdot.softmax_fwd: dtype");
+  check_launch(hipGetLastError(), "softmax_fwd");
+  return y;
+}
+
+at::Tensor softmax_bwd(const at::Tensor& y, const at::Tensor& dy, double scale) {
+  TORCH_CHECK(y.is_cuda() && y.is_contiguous() && dy.is_contiguous(), "xdot.softmax_bwd: contiguous GPU tensors required");
+  TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == dy.scalar_type(), "xdot.softmax_bwd: y/dy mismatch");
+  const int64_t T = y.size(-1);
+  const int64_t rows = T == 0 ? 0 : y.numel() / T;
+  auto dx = at::empty_like(y);
+  xdot::smx::Args a{};
+  a.x = y.data_ptr(); a.dy = dy.data_ptr(); a.out = dx.data_ptr(); a.rows = rows; a.T = T;
+  a.scale = (float)scale; a.mdiv = 1; a.mmul = 0; a.mmod = 1;
+  const bool vec = (T % 8 == 0) && aligned16(y.data_ptr()) && aligned16(dy.data_ptr()) && aligned16(dx.data_ptr());
+  c10::DeviceGuard guard(y.device());
+  TORCH_CHECK(xdot_softmax_bwd_launch(&a, dt_code(y.scalar_type()), vec, cur_stream(y)) == 0, "xdot.softmax_bwd: dtype");
+  check_launch(hipGetLastError(), "softmax_bwd");
+  return dx;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(xdot, m) {
+  m.def("gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int nseg, int nb1, int nb2, "
+        "int lda, int ldb, int ldc, int sA1, int sA2, int sB1, int sB2, int sC1, int sC2, "
+        "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha) -> ()");
+  m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
+  m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
+  m.impl("gemm", &gemm);
+  m.impl("softmax_fwd", &softmax_fwd);
+  m.impl("softmax_bwd", &softmax_bwd);
+}

@@ -1,0 +1,91 @@
+"""Numerics of the gfx950 HIP kernels against plain fp32 PyTorch references (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [torch.bfloat16, torch.float16, torch.float32]
+
+
+def _tol(dt, k):
+    if dt == torch.float32:
+        return 1e-4 * math.sqrt(k)
+    return (2e-2 if dt == torch.bfloat16 else 4e-3) * math.sqrt(max(k, 1) / 64)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (200, 77, 96), (513, 300, 130), (64, 1000, 8)])
+def test_strided_gemm_layouts(gpu, dt, a_mc, b_mc, M, N, K):
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    A = torch.randn(2, M, K, generator=g) if not a_mc else torch.randn(2, K, M, generator=g)
+    B = torch.randn(2, N, K, generator=g) if not b_mc else torch.randn(2, K, N, generator=g)
+    Ad, Bd = A.to(gpu, dt), B.to(gpu, dt)
+    C = torch.empty(2, M, N, device=gpu, dtype=torch.float32)
+    strided_gemm(Ad, Bd, C, M=M, N=N, K=K, nb2=2, lda=(M if a_mc else K), ldb=(N if b_mc else K),
+                 ldc=N, sA2=M * K, sB2=N * K, sC2=M * N, a_mc=a_mc, b_mc=b_mc, alpha=0.5)
+    Af = Ad.float()
+    Bf = Bd.float()
+    opA = Af.transpose(-1, -2) if a_mc else Af
+    opB = Bf if b_mc else Bf.transpose(-1, -2)
+    ref = 0.5 * torch.matmul(opA, opB)
+    err = (C - ref).abs().max().item()
+    assert err <= _tol(dt, K) * max(1.0, ref.abs().max().item() / 4), err
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_segments_and_bf16_out(gpu, dt):
+    """K segments (the fused sum over ranks of distributed_matmul_all)."""
+    from xdot.ops.gemm import all_chunk_into
+
+    N, Pn, R, c = 3, 2, 50, 40
+    left = torch.randn(Pn, R, N * R, device=gpu).to(dt)
+    chunk = torch.randn(N, Pn, R, c, device=gpu).to(dt)
+    out = torch.zeros(Pn, R, c, device=gpu, dtype=dt)
+    all_chunk_into(out, left, chunk, 0)
+    ref = sum(left.float()[..., j * R:(j + 1) * R] @ chunk.float()[j] for j in range(N))
+    assert torch.allclose(out.float(), ref, atol=_tol(dt, N * R) * 4, rtol=2e-2)
+
+
+def test_gemm_integer_exact_fp32(gpu):
+    """Exact small-integer products must be bit-exact in fp32 (reference tests use ==)."""
+    from xdot.ops.gemm import matmul
+
+    a = torch.randint(-8, 8, (3, 67, 45), device=gpu).float()
+    b = torch.randint(-8, 8, (3, 45, 91), device=gpu).float()
+    assert torch.equal(matmul(a, b), a @ b)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("T", [8, 100, 2048, 25000, 70000])
+def test_softmax_fwd_bwd(gpu, dt, T):
+    from xdot.ops.softmax import scale_mask_softmax_fwd, scale_mask_softmax_bwd
+
+    B, H, R = 1, 2, 3
+    x = (torch.randn(B, H, R, T, device=gpu) * 3).to(dt)
+    mask = torch.rand(B, R, T, device=gpu) < 0.3
+    mask[..., 0] = False
+    scale = 0.37
+    y = scale_mask_softmax_fwd(x, mask, scale)
+    ref = torch.softmax((x.float() * scale).masked_fill(mask.unsqueeze(1), -float("inf")), -1)
+    atol = 1e-6 if dt == torch.float32 else 8e-3
+    assert torch.allclose(y.float(), ref, atol=atol, rtol=2e-2)
+    dy = torch.randn_like(x)
+    dx = scale_mask_softmax_bwd(y, dy, scale)
+    yf = y.float()
+    dref = scale * yf * (dy.float() - (dy.float() * yf).sum(-1, keepdim=True))
+    assert torch.allclose(dx.float(), dref, atol=atol * 4, rtol=3e-2)
+
+
+def test_softmax_fully_masked_row_is_nan(gpu):
+    from xdot.ops.softmax import scale_mask_softmax_fwd
+
+    x = torch.randn(1, 1, 2, 64, device=gpu)
+    mask = torch.zeros(1, 2, 64, dtype=torch.bool, device=gpu)
+    mask[0, 1] = True
+    y = scale_mask_softmax_fwd(x, mask, 1.0)
+    assert torch.isnan(y[0, 0, 1]).all() and not torch.isnan(y[0, 0, 0]).any()

@@ -1,0 +1,69 @@
+"""Loader for the in-tree gfx950 extension ``xdot/_C.so`` (``torch.ops.xdot.*``).
+
+Policy: GPU tensors run on the HIP kernels.  If the extension is missing on a machine with
+a GPU, xdot raises (set ``XDOT_ALLOW_TORCH_FALLBACK=1`` to permit the slow torch path, e.g.
+for debugging); CPU tensors always use the torch reference implementations.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+from .utils.env import FLAGS
+
+_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
+_lock = threading.Lock()
+_state = {"loaded": False, "error": None}
+
+
+def lib_path() -> str:
+    return _LIB
+
+
+def load(build_if_missing: bool = False) -> bool:
+    """Load ``_C.so`` once.  Returns True on success."""
+    if _state["loaded"]:
+        return True
+    with _lock:
+        if _state["loaded"]:
+            return True
+        if not os.path.exists(_LIB) and build_if_missing:
+            from . import build as _b
+
+            _b.build()
+        if not os.path.exists(_LIB):
+            _state["error"] = f"{_LIB} not built (run `python -m xdot.build`)"
+            return False
+        try:
+            torch.ops.load_library(_LIB)
+            _state["loaded"] = True
+        except Exception as e:  # noqa: BLE001
+            _state["error"] = f"failed to load {_LIB}: {e}"
+            return False
+    return True
+
+
+def available() -> bool:
+    return load()
+
+
+def use_hip(*tensors: torch.Tensor) -> bool:
+    """Decide whether GPU tensors go to the HIP kernels.  Raises if they should but the
+    extension is not loadable (no silent fallback on a GPU box)."""
+    if not any(isinstance(t, torch.Tensor) and t.is_cuda for t in tensors):
+        return False
+    if FLAGS.backend == "torch":
+        return False
+    if load():
+        return True
+    if FLAGS.allow_torch_fallback:
+        return False
+    raise RuntimeError(f"xdot: HIP extension unavailable for GPU tensors: {_state['error']}")
+
+
+def ops():
+    if not load():
+        raise RuntimeError(f"xdot: HIP extension unavailable: {_state['error']}")
+    return torch.ops.xdot

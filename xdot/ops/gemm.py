@@ -1,0 +1,120 @@
+"""Python face of the generic MFMA GEMM (``csrc/gemm.hip``).
+
+``strided_gemm`` exposes the kernel's full addressing model (2-level batch, K segments,
+either operand k- or mn-contiguous); the helpers below express the three distributed
+products of the reference with it.  Every helper also has a torch reference path used on
+CPU, for dtypes the kernel does not take (float64 / integer) and for testing.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _ext
+
+_HIP_IN = (torch.bfloat16, torch.float16, torch.float32)
+
+
+def hip_dtype_ok(*ts: torch.Tensor) -> bool:
+    return all(t.dtype in _HIP_IN for t in ts) and len({t.dtype for t in ts}) == 1
+
+
+def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0, sA2=0,
+                 sB1=0, sB2=0, sC1=0, sC2=0, sAseg=0, sBseg=0, a_mc=False, b_mc=False,
+                 alpha=1.0) -> None:
+    """C[z1, z2](m, n) = alpha * sum_s sum_k opA(m, k) * opB(k, n)  (see csrc/gemm.hip)."""
+    _ext.ops().gemm(A, B, C, int(M), int(N), int(K), int(nseg), int(nb1), int(nb2), int(lda),
+                    int(ldb), int(ldc), int(sA1), int(sA2), int(sB1), int(sB2), int(sC1), int(sC2),
+                    int(sAseg), int(sBseg), bool(a_mc), bool(b_mc), float(alpha))
+
+
+def _flat(t: torch.Tensor, lead: int) -> torch.Tensor:
+    """contiguous view with the leading ``lead`` dims flattened to one"""
+    t = t.contiguous()
+    return t.view(-1, *t.shape[t.dim() - lead:]) if lead else t
+
+
+# ---------------------------------------------------------------------------------------
+# nt: out[p, :, j*R + c0 : j*R + c0 + c] = alpha * left[p] @ chunk[j, p]^T
+# ---------------------------------------------------------------------------------------
+def nt_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, c0: int,
+                  alpha: float = 1.0) -> None:
+    """``out``: (Pn, R, N*Rr) contiguous; ``left``: (Pn, R, D); ``chunk``: (N, Pn, c, D)."""
+    N, Pn, c, D = chunk.shape
+    R = left.shape[-2]
+    T = out.shape[-1]
+    Rr = T // N  # rows per rank of the gathered operand
+    if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
+        left = left.contiguous()
+        chunk = chunk.contiguous()
+        strided_gemm(left, chunk, out[..., c0:], M=R, N=c, K=D, nb1=N, nb2=Pn,
+                     lda=D, ldb=D, ldc=T, sA1=0, sA2=R * D, sB1=Pn * c * D, sB2=c * D,
+                     sC1=Rr, sC2=R * T, a_mc=False, b_mc=False, alpha=alpha)
+        return
+    part = torch.matmul(left.unsqueeze(0).to(torch.promote_types(left.dtype, chunk.dtype)),
+                        chunk.transpose(-1, -2))                      # (N, Pn, R, c)
+    if alpha != 1.0:
+        part = part * alpha
+    ov = out.view(Pn, R, N, Rr)
+    ov[..., c0:c0 + c] = part.permute(1, 2, 0, 3).to(out.dtype)
+
+
+# ---------------------------------------------------------------------------------------
+# all: out[p, :, d0:d0+c] = sum_j left[p, :, j*R:(j+1)*R] @ chunk[j, p]
+# ---------------------------------------------------------------------------------------
+def all_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, d0: int) -> None:
+    """``out``: (Pn, R, D); ``left``: (Pn, R, T); ``chunk``: (N, Pn, R, c) feature columns."""
+    N, Pn, R, c = chunk.shape
+    T = left.shape[-1]
+    D = out.shape[-1]
+    if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
+        left = left.contiguous()
+        chunk = chunk.contiguous()
+        strided_gemm(left, chunk, out[..., d0:], M=R, N=c, K=R, nseg=N, nb1=1, nb2=Pn,
+                     lda=T, ldb=c, ldc=D, sA2=R * T, sB2=R * c, sC2=R * D,
+                     sAseg=R, sBseg=Pn * R * c, a_mc=False, b_mc=True)
+        return
+    ct = torch.promote_types(left.dtype, chunk.dtype)
+    splits = left.view(Pn, R, N, R).permute(2, 0, 1, 3).to(ct)        # view, no stack copy
+    res = torch.matmul(splits, chunk.to(ct)).sum(0)                   # (Pn, R, c)
+    out[..., d0:d0 + c] = res.to(out.dtype)
+
+
+# ---------------------------------------------------------------------------------------
+# tn: send[j, p] = left[p, :, j*R:(j+1)*R]^T @ right[p]   (reduce-scatter send buffer)
+# ---------------------------------------------------------------------------------------
+def tn_partials_into(send: torch.Tensor, left: torch.Tensor, right: torch.Tensor) -> None:
+    """``send``: (N, Pn, R, D); ``left``: (Pn, R, T); ``right``: (Pn, R, D)."""
+    N, Pn, R, D = send.shape
+    T = left.shape[-1]
+    if _ext.use_hip(send, left, right) and hip_dtype_ok(left, right) and send.dtype in _HIP_IN:
+        left = left.contiguous()
+        right = right.contiguous()
+        strided_gemm(left, right, send, M=R, N=D, K=R, nb1=N, nb2=Pn,
+                     lda=T, ldb=D, ldc=D, sA1=R, sA2=R * T, sB1=0, sB2=R * D,
+                     sC1=Pn * R * D, sC2=R * D, a_mc=True, b_mc=True)
+        return
+    ct = torch.promote_types(left.dtype, right.dtype)
+    blocks = left.view(Pn, R, N, R).permute(2, 0, 3, 1).to(ct)        # (N, Pn, R_col, R_row)
+    send.copy_(torch.matmul(blocks, right.to(ct).unsqueeze(0)).to(send.dtype))
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, *, trans_b: bool = False, alpha: float = 1.0,
+           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Batched ``alpha * a @ op(b)`` on the MFMA kernel (local, non-distributed helper)."""
+    if not (_ext.use_hip(a, b) and hip_dtype_ok(a, b)):
+        r = torch.matmul(a, b.transpose(-1, -2) if trans_b else b)
+        return (r * alpha if alpha != 1.0 else r).to(out_dtype or r.dtype)
+    lead = a.shape[:-2]
+    a3 = _flat(a, 2)
+    b3 = _flat(b, 2)
+    if b3.shape[0] not in (1, a3.shape[0]):
+        raise ValueError("matmul: batch mismatch")
+    Pn, M, K = a3.shape
+    N = b3.shape[-2] if trans_b else b3.shape[-1]
+    out = torch.empty(Pn, M, N, dtype=out_dtype or a.dtype, device=a.device)
+    sb = 0 if b3.shape[0] == 1 else b3.shape[-1] * b3.shape[-2]
+    strided_gemm(a3, b3, out, M=M, N=N, K=K, nb2=Pn, lda=K, ldb=b3.shape[-1], ldc=N,
+                 sA2=M * K, sB2=sb, sC2=M * N, a_mc=False, b_mc=not trans_b, alpha=alpha)
+    return out.view(*lead, M, N)

@@ -1,0 +1,211 @@
+"""Sequence-parallel distributed products (time axis sharded into contiguous T/N row blocks).
+
+Rank ``r`` holds global rows ``[r*R, (r+1)*R)`` (``R = T/N``, equal on all ranks) of every
+sequence tensor; arbitrary identical leading dims ``P`` are allowed.  Contract (SURVEY §2.5,
+reference ``distributed_dot_product/multiplication/functions.py``):
+
+==============================  ==============  ==========  ===================================
+function                        local inputs    local out   global math (row block ``r``)
+==============================  ==============  ==========  ===================================
+``distributed_matmul_nt``       (P,R,D),(P,R,D)  (P,R,T)     L·Rᵀ, column ``j*R+i`` = rank j row i
+``distributed_matmul_all``      (P,R,T),(P,R,D)  (P,R,D)     L·R
+``distributed_matmul_tn``       (P,R,T),(P,R,D)  (P,R,D)     Lᵀ·R
+``distributed_matmul_block``    (P,R,K),(P,K,M)  (P,R,M)     Σ_ranks L_r·R_r  (Sum all-reduce)
+==============================  ==============  ==========  ===================================
+
+MI355X design, per op:
+
+* ``nt`` (reference :45-99): RCCL all-gather of ``right`` (whole shard by default, or
+  ``offset``-row chunks, double-buffered), then ONE batched MFMA GEMM per chunk over
+  (source rank, P) that writes straight into the final (P, R, T) layout — no ``(N,P,R,R)``
+  staging buffer and no permute copy (reference K3/K4).  Optional ``alpha`` fuses the
+  attention scale into the epilogue.
+* ``all`` (reference :161-212): all-gather ``right`` (feature-column chunks if ``offset``),
+  then one GEMM whose K loop walks the N source-rank column blocks of ``left`` in place — the
+  reference's full ``torch.stack`` copy of ``left`` (7.5 GB at T=75000) and the trailing
+  ``sum(dim=0)`` are gone; ``left`` is read once per chunk.
+* ``tn`` (reference :103-148): one batched GEMM producing all N partial blocks
+  ``left[:, jR:(j+1)R]ᵀ·right`` into a contiguous send buffer (``left`` read transposed in
+  place by the kernel's LDS transpose read), then ONE ``reduce_scatter`` — half the bytes and
+  1/N the collective launches of the reference's N full all-reduces (with N-1 leaked
+  handles).  Half-precision partials are reduced in fp32.
+* No host barrier before each op (reference calls ``MPI.Barrier`` each time).
+
+Output dtype = input dtype (the reference hard-codes fp32 via ``torch.empty`` without dtype
+and therefore crashes in bf16); pass ``out_dtype=torch.float32`` for reference-identical fp32
+outputs.  GPU tensors run on the HIP kernels; CPU tensors on torch.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops import gemm as G
+from ..utils import comm as _comm
+from ..utils.checks import check_consistent
+from ..utils.profiling import measure
+from .schedule import Offset, gather_pipeline, plan_chunks, resolve_offset
+
+__all__ = ["distributed_matmul_nt", "distributed_matmul_all", "distributed_matmul_tn",
+           "distributed_matmul_block", "gather_sequence"]
+
+
+def _prep(left: torch.Tensor, right: torch.Tensor, name: str):
+    if left.shape[:-2] != right.shape[:-2]:
+        raise ValueError(f"{name}: leading dims differ: {tuple(left.shape)} vs {tuple(right.shape)}")
+    if left.device != right.device:
+        raise ValueError(f"{name}: operands on different devices")
+
+
+def _result_dtype(left, right, out_dtype):
+    return out_dtype if out_dtype is not None else torch.promote_types(left.dtype, right.dtype)
+
+
+@measure
+def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offset = None, *,
+                          comm: Optional[_comm.Communicator] = None, alpha: float = 1.0,
+                          out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Row block ``r`` of ``L·Rᵀ``: (P, R, D) x (P, R, D) -> (P, R, T).
+
+    ``offset``: rows of ``right`` gathered per step (``None``: whole shard; ``'auto'``:
+    sized from free HBM).  Reference: ``functions.py:45-99``.
+    """
+    _prep(left, right, "distributed_matmul_nt")
+    if left.shape[-1] != right.shape[-1]:
+        raise ValueError("distributed_matmul_nt: feature dims differ")
+    comm = comm or _comm.get_comm()
+    n = comm.world_size
+    P = tuple(left.shape[:-2])
+    R, D = left.shape[-2], left.shape[-1]
+    Rr = right.shape[-2]
+    Pn = 1
+    for d in P:
+        Pn *= d
+    T = Rr * n
+    off = resolve_offset(offset, Rr, n * Pn * D * right.element_size(), right.device)
+    chunks = plan_chunks(Rr, off)
+    check_consistent(comm, "nt", left, right, tuple(chunks))
+    out = torch.empty((Pn, R, T), dtype=_result_dtype(left, right, out_dtype), device=left.device)
+    if R == 0 or T == 0:
+        return out.view(*P, R, T)
+    l3 = left.reshape(Pn, R, D)
+    r3 = right.reshape(Pn, Rr, D)
+
+    def consume(s, e, gathered):  # gathered: (N, Pn, c, D)
+        G.nt_chunk_into(out, l3, gathered, s, alpha)
+
+    gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
+                    right.device, consume)
+    return out.view(*P, R, T)
+
+
+@measure
+def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offset = None, *,
+                           comm: Optional[_comm.Communicator] = None,
+                           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Row block ``r`` of ``L·R``: (P, R, T) x (P, R, D) -> (P, R, D).
+
+    ``offset``: feature columns of ``right`` gathered per step.  Reference: ``functions.py:161-212``.
+    """
+    _prep(left, right, "distributed_matmul_all")
+    comm = comm or _comm.get_comm()
+    n = comm.world_size
+    P = tuple(left.shape[:-2])
+    R, T = left.shape[-2], left.shape[-1]
+    Rr, D = right.shape[-2], right.shape[-1]
+    if T != Rr * n:
+        raise ValueError(f"distributed_matmul_all: left has {T} columns, expected {Rr} x {n}")
+    Pn = 1
+    for d in P:
+        Pn *= d
+    off = resolve_offset(offset, D, n * Pn * Rr * right.element_size(), right.device)
+    chunks = plan_chunks(D, off)
+    check_consistent(comm, "all", left, right, tuple(chunks))
+    out = torch.empty((Pn, R, D), dtype=_result_dtype(left, right, out_dtype), device=left.device)
+    if R == 0 or D == 0:
+        return out.view(*P, R, D)
+    if T == 0:
+        return out.zero_().view(*P, R, D)
+    l3 = left.reshape(Pn, R, T)
+    r3 = right.reshape(Pn, Rr, D)
+
+    def consume(s, e, gathered):  # (N, Pn, Rr, c)
+        G.all_chunk_into(out, l3, gathered, s)
+
+    gather_pipeline(comm, chunks, lambda s, e: r3[..., s:e], lambda c: (Pn, Rr, c), right.dtype,
+                    right.device, consume)
+    return out.view(*P, R, D)
+
+
+@measure
+def distributed_matmul_tn(left: torch.Tensor, right: torch.Tensor, *,
+                          comm: Optional[_comm.Communicator] = None,
+                          out_dtype: Optional[torch.dtype] = None,
+                          reduce_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Row block ``r`` of ``Lᵀ·R``: (P, R, T) x (P, R, D) -> (P, R, D).
+
+    One batched GEMM into an (N, P, R, D) send buffer + one reduce-scatter.
+    Reference: ``functions.py:103-148``.
+    """
+    _prep(left, right, "distributed_matmul_tn")
+    comm = comm or _comm.get_comm()
+    n = comm.world_size
+    P = tuple(left.shape[:-2])
+    R, T = left.shape[-2], left.shape[-1]
+    D = right.shape[-1]
+    if right.shape[-2] != R:
+        raise ValueError("distributed_matmul_tn: left/right row counts differ")
+    if T % n != 0:
+        raise ValueError(f"distributed_matmul_tn: {T} columns not divisible by world size {n}")
+    Rc = T // n
+    if Rc != R:
+        raise ValueError("distributed_matmul_tn: column block size must equal the local row count")
+    Pn = 1
+    for d in P:
+        Pn *= d
+    check_consistent(comm, "tn", left, right)
+    res_dt = _result_dtype(left, right, out_dtype)
+    if reduce_dtype is None:
+        reduce_dtype = torch.float32 if res_dt in (torch.bfloat16, torch.float16) and n > 1 else res_dt
+    send = torch.empty((n, Pn, Rc, D), dtype=reduce_dtype, device=left.device)
+    if R > 0 and D > 0:
+        G.tn_partials_into(send, left.reshape(Pn, R, T), right.reshape(Pn, R, D))
+    else:
+        send.zero_()
+    if n == 1:
+        out = send[0]
+    else:
+        out = torch.empty((Pn, Rc, D), dtype=reduce_dtype, device=left.device)
+        comm.reduce_scatter(out, send)
+    return out.to(res_dt).view(*P, Rc, D)
+
+
+@measure
+def distributed_matmul_block(left: torch.Tensor, right: torch.Tensor, transpose: bool = False, *,
+                             comm: Optional[_comm.Communicator] = None) -> torch.Tensor:
+    """``Σ_ranks left_r @ right_r`` (optionally transposed), Sum all-reduced.
+
+    The reference's helper (``functions.py:151-157``) is dead code with two bugs — a
+    ``.tranpose`` typo and Horovod's default *Average* op — this is the intended operation.
+    """
+    comm = comm or _comm.get_comm()
+    block = G.matmul(left, right)
+    if transpose:
+        block = block.transpose(-1, -2).contiguous()
+    comm.all_reduce(block, op="sum")
+    return block
+
+
+def gather_sequence(x: torch.Tensor, dim: int = -2, *, comm: Optional[_comm.Communicator] = None) -> torch.Tensor:
+    """All-gather a sequence-sharded tensor along ``dim`` (rank-major), e.g. for inspection."""
+    comm = comm or _comm.get_comm()
+    n = comm.world_size
+    if n == 1:
+        return x
+    dim = dim % x.dim()
+    xm = x.movedim(dim, 0).contiguous()
+    out = torch.empty((n,) + tuple(xm.shape), dtype=x.dtype, device=x.device)
+    comm.all_gather_into(out, xm)
+    out = out.reshape((n * xm.shape[0],) + tuple(xm.shape[1:]))
+    return out.movedim(0, dim)

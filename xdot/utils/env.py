@@ -1,0 +1,40 @@
+"""Runtime flags (environment variables), read once at import and overridable in code.
+
+=============================  ==========================================================
+``XDOT_DEBUG`` / ``DISTRIBUTED_DOT_DEBUG``  print per-op shapes, HBM delta and synced time
+                                           (reference alias: ``functions.py:21``)
+``XDOT_CHECK``                 all-gather an op fingerprint before every distributed op
+                               and raise on rank divergence (instead of hanging)
+``XDOT_BACKEND``               ``auto`` | ``hip`` | ``torch``: compute backend for GPU tensors
+``XDOT_ALLOW_TORCH_FALLBACK``  ``1`` lets GPU ops fall back to torch when ``_C.so`` is absent
+                               (default: fail loudly)
+``XDOT_COMM_TIMEOUT_S``        collective timeout in seconds (default 600)
+``XDOT_CHUNK_BUDGET_MB``       transient-buffer budget used by the chunk planner
+=============================  ==========================================================
+"""
+from __future__ import annotations
+
+import os
+
+
+def _flag(*names: str, default: str = "0") -> bool:
+    for n in names:
+        v = os.environ.get(n)
+        if v is not None:
+            return v.strip().lower() not in ("", "0", "false", "no", "off")
+    return default not in ("0", "")
+
+
+class _Flags:
+    def __init__(self):
+        self.reload()
+
+    def reload(self):
+        self.debug = _flag("XDOT_DEBUG", "DISTRIBUTED_DOT_DEBUG")
+        self.check = _flag("XDOT_CHECK")
+        self.backend = os.environ.get("XDOT_BACKEND", "auto").lower()
+        self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
+        self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
+
+
+FLAGS = _Flags()
