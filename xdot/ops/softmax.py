@@ -58,7 +58,8 @@ def scale_mask_softmax_fwd(scores: torch.Tensor, mask: Optional[torch.Tensor], s
 def scale_mask_softmax_bwd(y: torch.Tensor, dy: torch.Tensor, scale: float) -> torch.Tensor:
     if _ext.use_hip(y) and y.dtype in (torch.float32, torch.bfloat16, torch.float16):
         return _ext.ops().softmax_bwd(y.contiguous(), dy.contiguous().to(y.dtype), float(scale))
-    yf, dyf = y.float(), dy.float()
+    cdt = torch.float64 if y.dtype == torch.float64 else torch.float32
+    yf, dyf = y.to(cdt), dy.to(cdt)
     return (scale * yf * (dyf - (dyf * yf).sum(-1, keepdim=True))).to(y.dtype)
 
 

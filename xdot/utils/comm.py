@@ -286,8 +286,8 @@ class ThreadComm(Communicator):
     def reduce_scatter(self, out, inp, async_op=False):
         parts = self._exchange(inp.contiguous())
         n = out.numel()
-        acc = torch.zeros(n, dtype=torch.float64 if not out.is_floating_point() else torch.float32,
-                          device=out.device)
+        acc_dt = torch.float32 if out.dtype in (torch.bfloat16, torch.float16) else out.dtype
+        acc = torch.zeros(n, dtype=acc_dt, device=out.device)
         for p in parts:
             acc += p.reshape(-1)[self.rank * n:(self.rank + 1) * n].to(acc.dtype)
         out.view(-1).copy_(acc) if out.is_contiguous() else out.copy_(acc.view(out.shape))
