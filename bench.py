@@ -1,0 +1,157 @@
+"""Headline benchmark: DistributedDotProductAttn training step, T=25000, d=768, h=8.
+
+Metric (BASELINE.json): ``ms/fwd+bwd DistributedDotProductAttn T=25000 d=768 h=8; scaling
+1/2/4/8 GPU``.  One step = forward + backward of the module on this rank's T/N rows
+(global T fixed => strong scaling), MSE loss as in the reference ``example.py``, the
+sequence-parallel Sum all-reduce of the replicated parameter gradients and an AdamW step.
+Synthetic random inputs, random-init weights, bf16 compute, the reference's all-False
+boolean mask (``example.py:29``) is passed and honoured.
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+Rank 0 prints one JSON line.  ``value`` = wall ms per step, max over ranks (the job's step
+time); the timed region is bracketed by a barrier and ``torch.cuda.synchronize()``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "ms/fwd+bwd DistributedDotProductAttn T=25000 d=768 h=8; scaling 1/2/4/8 GPU"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seq-len", type=int, default=25000, help="global T")
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--heads", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--impl", default="auto", choices=["auto", "flash", "materialized"])
+    ap.add_argument("--offset", type=int, default=None)
+    ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random"])
+    ap.add_argument("--no-optim", action="store_true", help="(diagnostic) skip the optimizer step")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import xdot
+    from xdot.utils import comm as C
+    from xdot.parallel import GradSync
+
+    comm = C.init("auto")
+    n, rank = comm.world_size, comm.rank
+    if n != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but world size {n}", file=sys.stderr)
+    dev = torch.device(a.device, C.get_local_rank() % max(1, torch.cuda.device_count())) if a.device == "cuda" \
+        else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    T = a.seq_len
+    if T % n:
+        raise SystemExit(f"seq-len {T} not divisible by world size {n}")
+    R = T // n
+
+    torch.manual_seed(1234)  # identical weights on every rank
+    model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl).to(dev, dt)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
+    sync = GradSync(model, comm=comm)
+    crit = torch.nn.MSELoss()
+
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.rand(a.batch, R, a.dim, device=dev, dtype=dt, generator=g)
+    y = torch.rand(a.batch, R, a.dim, device=dev, dtype=dt, generator=g)
+    if a.mask == "none":
+        mask = None
+    elif a.mask == "zeros":
+        mask = torch.zeros(a.batch, R, T, dtype=torch.bool, device=dev)
+    else:
+        mask = torch.rand(a.batch, R, T, device=dev, generator=g) < 0.1
+        mask[..., 0] = False
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = model(x, x, x, mask)
+        loss = crit(out, y)
+        loss.backward()
+        sync.wait()
+        if not a.no_optim:
+            opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    impl = model._pick_impl(x)
+
+    def sync_all():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    prof = None
+    if a.profile_dir and rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync_all()
+    t1 = time.perf_counter()
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
+        with open(os.path.join(a.profile_dir, "ops.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+
+    ms = (t1 - t0) * 1e3 / max(1, a.steps)
+    t = torch.tensor([ms], dtype=torch.float64, device=dev if comm.backend == "nccl" else "cpu")
+    comm.all_reduce(t, op="max")
+    ms = float(t.item())
+    lossv = float(loss.float().item())
+    if not math.isfinite(lossv):
+        raise SystemExit(f"non-finite loss {lossv}")
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(ms, 4),
+            "unit": "ms",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (random inputs, random-init weights)",
+            "config": {"model": f"DistributedDotProductAttn(d={a.dim},h={a.heads})", "global_batch": a.batch,
+                       "seq_len": T, "parallelism": f"sp{n}", "impl": impl, "mask": a.mask,
+                       "step": "fwd+bwd+grad-allreduce+AdamW" if not a.no_optim else "fwd+bwd+grad-allreduce"},
+            "tokens_per_s": round(a.batch * T / (ms / 1e3), 1),
+            "loss": lossv,
+        }
+        print(json.dumps(rec), flush=True)
+    C.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -131,6 +131,100 @@ at::Tensor softmax_bwd(const at::Tensor& y, const at::Tensor& dy, double scale) 
   return dx;
 }
 
+// ------------------------------------------------------------------------------------
+std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kBool && mask.dim() == 3, "xdot.mask_pack: (B, R, T) bool GPU mask");
+  auto m = mask.contiguous();
+  const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
+  const int64_t NKT = (T + 63) / 64;
+  auto bits = at::empty({B, R, NKT}, m.options().dtype(at::kLong));
+  auto flags = at::empty({B, (R + 31) / 32, NKT}, m.options().dtype(at::kByte));
+  TORCH_CHECK(B * R * NKT < (1LL << 40) && T < (1LL << 31), "xdot.mask_pack: too large");
+  c10::DeviceGuard guard(m.device());
+  xdot_mask_pack_launch(reinterpret_cast<const uint8_t*>(m.data_ptr()), reinterpret_cast<uint64_t*>(bits.data_ptr()),
+                        flags.data_ptr<uint8_t>(), (int)B, (int)R, (int)T, cur_stream(m));
+  check_launch(hipGetLastError(), "mask_pack");
+  return {bits, flags};
+}
+
+struct FlashGeom {
+  int64_t B, R, C, N, Rc, T, D;
+};
+
+FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc, int64_t H,
+                      const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags) {
+  TORCH_CHECK(rows.is_cuda() && kc.is_cuda() && vc.is_cuda(), "xdot.flash: GPU tensors required");
+  TORCH_CHECK(rows.is_contiguous() && kc.is_contiguous() && vc.is_contiguous(), "xdot.flash: contiguous tensors required");
+  TORCH_CHECK(rows.scalar_type() == kc.scalar_type() && rows.scalar_type() == vc.scalar_type(), "xdot.flash: dtype mismatch");
+  TORCH_CHECK(rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kHalf, "xdot.flash: bf16/fp16 only");
+  TORCH_CHECK(rows.dim() == 3 && kc.dim() == 4 && vc.sizes() == kc.sizes(), "xdot.flash: rows (B,R,C), cols (N,B,Rc,C)");
+  FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(0), kc.size(2), 0, 0};
+  TORCH_CHECK(kc.size(1) == g.B && kc.size(3) == g.C, "xdot.flash: batch / feature mismatch");
+  TORCH_CHECK(H > 0 && g.C % H == 0, "xdot.flash: C not divisible by heads");
+  g.D = g.C / H;
+  TORCH_CHECK(g.D == 32 || g.D == 64 || g.D == 96 || g.D == 128, "xdot.flash: head dim must be 32/64/96/128");
+  g.T = g.N * g.Rc;
+  TORCH_CHECK(g.T < (1LL << 31) && g.R < (1LL << 31) && g.B * H * ((g.R + 127) / 128) < (1LL << 31), "xdot.flash: too large");
+  TORCH_CHECK(aligned16(rows.data_ptr()) && aligned16(kc.data_ptr()) && aligned16(vc.data_ptr()), "xdot.flash: 16-byte alignment");
+  const bool hb = bits.has_value() && bits->defined(), hf = flags.has_value() && flags->defined();
+  TORCH_CHECK(hb == hf, "xdot.flash: mask bits and flags go together");
+  if (hb) {
+    const int64_t NKT = (g.T + 63) / 64;
+    TORCH_CHECK(bits->is_contiguous() && bits->numel() == g.B * g.R * NKT, "xdot.flash: mask bits shape");
+    TORCH_CHECK(flags->is_contiguous() && flags->numel() == g.B * ((g.R + 31) / 32) * NKT, "xdot.flash: mask flags shape");
+  }
+  return g;
+}
+
+std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
+                                             const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
+                                             int64_t H, double scale) {
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  auto out = at::empty_like(rows);
+  auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  xdot::fa::FwdArgs a{};
+  a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.out = out.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  const bool hb = bits.has_value() && bits->defined();
+  a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
+  a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
+  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.Rc = (int)g.Rc;
+  a.cs = g.B * g.Rc * g.C; a.bs = g.Rc * g.C; a.scale = (float)scale;
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0, "xdot.flash_fwd: config");
+  check_launch(hipGetLastError(), "flash_fwd");
+  return {out, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc,
+                                                         const at::Tensor& vc, const at::Tensor& out, const at::Tensor& lse,
+                                                         const c10::optional<at::Tensor>& bits,
+                                                         const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  TORCH_CHECK(dout.sizes() == rows.sizes() && out.sizes() == rows.sizes() && dout.is_contiguous() && out.is_contiguous(),
+              "xdot.flash_bwd: dout/out shape");
+  TORCH_CHECK(dout.scalar_type() == rows.scalar_type() && out.scalar_type() == rows.scalar_type(), "xdot.flash_bwd: dtype");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat && lse.numel() == g.B * H * g.R, "xdot.flash_bwd: lse");
+  auto drows = at::empty_like(rows);
+  auto dkc = at::empty(kc.sizes(), kc.options().dtype(at::kFloat));
+  auto dvc = at::empty(vc.sizes(), vc.options().dtype(at::kFloat));
+  auto delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  xdot::fa::BwdArgs a{};
+  a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.dout = dout.data_ptr();
+  a.lse = lse.data_ptr<float>(); a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
+  a.dkc = dkc.data_ptr<float>(); a.dvc = dvc.data_ptr<float>();
+  const bool hb = bits.has_value() && bits->defined();
+  a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
+  a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
+  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.Rc = (int)g.Rc;
+  a.cs = g.B * g.Rc * g.C; a.bs = g.Rc * g.C; a.scale = (float)scale;
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_bwd_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(rows.scalar_type()), (int)g.D,
+                                    cur_stream(rows)) == 0, "xdot.flash_bwd: config");
+  check_launch(hipGetLastError(), "flash_bwd");
+  return {drows, dkc, dvc};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(xdot, m) {
@@ -139,10 +233,17 @@ TORCH_LIBRARY(xdot, m) {
         "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha) -> ()");
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
+  m.def("mask_pack(Tensor mask) -> (Tensor, Tensor)");
+  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale) -> (Tensor, Tensor)");
+  m.def("flash_bwd(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, Tensor? flags, "
+        "int H, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("softmax_fwd", &softmax_fwd);
   m.impl("softmax_bwd", &softmax_bwd);
+  m.impl("mask_pack", &mask_pack);
+  m.impl("flash_fwd", &flash_fwd);
+  m.impl("flash_bwd", &flash_bwd);
 }

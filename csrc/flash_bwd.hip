@@ -1,0 +1,391 @@
+// xdot — sequence-parallel flash-attention BACKWARD for gfx950 (MI355X).
+//
+// Reference backward of the module (distributed_dot_product/multiplication/ops.py:29-37 and
+// :49-54, driven by module.py:60-71): 2x distributed_matmul_nt + 2x distributed_matmul_tn +
+// 1x distributed_matmul_all + ATen softmax/masked_fill/div backward, each a full pass over a
+// materialised (B, H, R, T) tensor and each re-gathering K/V over the network.
+//
+// Here the probabilities are recomputed per tile from the forward's LSE and three kernels
+// run back to back, no score-sized tensor ever exists:
+//   flash_bwd_prep  δ[row] = Σ_d dO·O                                   (memory-bound, tiny)
+//   flash_bwd_rows  per 128 local rows: sweep all T gathered columns,
+//                   Sᵀ, dPᵀ by MFMA, dSᵀ = Pᵀ ⊙ (dPᵀ − δ), dK += dS · Q_cols
+//                   -> grad of the row side (this rank's `keys`), no atomics
+//   flash_bwd_cols  per 128 gathered columns: sweep all R local rows,
+//                   S, dP by MFMA, P, dS, dV_cols += Pᵀ · dO, dQ_cols += dSᵀ · K_rows
+//                   -> fp32 partials for ALL T columns in the gathered (rank-major)
+//                   layout, which the host reduce-scatters over RCCL (the `tn` pattern).
+// Splitting the row-side and column-side sums into two kernels costs two extra MFMA
+// products (S and dP are recomputed once more) but removes every cross-workgroup float
+// atomic: with 256-column blocks those would move ≈7.5 GB of atomic traffic per step at
+// T=25000 — ≈5.8 ms at MI355X's ≈1.3 TB/s atomic rate, more than the MFMA work they save.
+// Accumulator-as-operand orientation (see flash_fwd.hip): each product is arranged so the
+// following MFMA sums over the accumulator's ROW index, so P and dS feed the next MFMA as
+// packed registers; the one operand that must be transposed is read with ds_read_b64_tr_b16.
+#include "flash_common.h"
+
+namespace xdot {
+namespace fa {
+
+// ---------------------------------------------------------------------------------------
+// δ = rowsum(dO ⊙ O) per (b, h, row); one thread per (b, row, h)
+template <int DT, int D>
+__global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const void* out_, float* delta) {
+  using T16 = typename dt_traits<DT>::T;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.R * a.H;
+  if (idx >= total) return;
+  const int h = (int)(idx % a.H);
+  const int64_t br = idx / a.H;
+  const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int64_t off = br * (a.H * D) + h * D;
+  const T16* o = reinterpret_cast<const T16*>(out_) + off;
+  const T16* d = reinterpret_cast<const T16*>(a.dout) + off;
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    union { u32x4 u; T16 e[8]; } x, y;
+    x.u = *reinterpret_cast<const u32x4*>(o + 8 * c);
+    y.u = *reinterpret_cast<const u32x4*>(d + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += (float)x.e[e] * (float)y.e[e];
+  }
+  delta[((int64_t)b * a.H + h) * a.R + row] = acc;
+}
+
+// ---------------------------------------------------------------------------------------
+// grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols.
+template <int DT, int D>
+__global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  constexpr int ROWB = Geo<D>::ROWB;
+  constexpr int QS_BYTES = 64 * ROWB, STAGE = 2 * QS_BYTES;
+  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bh = lin / nrb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT = (a.T + 63) / 64;
+  const int r0 = rb * 128 + wave * 32;
+  const int row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+
+  const T16* kc = reinterpret_cast<const T16*>(a.kc) + h * D;
+  const T16* vc = reinterpret_cast<const T16*>(a.vc) + h * D;
+  u32x4 kf[KS], df[KS];
+  {
+    const int64_t off = ((int64_t)b * a.R + row) * C + h * D + 8 * hf;
+    const T16* pk = reinterpret_cast<const T16*>(a.rows) + off;
+    const T16* pd = reinterpret_cast<const T16*>(a.dout) + off;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      kf[s] = row_ok ? *reinterpret_cast<const u32x4*>(pk + 16 * s) : u32x4{0, 0, 0, 0};
+      df[s] = row_ok ? *reinterpret_cast<const u32x4*>(pd + 16 * s) : u32x4{0, 0, 0, 0};
+    }
+  }
+  const int64_t lrow = ((int64_t)b * a.H + h) * a.R + (row_ok ? row : 0);
+  const float lse2 = row_ok ? a.lse[lrow] * LOG2E : 0.f;
+  const float dlt = row_ok ? a.delta[lrow] : 0.f;
+  const float c2 = a.scale * LOG2E;
+  const float NEG_INF = -__builtin_inff();
+
+  u32x4 rq[LPT], rv[LPT];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = kt * 64 + r;
+      if (t < a.T) {
+        const int64_t off = col_off(t, b, a.Rc, a.cs, a.bs, C) + c * 8;
+        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+      } else {
+        rq[i] = u32x4{0, 0, 0, 0};
+        rv[i] = u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* qs = smem + buf * STAGE;
+    char* vs = qs + QS_BYTES;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
+      *reinterpret_cast<u32x4*>(qs + r * ROWB + c * 16) = rq[i];
+      *reinterpret_cast<u32x4*>(vs + r * ROWB + c * 16) = rv[i];
+    }
+  };
+
+  f32x16 dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
+  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
+  const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < NKT) load_tile(kt + 1);
+    const char* qs = smem + cur * STAGE;
+    const char* vs = qs + QS_BYTES;
+    const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
+    const bool tail = (kt + 1) * 64 > a.T;
+    if (flag != 1 && r0 < a.R) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[tt][r] = 0.f; dp[tt][r] = 0.f; }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s[tt] = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s[tt]);
+          dp[tt] = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, ks, lane), df[ks], dp[tt]);
+        }
+      }
+      const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
+      const bool chk = flag == 2 || tail;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float x = s[tt][r] * c2 - lse2;
+          if (chk) {
+            const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) x = NEG_INF;
+          }
+          const float p = exp2f(x);
+          s[tt][r] = p * (dp[tt][r] - dlt);  // dSᵀ (unscaled)
+        }
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(s[k4 >> 1], k4 & 1), dk[db]);
+    }
+    if (kt + 1 < NKT) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  if (row_ok) {
+    T16* op = reinterpret_cast<T16*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 wv;
+        wv[0] = pack2<DT>(dk[db][4 * g + 0] * a.scale, dk[db][4 * g + 1] * a.scale);
+        wv[1] = pack2<DT>(dk[db][4 * g + 2] * a.scale, dk[db][4 * g + 3] * a.scale);
+        *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = wv;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// grads of the gathered side.  4 waves x 32 columns; 64-row tiles of K_rows / dO.
+template <int DT, int D>
+__global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  constexpr int ROWB = Geo<D>::ROWB;
+  constexpr int IMG = 64 * ROWB;
+  constexpr int STAGE = 2 * IMG + 64 * 4 * 2 + 64 * 8 * 2;  // K, dO, lse2[64], delta[64], words[2][64]
+  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int ncb = (a.T + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = lin % ncb, bh = lin / ncb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT = (a.T + 63) / 64;
+  const int NRB32 = (a.R + 31) / 32;
+  const int c0 = cb * 128 + wave * 32;
+  const int col = c0 + (lane & 31);
+  const bool col_ok = col < a.T;
+  const int kt_w = c0 >> 6;           // this wave's 64-column mask tile
+  const int bit0 = c0 & 63;
+
+  u32x4 qf[KS], vf[KS];
+  {
+    const int64_t off = col_off(col_ok ? col : 0, b, a.Rc, a.cs, a.bs, C) + h * D + 8 * hf;
+    const T16* pq = reinterpret_cast<const T16*>(a.kc) + off;
+    const T16* pv = reinterpret_cast<const T16*>(a.vc) + off;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[s] = col_ok ? *reinterpret_cast<const u32x4*>(pq + 16 * s) : u32x4{0, 0, 0, 0};
+      vf[s] = col_ok ? *reinterpret_cast<const u32x4*>(pv + 16 * s) : u32x4{0, 0, 0, 0};
+    }
+  }
+  const T16* rows = reinterpret_cast<const T16*>(a.rows) + h * D;
+  const T16* dout = reinterpret_cast<const T16*>(a.dout) + h * D;
+  const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;
+  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
+  const float c2 = a.scale * LOG2E;
+  const float NEG_INF = -__builtin_inff();
+  const int NRT = (a.R + 63) / 64;
+  const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
+
+  u32x4 rk[LPT], rd[LPT];
+  float sl = 0.f, sd = 0.f;
+  uint64_t sw = 0;
+  auto load_tile = [&](int rt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = rt * 64 + r;
+      if (rr < a.R) {
+        const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
+        rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
+        rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
+      } else {
+        rk[i] = u32x4{0, 0, 0, 0};
+        rd[i] = u32x4{0, 0, 0, 0};
+      }
+    }
+    if (tid < 64) {
+      const int rr = rt * 64 + tid;
+      // rows past R: lse = +inf makes P = 0 for them
+      sl = rr < a.R ? lse[rr] * LOG2E : __builtin_inff();
+      sd = rr < a.R ? dlt[rr] : 0.f;
+    } else if (tid < 192 && a.mbits) {
+      const int r = (tid - 64) & 63, k = (tid - 64) >> 6, rr = rt * 64 + r;
+      sw = (rr < a.R && kt0 + k < NKT) ? a.mbits[((int64_t)b * a.R + rr) * NKT + kt0 + k] : 0ull;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* ks = smem + buf * STAGE;
+    char* ds = ks + IMG;
+    float* ls = reinterpret_cast<float*>(ds + IMG);
+    float* dls = ls + 64;
+    uint64_t* ws = reinterpret_cast<uint64_t*>(dls + 64);
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
+      *reinterpret_cast<u32x4*>(ks + r * ROWB + c * 16) = rk[i];
+      *reinterpret_cast<u32x4*>(ds + r * ROWB + c * 16) = rd[i];
+    }
+    if (tid < 64) {
+      ls[tid] = sl;
+      dls[tid] = sd;
+    } else if (tid < 192 && a.mbits) {
+      ws[tid - 64] = sw;
+    }
+  };
+
+  f32x16 dq[DB], dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dq[i][r] = 0.f; dv[i][r] = 0.f; }
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int rt = 0; rt < NRT; ++rt) {
+    const int cur = rt & 1;
+    if (rt + 1 < NRT) load_tile(rt + 1);
+    const char* ks = smem + cur * STAGE;
+    const char* ds = ks + IMG;
+    const float* ls = reinterpret_cast<const float*>(ds + IMG);
+    const float* dls = ls + 64;
+    const uint64_t* ws = reinterpret_cast<const uint64_t*>(dls + 64);
+    int flag = 0;
+    if (a.mflags && c0 < a.T) {
+      const uint8_t* fl = a.mflags + (int64_t)b * NRB32 * NKT;
+      const int f0 = fl[(int64_t)(2 * rt) * NKT + kt_w];
+      const int f1 = (2 * rt + 1 < NRB32) ? fl[(int64_t)(2 * rt + 1) * NKT + kt_w] : 1;
+      flag = (f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2);
+    }
+    if (flag != 1 && c0 < a.T) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[tt][r] = 0.f; dp[tt][r] = 0.f; }
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          s[tt] = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, kk, lane), qf[kk], s[tt]);
+          dp[tt] = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, kk, lane), vf[kk], dp[tt]);
+        }
+      }
+      // P and dS; rows of register r: tt*32 + (r&3) + 8*(r>>2) + 4*hf
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int rbase = tt * 32 + 8 * g + 4 * hf;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + rbase);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            float x = s[tt][r] * c2 - l4[e];
+            if (flag == 2) {
+              const uint64_t wv = ws[(kt_w - kt0) * 64 + rbase + e];
+              if ((wv >> (bit0 + (lane & 31))) & 1ull) x = NEG_INF;
+            }
+            const float p = exp2f(x);
+            s[tt][r] = p;
+            dp[tt][r] = p * (dp[tt][r] - d4[e]);
+          }
+        }
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(s[k4 >> 1], k4 & 1), dv[db]);
+          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(dp[k4 >> 1], k4 & 1), dq[db]);
+        }
+    }
+    if (rt + 1 < NRT) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  if (col_ok) {
+    const int64_t off = col_off(col, b, a.Rc, a.cs, a.bs, C) + h * D;
+    float* pq = a.dkc + off;
+    float* pv = a.dvc + off;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 q4 = {dq[db][4 * g] * a.scale, dq[db][4 * g + 1] * a.scale, dq[db][4 * g + 2] * a.scale, dq[db][4 * g + 3] * a.scale};
+        f32x4 v4 = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+        *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) = q4;
+        *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) = v4;
+      }
+  }
+}
+
+template <int DT, int D>
+static void launch_bwd(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
+  const int64_t n0 = (int64_t)a.B * a.R * a.H;
+  hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
+  BwdArgs a2 = a;
+  a2.delta = delta;
+  constexpr int ROWB = Geo<D>::ROWB;
+  const int nrb = (a.R + 127) / 128;
+  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H), dim3(256), 2 * (2 * 64 * ROWB), st, a2);
+  const int ncb = (a.T + 127) / 128;
+  constexpr int STAGE = 2 * 64 * ROWB + 64 * 4 * 2 + 64 * 8 * 2;
+  hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a2);
+}
+
+}  // namespace fa
+}  // namespace xdot
+
+extern "C" int xdot_flash_bwd_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
+                                     hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+#define XB(DTV, DV) if (dt == DTV && D == DV) { launch_bwd<DTV, DV>(*a, out, delta, st); return 0; }
+  XB(DT_BF16, 32) XB(DT_BF16, 64) XB(DT_BF16, 96) XB(DT_BF16, 128)
+  XB(DT_F16, 32) XB(DT_F16, 64) XB(DT_F16, 96) XB(DT_F16, 128)
+#undef XB
+  return -1;
+}

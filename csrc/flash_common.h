@@ -1,0 +1,95 @@
+// xdot — shared pieces of the gfx950 flash-attention kernels (fwd + bwd).
+//
+// Conventions (see csrc/flash_fwd.hip for the full design):
+//   "rows"  = local query-side rows of this rank (the module's projected `keys`, R rows)
+//   "cols"  = gathered key-side rows (the module's projected `queries`/`values`, T rows)
+//   All tensors are head-interleaved (..., H*D) so no transpose copies exist anywhere.
+//   Gathered tensors are rank-major (N, B, Rc, C): col t of batch b lives at
+//   (t / Rc) * cs + b * bs + (t % Rc) * C + h * D.
+// MFMA: v_mfma_f32_32x32x16_{bf16,f16}.  For a 32x32 accumulator X, lane l holds column
+// l&31 and rows (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15 (CDNA4 C/D map).
+#pragma once
+#include "common.h"
+
+namespace xdot {
+namespace fa {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ----------------------------------------------------------------------------------------
+template <int DT> struct mfma32;
+template <> struct mfma32<DT_BF16> {
+  static __device__ __forceinline__ f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct mfma32<DT_F16> {
+  static __device__ __forceinline__ f32x16 run(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+// pack two fp32 into one dword of two 16-bit values (round to nearest even)
+template <int DT> __device__ __forceinline__ uint32_t pack2(float a, float b);
+template <> __device__ __forceinline__ uint32_t pack2<DT_BF16>(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
+  bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+template <> __device__ __forceinline__ uint32_t pack2<DT_F16>(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+  h2 v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// accumulator registers 8s..8s+7 of a 32x32 tile -> MFMA operand fragment (k-step s)
+template <int DT>
+__device__ __forceinline__ u32x4 acc_to_frag(const f32x16& x, int s) {
+  u32x4 r;
+  r[0] = pack2<DT>(x[8 * s + 0], x[8 * s + 1]);
+  r[1] = pack2<DT>(x[8 * s + 2], x[8 * s + 3]);
+  r[2] = pack2<DT>(x[8 * s + 4], x[8 * s + 5]);
+  r[3] = pack2<DT>(x[8 * s + 6], x[8 * s + 7]);
+  return r;
+}
+
+// Transposed operand from a row-major [key][d] LDS image, matching acc_to_frag's k order:
+// lane l (d = d0 + (l&31), h = l>>5) gets elements j <-> key k0 + 8*(j>>2) + 4h + (j&3).
+__device__ __forceinline__ u32x4 tr_frag(const char* img, int row_stride, int k0, int d0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
+  const char* a0 = img + (k0 + 4 * h + q) * row_stride + (d0 + (g & 1) * 16 + 4 * p) * 2;
+  const char* a1 = a0 + 8 * row_stride;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  union { struct { s16x4 a, b; } s; u32x4 u; } c;
+  c.s.a = lo;
+  c.s.b = hi;
+  return c.u;
+}
+
+// Row-operand fragment (A or B of a 32x32x16 MFMA) from a row-major [row][d] LDS image:
+// lane l: row r0 + (l&31), d = 16*s + 8*(l>>5) .. +7.
+__device__ __forceinline__ u32x4 row_frag(const char* img, int row_stride, int r0, int s, int lane) {
+  return *reinterpret_cast<const u32x4*>(img + (r0 + (lane & 31)) * row_stride + (16 * s + 8 * (lane >> 5)) * 2);
+}
+
+// global address of gathered col t (element offset), head offset excluded
+__device__ __forceinline__ int64_t col_off(int t, int b, int Rc, int64_t cs, int64_t bs, int C) {
+  const int j = t / Rc;
+  return (int64_t)j * cs + (int64_t)b * bs + (int64_t)(t - j * Rc) * C;
+}
+
+// LDS row strides (bytes).  Row images read by ds_read_b128 use an odd number of 16-byte
+// slots (conflict-free for the b128 lane groups); images read with ds_read_b64_tr_b16 need
+// (stride/4) % 64 in {16, 48} (the 4 rows of a transposed read land in disjoint banks).
+template <int D> struct Geo {
+  static constexpr int ROWB = D * 2 + 16;                                        // b128 image
+  static constexpr int TRB = (D == 32) ? 64 : (D == 64 || D == 96) ? 192 : 320;  // tr image
+};
+
+}  // namespace fa
+}  // namespace xdot

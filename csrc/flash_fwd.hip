@@ -1,0 +1,227 @@
+// xdot — sequence-parallel flash-attention FORWARD for gfx950 (MI355X).
+//
+// Per rank: O = softmax(scale * K_rows · Q_colsᵀ, bool mask) · V_cols, where the columns are
+// the all-gathered T rows of the module's `queries`/`values` projections and the rows are
+// this rank's R rows of `keys` (reference: distributed_dot_product/module.py:60-71 — there
+// the (B, H, R, T) scores are materialised by distributed_matmul_nt, scaled, masked,
+// softmaxed and multiplied by distributed_matmul_all; here they only ever exist as MFMA
+// accumulators).
+//
+// Structure (one workgroup = 4 waves = 128 rows of one (batch, head); 2 workgroups/CU):
+//   * each wave owns 32 rows; their K-fragments stay in VGPRs for the whole sweep;
+//   * the workgroup streams 64-column tiles of Q_cols / V_cols HBM -> VGPR -> LDS, double
+//     buffered: tile t+1's global loads are issued before tile t's MFMAs and written to LDS
+//     after them (one barrier per tile);
+//   * S is computed TRANSPOSED (Sᵀ = Q_cols · K_rowsᵀ, v_mfma_f32_32x32x16) so that every
+//     lane holds 32 scores of ONE row: the online-softmax max/sum are lane-local plus a
+//     single cross-half exchange — no LDS round trip, no serial lanes;
+//   * the probabilities are packed to bf16 straight from the accumulators and used as the B
+//     operand of Oᵀ += V_colsᵀ · Pᵀ, with V_cols read through ds_read_b64_tr_b16 (hardware
+//     transpose) from a bank-conflict-free LDS image;
+//   * the boolean mask arrives pre-packed (csrc/mask_pack.hip): fully masked tiles are
+//     skipped, unmasked tiles pay nothing, partial tiles test one 64-bit word per row;
+//   * output O is written in the head-interleaved (B, R, H*D) layout the output projection
+//     consumes, plus the natural-log LSE per row for the backward recomputation.
+// Workgroup ids are XCD-remapped so the row blocks that stream the same (b, h) columns share
+// an XCD L2.
+#include "flash_common.h"
+
+namespace xdot {
+namespace fa {
+
+template <int DT, int D>
+__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  constexpr int ROWB = Geo<D>::ROWB, TRB = Geo<D>::TRB;
+  constexpr int QS_BYTES = 64 * ROWB, VS_BYTES = 64 * TRB, STAGE = QS_BYTES + VS_BYTES;
+  constexpr int KS = D / 16;      // k-steps over the head dim
+  constexpr int DB = D / 32;      // 32-wide d blocks of the output
+  constexpr int CPR = D / 8;      // 16-byte chunks per row
+  constexpr int LPT = (64 * CPR) / 256;  // 16-byte loads per thread per operand per tile
+  static_assert((64 * CPR) % 256 == 0, "tile/thread mismatch");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bh = lin / nrb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT = (a.T + 63) / 64;
+  const int r0 = rb * 128 + wave * 32;
+  const int row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+
+  const T16* rows = reinterpret_cast<const T16*>(a.rows);
+  const T16* kc = reinterpret_cast<const T16*>(a.kc) + h * D;
+  const T16* vc = reinterpret_cast<const T16*>(a.vc) + h * D;
+
+  // row-side fragments (B operand of Sᵀ): lane -> row, d = 16s + 8hf .. +7
+  u32x4 kf[KS];
+  {
+    const T16* p = rows + ((int64_t)b * a.R + row) * C + h * D + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) kf[s] = row_ok ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0, 0, 0, 0};
+  }
+
+  // staging of one 64-column tile (Q_cols and V_cols), global -> registers
+  u32x4 rq[LPT], rv[LPT];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v / CPR, c = v % CPR;
+      const int t = kt * 64 + r;
+      if (t < a.T) {
+        const int64_t off = col_off(t, b, a.Rc, a.cs, a.bs, C) + c * 8;
+        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+      } else {
+        rq[i] = u32x4{0, 0, 0, 0};
+        rv[i] = u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* qs = smem + buf * STAGE;
+    char* vs = qs + QS_BYTES;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v / CPR, c = v % CPR;
+      *reinterpret_cast<u32x4*>(qs + r * ROWB + c * 16) = rq[i];
+      *reinterpret_cast<u32x4*>(vs + r * TRB + c * 16) = rv[i];
+    }
+  };
+
+  const float c2 = a.scale * LOG2E;
+  const float NEG_INF = -__builtin_inff();
+  float m_run = NEG_INF, l_run = 0.f;
+  f32x16 o[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+
+  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
+  const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < NKT) load_tile(kt + 1);
+    const char* qs = smem + cur * STAGE;
+    const char* vs = qs + QS_BYTES;
+    const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
+    const bool tail = (kt + 1) * 64 > a.T;
+    if (flag != 1 && r0 < a.R) {
+      // ---- Sᵀ = Q_cols · K_rowsᵀ : two 32x32 tiles (cols 0-31, 32-63) ----
+      f32x16 s[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[tt] = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s[tt]);
+      }
+      // ---- online softmax (lane-local row, partner lane = lane ^ 32) ----
+      float mx = NEG_INF;
+      if (flag == 2 || tail) {
+        const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            float v = s[tt][r] * c2;
+            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) v = NEG_INF;
+            s[tt][r] = v;
+            mx = fmaxf(mx, v);
+          }
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = s[tt][r] * c2;
+            s[tt][r] = v;
+            mx = fmaxf(mx, v);
+          }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      m_run = m_new;
+      float ls = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[tt][r] - m_use);
+          s[tt][r] = p;
+          ls += p;
+        }
+      l_run = l_run * alpha + ls;
+#pragma unroll
+      for (int i = 0; i < DB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      // ---- Oᵀ += V_colsᵀ · Pᵀ ----
+      u32x4 pf[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh) pf[tt * 2 + sh] = acc_to_frag<DT>(s[tt], sh);
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+          o[db] = mfma32<DT>::run(tr_frag(vs, TRB, k4 * 16, db * 32, lane), pf[k4], o[db]);
+    }
+    if (kt + 1 < NKT) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (row_ok) {
+    T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 w;
+        w[0] = pack2<DT>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
+        w[1] = pack2<DT>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = w;
+      }
+    if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
+  }
+}
+
+template <int DT, int D>
+static void launch_fwd(const FwdArgs& a, hipStream_t st) {
+  constexpr int STAGE = 64 * Geo<D>::ROWB + 64 * Geo<D>::TRB;
+  const int nrb = (a.R + 127) / 128;
+  hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
+}
+
+}  // namespace fa
+}  // namespace xdot
+
+extern "C" int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+#define XF(DTV, DV) if (dt == DTV && D == DV) { launch_fwd<DTV, DV>(*a, st); return 0; }
+  XF(DT_BF16, 32) XF(DT_BF16, 64) XF(DT_BF16, 96) XF(DT_BF16, 128)
+  XF(DT_F16, 32) XF(DT_F16, 64) XF(DT_F16, 96) XF(DT_F16, 128)
+#undef XF
+  return -1;
+}

@@ -34,6 +34,39 @@ struct Args {
 };
 }  // namespace smx
 
+namespace fa {
+struct FwdArgs {
+  const void* rows;        // (B, R, H*D)
+  const void* kc;          // gathered key side (N, B, Rc, H*D)
+  const void* vc;          // gathered value side
+  void* out;               // (B, R, H*D)
+  float* lse;              // (B, H, R) natural-log LSE
+  const uint64_t* mbits;   // (B, R, NKT) bit k = col kt*64+k masked, or null
+  const uint8_t* mflags;   // (B, ceil(R/32), NKT) 0 none / 1 all / 2 partial, or null
+  int B, H, R, T, Rc;      // Rc = rows per rank of the gathered side
+  int64_t cs, bs;          // gathered chunk stride, batch stride (elements)
+  float scale;             // softmax scale (not log2-scaled)
+};
+
+struct BwdArgs {
+  const void* rows;        // (B, R, H*D)   row side (k)
+  const void* kc;          // gathered key side (q)
+  const void* vc;          // gathered value side (v)
+  const void* dout;        // (B, R, H*D)   upstream grad of out
+  const float* lse;        // (B, H, R)
+  const float* delta;      // (B, H, R) rowsum(dO * O)
+  void* drows;             // (B, R, H*D)   grad of row side (out dtype)
+  float* dkc;              // (N, B, Rc, H*D) fp32 partials, gathered layout
+  float* dvc;              // (N, B, Rc, H*D) fp32 partials, gathered layout
+  const uint64_t* mbits;
+  const uint8_t* mflags;
+  int B, H, R, T, Rc;
+  int64_t cs, bs;
+  float scale;
+};
+
+}  // namespace fa
+
 }  // namespace xdot
 
 extern "C" {
@@ -41,4 +74,7 @@ int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out
                      int b_mc, int vec, hipStream_t st);
 int xdot_softmax_fwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 int xdot_softmax_bwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
+int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_t* flags, int B, int R, int T, hipStream_t st);
+int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
+int xdot_flash_bwd_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);
 }

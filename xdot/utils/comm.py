@@ -150,10 +150,20 @@ class TorchDistComm(Communicator):
     def backend(self):
         return str(self._backend)
 
+    def _staged(self, *ts) -> bool:
+        """gloo cannot run these collectives on device memory: stage GPU tensors through the
+        host (used to emulate several ranks on one GPU in tests; never on the RCCL path)."""
+        return self._backend == "gloo" and any(t.is_cuda for t in ts)
+
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
+        if self._staged(out, inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            self.all_gather_into(o, inp.detach().cpu())
+            out.copy_(o)
+            return Handle(out=out) if async_op else None
         inp = inp.contiguous()
-        if self._backend == "gloo" and inp.dtype in (torch.bfloat16, torch.float16) and not inp.is_cuda:
+        if self._backend == "gloo" and inp.dtype in (torch.bfloat16, torch.float16):
             # gloo lacks half-precision kernels on some builds: gather the raw bytes instead
             w = dist.all_gather_into_tensor(out.view(-1).view(torch.int16), inp.view(-1).view(torch.int16),
                                             group=self.group, async_op=async_op)
@@ -164,6 +174,11 @@ class TorchDistComm(Communicator):
     def reduce_scatter(self, out, inp, async_op=False):
         if inp.numel() != out.numel() * self.world_size:
             raise ValueError("reduce_scatter: size mismatch")
+        if self._staged(out, inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            self.reduce_scatter(o, inp.detach().cpu())
+            out.copy_(o)
+            return Handle(out=out) if async_op else None
         inp = inp.contiguous()
         if self._backend == "gloo" and inp.dtype in (torch.bfloat16, torch.float16):
             # reduce in fp32 on gloo (no half reductions on CPU backends)
@@ -184,10 +199,20 @@ class TorchDistComm(Communicator):
         return None
 
     def all_reduce(self, t, op="sum", async_op=False):
+        if self._staged(t):
+            c = t.detach().cpu()
+            dist.all_reduce(c, op=_OPS[op], group=self.group)
+            t.copy_(c)
+            return Handle(out=t) if async_op else None
         w = dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=async_op)
         return Handle(w, t) if async_op else None
 
     def broadcast(self, t, src=0, async_op=False):
+        if self._staged(t):
+            c = t.detach().cpu()
+            dist.broadcast(c, src=src, group=self.group)
+            t.copy_(c)
+            return Handle(out=t) if async_op else None
         w = dist.broadcast(t, src=src, group=self.group, async_op=async_op)
         return Handle(w, t) if async_op else None
 
@@ -236,7 +261,8 @@ class ThreadGroup:
         for t in threads:
             t.join()
         if errors:
-            raise errors[0]
+            real = [e for e in errors if not isinstance(e, threading.BrokenBarrierError)]
+            raise (real or errors)[0]
         return results
 
 
