@@ -79,6 +79,11 @@ def test_module_unmasked_float32_reference_config():
                                                 dtype=torch.float32, tol=1e-5))
 
 
+def test_module_bf16_gloo():
+    """bf16 end to end over real gloo collectives (half-precision gathers / reductions)."""
+    run_gloo(_module_parity, 2, 4, "flash", None, True, torch.bfloat16, 0.08)
+
+
 def test_fully_masked_row_gives_nan():
     from xdot import DistributedDotProductAttn
 

@@ -163,12 +163,7 @@ class TorchDistComm(Communicator):
             out.copy_(o)
             return Handle(out=out) if async_op else None
         inp = inp.contiguous()
-        if self._backend == "gloo" and inp.dtype in (torch.bfloat16, torch.float16):
-            # gloo lacks half-precision kernels on some builds: gather the raw bytes instead
-            w = dist.all_gather_into_tensor(out.view(-1).view(torch.int16), inp.view(-1).view(torch.int16),
-                                            group=self.group, async_op=async_op)
-        else:
-            w = dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
+        w = dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
         return Handle(w, out) if async_op else None
 
     def reduce_scatter(self, out, inp, async_op=False):
