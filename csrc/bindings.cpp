@@ -148,7 +148,7 @@ std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
 }
 
 struct FlashGeom {
-  int64_t B, R, C, N, Rc, T, D;
+  int64_t B, R, C, T, D;
 };
 
 FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc, int64_t H,
@@ -157,13 +157,13 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   TORCH_CHECK(rows.is_contiguous() && kc.is_contiguous() && vc.is_contiguous(), "xdot.flash: contiguous tensors required");
   TORCH_CHECK(rows.scalar_type() == kc.scalar_type() && rows.scalar_type() == vc.scalar_type(), "xdot.flash: dtype mismatch");
   TORCH_CHECK(rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kHalf, "xdot.flash: bf16/fp16 only");
-  TORCH_CHECK(rows.dim() == 3 && kc.dim() == 4 && vc.sizes() == kc.sizes(), "xdot.flash: rows (B,R,C), cols (N,B,Rc,C)");
-  FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(0), kc.size(2), 0, 0};
-  TORCH_CHECK(kc.size(1) == g.B && kc.size(3) == g.C, "xdot.flash: batch / feature mismatch");
+  TORCH_CHECK(rows.dim() == 3 && kc.dim() == 3 && vc.sizes() == kc.sizes(), "xdot.flash: rows (B,R,C), cols (B,T,C)");
+  FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(1), 0};
+  TORCH_CHECK(kc.size(0) == g.B && kc.size(2) == g.C, "xdot.flash: batch / feature mismatch");
+  TORCH_CHECK(g.T > 0, "xdot.flash: empty key side");
   TORCH_CHECK(H > 0 && g.C % H == 0, "xdot.flash: C not divisible by heads");
   g.D = g.C / H;
   TORCH_CHECK(g.D == 32 || g.D == 64 || g.D == 96 || g.D == 128, "xdot.flash: head dim must be 32/64/96/128");
-  g.T = g.N * g.Rc;
   TORCH_CHECK(g.T < (1LL << 31) && g.R < (1LL << 31) && g.B * H * ((g.R + 127) / 128) < (1LL << 31), "xdot.flash: too large");
   TORCH_CHECK(aligned16(rows.data_ptr()) && aligned16(kc.data_ptr()) && aligned16(vc.data_ptr()), "xdot.flash: 16-byte alignment");
   const bool hb = bits.has_value() && bits->defined(), hf = flags.has_value() && flags->defined();
@@ -176,52 +176,111 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   return g;
 }
 
+// Column split so small row counts (e.g. T/N = 3125 rows at N = 8: 200 workgroups) still put
+// >= `target` workgroups on the 256 CUs; every split keeps >= 8 column tiles.
+int pick_split(int64_t blocks, int64_t T, int64_t target, int64_t req) {
+  const int64_t nkt = (T + 63) / 64;
+  if (req > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(req, nkt));
+  if (blocks >= target) return 1;
+  int64_t s = (target + blocks - 1) / blocks;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, nkt / 8));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 8));
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
-                                             int64_t H, double scale) {
+                                             int64_t H, double scale, int64_t nsplit) {
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   auto out = at::empty_like(rows);
   auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  const int ns = pick_split(((g.R + 127) / 128) * g.B * H, g.T, 512, nsplit);
+  at::Tensor opart, lpart;
+  if (ns > 1) {
+    opart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
+    lpart = at::empty({ns, g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  }
   xdot::fa::FwdArgs a{};
   a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.out = out.data_ptr();
   a.lse = lse.data_ptr<float>();
   const bool hb = bits.has_value() && bits->defined();
   a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
   a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
-  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.Rc = (int)g.Rc;
-  a.cs = g.B * g.Rc * g.C; a.bs = g.Rc * g.C; a.scale = (float)scale;
+  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.scale = (float)scale;
+  a.nsplit = ns;
+  a.opart = ns > 1 ? opart.data_ptr<float>() : nullptr;
+  a.lpart = ns > 1 ? lpart.data_ptr<float>() : nullptr;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0, "xdot.flash_fwd: config");
   check_launch(hipGetLastError(), "flash_fwd");
   return {out, lse};
 }
 
+xdot::fa::BwdArgs bwd_args(const FlashGeom& g, const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc,
+                           const at::Tensor& vc, const at::Tensor& lse, const c10::optional<at::Tensor>& bits,
+                           const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
+  TORCH_CHECK(dout.sizes() == rows.sizes() && dout.is_contiguous() && dout.scalar_type() == rows.scalar_type(),
+              "xdot.flash_bwd: dout shape/dtype");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat && lse.numel() == g.B * H * g.R, "xdot.flash_bwd: lse");
+  xdot::fa::BwdArgs a{};
+  a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.dout = dout.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  const bool hb = bits.has_value() && bits->defined();
+  a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
+  a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
+  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.scale = (float)scale;
+  a.nsplit = 1;
+  return a;
+}
+
+// gathered-side grads (fp32 (B, T, C) partials for the reduce-scatter) + δ = rowsum(dO·O)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const at::Tensor& rows,
+                                                              const at::Tensor& kc, const at::Tensor& vc,
+                                                              const at::Tensor& out, const at::Tensor& lse,
+                                                              const c10::optional<at::Tensor>& bits,
+                                                              const c10::optional<at::Tensor>& flags, int64_t H,
+                                                              double scale) {
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
+              "xdot.flash_bwd_cols: out shape/dtype");
+  auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
+  auto dkc = at::empty(kc.sizes(), kc.options().dtype(at::kFloat));
+  auto dvc = at::empty(vc.sizes(), vc.options().dtype(at::kFloat));
+  auto delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  a.dkc = dkc.data_ptr<float>(); a.dvc = dvc.data_ptr<float>();
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(rows.scalar_type()),
+                                         (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
+  check_launch(hipGetLastError(), "flash_bwd_cols");
+  return {dkc, dvc, delta};
+}
+
+// row-side grad (this rank's rows), column-split when the row count is small
+at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
+                          const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
+                          const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit) {
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
+              "xdot.flash_bwd_rows: delta");
+  auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
+  auto drows = at::empty_like(rows);
+  const int ns = pick_split(((g.R + 127) / 128) * g.B * H, g.T, 512, nsplit);
+  at::Tensor dpart;
+  if (ns > 1) dpart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
+  a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
+  a.nsplit = ns; a.dpart = ns > 1 ? dpart.data_ptr<float>() : nullptr;
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
+              "xdot.flash_bwd_rows: config");
+  check_launch(hipGetLastError(), "flash_bwd_rows");
+  return drows;
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc,
                                                          const at::Tensor& vc, const at::Tensor& out, const at::Tensor& lse,
                                                          const c10::optional<at::Tensor>& bits,
                                                          const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
-  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
-  TORCH_CHECK(dout.sizes() == rows.sizes() && out.sizes() == rows.sizes() && dout.is_contiguous() && out.is_contiguous(),
-              "xdot.flash_bwd: dout/out shape");
-  TORCH_CHECK(dout.scalar_type() == rows.scalar_type() && out.scalar_type() == rows.scalar_type(), "xdot.flash_bwd: dtype");
-  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat && lse.numel() == g.B * H * g.R, "xdot.flash_bwd: lse");
-  auto drows = at::empty_like(rows);
-  auto dkc = at::empty(kc.sizes(), kc.options().dtype(at::kFloat));
-  auto dvc = at::empty(vc.sizes(), vc.options().dtype(at::kFloat));
-  auto delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
-  xdot::fa::BwdArgs a{};
-  a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.dout = dout.data_ptr();
-  a.lse = lse.data_ptr<float>(); a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
-  a.dkc = dkc.data_ptr<float>(); a.dvc = dvc.data_ptr<float>();
-  const bool hb = bits.has_value() && bits->defined();
-  a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
-  a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
-  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.Rc = (int)g.Rc;
-  a.cs = g.B * g.Rc * g.C; a.bs = g.Rc * g.C; a.scale = (float)scale;
-  c10::DeviceGuard guard(rows.device());
-  TORCH_CHECK(xdot_flash_bwd_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(rows.scalar_type()), (int)g.D,
-                                    cur_stream(rows)) == 0, "xdot.flash_bwd: config");
-  check_launch(hipGetLastError(), "flash_bwd");
+  auto [dkc, dvc, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale);
+  auto drows = flash_bwd_rows(dout, rows, kc, vc, lse, delta, bits, flags, H, scale, 0);
   return {drows, dkc, dvc};
 }
 
@@ -234,7 +293,11 @@ TORCH_LIBRARY(xdot, m) {
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor)");
-  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale) -> (Tensor, Tensor)");
+  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
+  m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
+        "Tensor? flags, int H, float scale) -> (Tensor, Tensor, Tensor)");
+  m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
+        "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
   m.def("flash_bwd(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, Tensor? flags, "
         "int H, float scale) -> (Tensor, Tensor, Tensor)");
 }
@@ -246,4 +309,6 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("mask_pack", &mask_pack);
   m.impl("flash_fwd", &flash_fwd);
   m.impl("flash_bwd", &flash_bwd);
+  m.impl("flash_bwd_cols", &flash_bwd_cols);
+  m.impl("flash_bwd_rows", &flash_bwd_rows);
 }

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 // ---------------------------------------------------------------------------------------
 // grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols.
 template <int DT, int D>
-__global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   constexpr int ROWB = Geo<D>::ROWB;
   constexpr int QS_BYTES = 64 * ROWB, STAGE = 2 * QS_BYTES;
@@ -66,10 +66,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb = lin % nrb, bh = lin / nrb;
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int NKT = (a.T + 63) / 64;
+  const int kt_beg = (int)((int64_t)sp * NKT / a.nsplit), kt_end = (int)((int64_t)(sp + 1) * NKT / a.nsplit);
   const int r0 = rb * 128 + wave * 32;
   const int row = r0 + (lane & 31);
   const bool row_ok = row < a.R;
@@ -97,15 +99,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = kt * 64 + r;
-      if (t < a.T) {
-        const int64_t off = col_off(t, b, a.Rc, a.cs, a.bs, C) + c * 8;
-        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
-      } else {
-        rq[i] = u32x4{0, 0, 0, 0};
-        rv[i] = u32x4{0, 0, 0, 0};
-      }
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = min(kt * 64 + r, a.T - 1);
+      const int64_t off = col_off(t, b, a.T, C) + c * 8;
+      rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+      rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
     }
   };
   auto store_tile = [&](int buf) {
@@ -127,52 +124,59 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
   const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
-  load_tile(0);
+  load_tile(kt_beg);
   store_tile(0);
   __syncthreads();
-  for (int kt = 0; kt < NKT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < NKT) load_tile(kt + 1);
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_beg) & 1;
+    if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
     const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { s[tt][r] = 0.f; dp[tt][r] = 0.f; }
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s[tt] = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s[tt]);
-          dp[tt] = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, ks, lane), df[ks], dp[tt]);
-        }
-      }
       const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
       const bool chk = flag == 2 || tail;
+      // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+      for (int tt = 0; tt < 2; ++tt) {
+        f32x16 s = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, 0, lane), kf[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, 0, lane), df[0], f32x16{});
+#pragma unroll
+        for (int ks = 1; ks < KS; ++ks) {
+          s = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s);
+          dp = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, ks, lane), df[ks], dp);
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float x = s[tt][r] * c2 - lse2;
+          float x = __builtin_fmaf(s[r], c2, -lse2);
           if (chk) {
             const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
             if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) x = NEG_INF;
           }
-          const float p = exp2f(x);
-          s[tt][r] = p * (dp[tt][r] - dlt);  // dSᵀ (unscaled)
+          s[r] = fast_exp2(x) * (dp[r] - dlt);  // dSᵀ (unscaled)
         }
+        const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
 #pragma unroll
-      for (int db = 0; db < DB; ++db)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(s[k4 >> 1], k4 & 1), dk[db]);
+        for (int db = 0; db < DB; ++db) {
+          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, tt * 32, db * 32, lane), f0, dk[db]);
+          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, tt * 32 + 16, db * 32, lane), f1, dk[db]);
+        }
+      }
     }
-    if (kt + 1 < NKT) store_tile(cur ^ 1);
+    if (kt + 1 < kt_end) store_tile(cur ^ 1);
     __syncthreads();
   }
-  if (row_ok) {
+  if (row_ok && a.nsplit > 1) {
+    float* op = a.dpart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v = {dk[db][4 * g] * a.scale, dk[db][4 * g + 1] * a.scale, dk[db][4 * g + 2] * a.scale, dk[db][4 * g + 3] * a.scale};
+        *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
+      }
+  } else if (row_ok) {
     T16* op = reinterpret_cast<T16*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_rows_kernel(BwdArgs a) {
 // ---------------------------------------------------------------------------------------
 // grads of the gathered side.  4 waves x 32 columns; 64-row tiles of K_rows / dO.
 template <int DT, int D>
-__global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   constexpr int ROWB = Geo<D>::ROWB;
   constexpr int IMG = 64 * ROWB;
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
 
   u32x4 qf[KS], vf[KS];
   {
-    const int64_t off = col_off(col_ok ? col : 0, b, a.Rc, a.cs, a.bs, C) + h * D + 8 * hf;
+    const int64_t off = col_off(col_ok ? col : 0, b, a.T, C) + h * D + 8 * hf;
     const T16* pq = reinterpret_cast<const T16*>(a.kc) + off;
     const T16* pv = reinterpret_cast<const T16*>(a.vc) + off;
 #pragma unroll
@@ -232,32 +236,18 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
   const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
 
   u32x4 rk[LPT], rd[LPT];
-  float sl = 0.f, sd = 0.f;
-  uint64_t sw = 0;
   auto load_tile = [&](int rt) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = rt * 64 + r;
-      if (rr < a.R) {
-        const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
-        rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
-        rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
-      } else {
-        rk[i] = u32x4{0, 0, 0, 0};
-        rd[i] = u32x4{0, 0, 0, 0};
-      }
-    }
-    if (tid < 64) {
-      const int rr = rt * 64 + tid;
-      // rows past R: lse = +inf makes P = 0 for them
-      sl = rr < a.R ? lse[rr] * LOG2E : __builtin_inff();
-      sd = rr < a.R ? dlt[rr] : 0.f;
-    } else if (tid < 192 && a.mbits) {
-      const int r = (tid - 64) & 63, k = (tid - 64) >> 6, rr = rt * 64 + r;
-      sw = (rr < a.R && kt0 + k < NKT) ? a.mbits[((int64_t)b * a.R + rr) * NKT + kt0 + k] : 0ull;
+      // rows past R re-read row R-1 (finite); their lse = +inf below makes P = dS = 0
+      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = min(rt * 64 + r, a.R - 1);
+      const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
+      rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
+      rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
     }
   };
-  auto store_tile = [&](int buf) {
+  // the per-row lse/δ/mask words go global -> LDS right here (short register lifetime)
+  auto store_tile = [&](int buf, int rt) {
     char* ks = smem + buf * STAGE;
     char* ds = ks + IMG;
     float* ls = reinterpret_cast<float*>(ds + IMG);
@@ -270,10 +260,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
       *reinterpret_cast<u32x4*>(ds + r * ROWB + c * 16) = rd[i];
     }
     if (tid < 64) {
-      ls[tid] = sl;
-      dls[tid] = sd;
+      const int rr = rt * 64 + tid;
+      // rows past R: lse = +inf makes P = 0 for them
+      ls[tid] = rr < a.R ? lse[rr] * LOG2E : __builtin_inff();
+      dls[tid] = rr < a.R ? dlt[rr] : 0.f;
     } else if (tid < 192 && a.mbits) {
-      ws[tid - 64] = sw;
+      const int r = (tid - 64) & 63, k = (tid - 64) >> 6, rr = rt * 64 + r;
+      ws[tid - 64] = (rr < a.R && kt0 + k < NKT) ? a.mbits[((int64_t)b * a.R + rr) * NKT + kt0 + k] : 0ull;
     }
   };
 
@@ -284,7 +277,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
     for (int r = 0; r < 16; ++r) { dq[i][r] = 0.f; dv[i][r] = 0.f; }
 
   load_tile(0);
-  store_tile(0);
+  store_tile(0, 0);
   __syncthreads();
   for (int rt = 0; rt < NRT; ++rt) {
     const int cur = rt & 1;
@@ -302,20 +295,16 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
       flag = (f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2);
     }
     if (flag != 1 && c0 < a.T) {
-      f32x16 s[2], dp[2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
+        f32x16 s = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, 0, lane), qf[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, 0, lane), vf[0], f32x16{});
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { s[tt][r] = 0.f; dp[tt][r] = 0.f; }
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          s[tt] = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, kk, lane), qf[kk], s[tt]);
-          dp[tt] = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, kk, lane), vf[kk], dp[tt]);
+        for (int kk = 1; kk < KS; ++kk) {
+          s = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, kk, lane), qf[kk], s);
+          dp = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, kk, lane), vf[kk], dp);
         }
-      }
-      // P and dS; rows of register r: tt*32 + (r&3) + 8*(r>>2) + 4*hf
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        // P and dS; rows of register r: tt*32 + (r&3) + 8*(r>>2) + 4*hf
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int rbase = tt * 32 + 8 * g + 4 * hf;
@@ -324,29 +313,32 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            float x = s[tt][r] * c2 - l4[e];
+            float x = __builtin_fmaf(s[r], c2, -l4[e]);
             if (flag == 2) {
               const uint64_t wv = ws[(kt_w - kt0) * 64 + rbase + e];
               if ((wv >> (bit0 + (lane & 31))) & 1ull) x = NEG_INF;
             }
-            const float p = exp2f(x);
-            s[tt][r] = p;
-            dp[tt][r] = p * (dp[tt][r] - d4[e]);
+            const float p = fast_exp2(x);
+            s[r] = p;
+            dp[r] = p * (dp[r] - d4[e]);
           }
         }
+        const u32x4 p0 = acc_to_frag<DT>(s, 0), p1 = acc_to_frag<DT>(s, 1);
+        const u32x4 g0 = acc_to_frag<DT>(dp, 0), g1 = acc_to_frag<DT>(dp, 1);
 #pragma unroll
-      for (int db = 0; db < DB; ++db)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(s[k4 >> 1], k4 & 1), dv[db]);
-          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, k4 * 16, db * 32, lane), acc_to_frag<DT>(dp[k4 >> 1], k4 & 1), dq[db]);
+        for (int db = 0; db < DB; ++db) {
+          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, tt * 32, db * 32, lane), p0, dv[db]);
+          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, tt * 32 + 16, db * 32, lane), p1, dv[db]);
+          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, tt * 32, db * 32, lane), g0, dq[db]);
+          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, tt * 32 + 16, db * 32, lane), g1, dq[db]);
         }
+      }
     }
-    if (rt + 1 < NRT) store_tile(cur ^ 1);
+    if (rt + 1 < NRT) store_tile(cur ^ 1, rt + 1);
     __syncthreads();
   }
   if (col_ok) {
-    const int64_t off = col_off(col, b, a.Rc, a.cs, a.bs, C) + h * D;
+    const int64_t off = col_off(col, b, a.T, C) + h * D;
     float* pq = a.dkc + off;
     float* pv = a.dvc + off;
 #pragma unroll
@@ -361,31 +353,74 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_cols_kernel(BwdArgs a) {
   }
 }
 
+// sum column-split partials of the row-side gradient -> output dtype
 template <int DT, int D>
-static void launch_bwd(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
+__global__ __launch_bounds__(256) void flash_bwd_rows_sum(BwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  const int64_t total4 = (int64_t)a.B * a.R * a.H * D / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total4) return;
+  const int64_t stride = total4 * 4;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(a.dpart + idx * 4);
+  for (int s = 1; s < a.nsplit; ++s) acc += *reinterpret_cast<const f32x4*>(a.dpart + s * stride + idx * 4);
+  u32x2 w;
+  w[0] = pack2<DT>(acc[0], acc[1]);
+  w[1] = pack2<DT>(acc[2], acc[3]);
+  *reinterpret_cast<u32x2*>(reinterpret_cast<T16*>(a.drows) + idx * 4) = w;
+}
+
+template <int DT, int D>
+static void launch_bwd_cols(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
   const int64_t n0 = (int64_t)a.B * a.R * a.H;
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
   BwdArgs a2 = a;
   a2.delta = delta;
   constexpr int ROWB = Geo<D>::ROWB;
-  const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H), dim3(256), 2 * (2 * 64 * ROWB), st, a2);
   const int ncb = (a.T + 127) / 128;
   constexpr int STAGE = 2 * 64 * ROWB + 64 * 4 * 2 + 64 * 8 * 2;
   hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a2);
 }
 
+template <int DT, int D>
+static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
+  constexpr int ROWB = Geo<D>::ROWB;
+  const int nrb = (a.R + 127) / 128;
+  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * 64 * ROWB), st, a);
+  if (a.nsplit > 1) {
+    const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
+    hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
+  }
+}
+
 }  // namespace fa
 }  // namespace xdot
 
-extern "C" int xdot_flash_bwd_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
-                                     hipStream_t st) {
+#define XB_DISPATCH(CALL)                                                                        \
+  if (dt == DT_BF16 && D == 32) { CALL(DT_BF16, 32); return 0; }                                 \
+  if (dt == DT_BF16 && D == 64) { CALL(DT_BF16, 64); return 0; }                                 \
+  if (dt == DT_BF16 && D == 96) { CALL(DT_BF16, 96); return 0; }                                 \
+  if (dt == DT_BF16 && D == 128) { CALL(DT_BF16, 128); return 0; }                               \
+  if (dt == DT_F16 && D == 32) { CALL(DT_F16, 32); return 0; }                                   \
+  if (dt == DT_F16 && D == 64) { CALL(DT_F16, 64); return 0; }                                   \
+  if (dt == DT_F16 && D == 96) { CALL(DT_F16, 96); return 0; }                                   \
+  if (dt == DT_F16 && D == 128) { CALL(DT_F16, 128); return 0; }                                 \
+  return -1;
+
+extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
+                                          hipStream_t st) {
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
-#define XB(DTV, DV) if (dt == DTV && D == DV) { launch_bwd<DTV, DV>(*a, out, delta, st); return 0; }
-  XB(DT_BF16, 32) XB(DT_BF16, 64) XB(DT_BF16, 96) XB(DT_BF16, 128)
-  XB(DT_F16, 32) XB(DT_F16, 64) XB(DT_F16, 96) XB(DT_F16, 128)
-#undef XB
-  return -1;
+#define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, out, delta, st)
+  XB_DISPATCH(XC)
+#undef XC
+}
+
+extern "C" int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+#define XR(DTV, DV) launch_bwd_rows<DTV, DV>(*a, st)
+  XB_DISPATCH(XR)
+#undef XR
 }

@@ -4,8 +4,8 @@
 //   "rows"  = local query-side rows of this rank (the module's projected `keys`, R rows)
 //   "cols"  = gathered key-side rows (the module's projected `queries`/`values`, T rows)
 //   All tensors are head-interleaved (..., H*D) so no transpose copies exist anywhere.
-//   Gathered tensors are rank-major (N, B, Rc, C): col t of batch b lives at
-//   (t / Rc) * cs + b * bs + (t % Rc) * C + h * D.
+//   Gathered tensors are (B, T, C): col t of batch b lives at (b*T + t)*C + h*D (the RCCL
+//   all-gather output (N, 1, R, C) is exactly this layout for B = 1).
 // MFMA: v_mfma_f32_32x32x16_{bf16,f16}.  For a 32x32 accumulator X, lane l holds column
 // l&31 and rows (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15 (CDNA4 C/D map).
 #pragma once
@@ -77,11 +77,14 @@ __device__ __forceinline__ u32x4 row_frag(const char* img, int row_stride, int r
   return *reinterpret_cast<const u32x4*>(img + (r0 + (lane & 31)) * row_stride + (16 * s + 8 * (lane >> 5)) * 2);
 }
 
-// global address of gathered col t (element offset), head offset excluded
-__device__ __forceinline__ int64_t col_off(int t, int b, int Rc, int64_t cs, int64_t bs, int C) {
-  const int j = t / Rc;
-  return (int64_t)j * cs + (int64_t)b * bs + (int64_t)(t - j * Rc) * C;
+// global element offset of gathered col t (head offset excluded)
+__device__ __forceinline__ int64_t col_off(int t, int b, int T, int C) {
+  return ((int64_t)b * T + t) * C;
 }
+
+// v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;
+// arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // LDS row strides (bytes).  Row images read by ds_read_b128 use an odd number of 16-byte
 // slots (conflict-free for the b128 lane groups); images read with ds_read_b64_tr_b16 need

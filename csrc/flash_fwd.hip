@@ -45,10 +45,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb = lin % nrb, bh = lin / nrb;
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int NKT = (a.T + 63) / 64;
+  const int kt_beg = (int)((int64_t)sp * NKT / a.nsplit), kt_end = (int)((int64_t)(sp + 1) * NKT / a.nsplit);
   const int r0 = rb * 128 + wave * 32;
   const int row = r0 + (lane & 31);
   const bool row_ok = row < a.R;
@@ -72,15 +74,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     for (int i = 0; i < LPT; ++i) {
       const int v = tid + 256 * i;
       const int r = v / CPR, c = v % CPR;
-      const int t = kt * 64 + r;
-      if (t < a.T) {
-        const int64_t off = col_off(t, b, a.Rc, a.cs, a.bs, C) + c * 8;
-        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
-      } else {
-        rq[i] = u32x4{0, 0, 0, 0};
-        rv[i] = u32x4{0, 0, 0, 0};
-      }
+      // rows past T read row T-1: their scores are masked to -inf, so P = 0 multiplies
+      // finite values (no branch around the loads)
+      const int t = min(kt * 64 + r, a.T - 1);
+      const int64_t off = col_off(t, b, a.T, C) + c * 8;
+      rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+      rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
     }
   };
   auto store_tile = [&](int buf) {
@@ -107,13 +106,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
   const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
-  load_tile(0);
+  load_tile(kt_beg);
   store_tile(0);
   __syncthreads();
 
-  for (int kt = 0; kt < NKT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < NKT) load_tile(kt + 1);
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_beg) & 1;
+    if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
     const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
@@ -129,6 +128,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         for (int ks = 0; ks < KS; ++ks) s[tt] = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s[tt]);
       }
       // ---- online softmax (lane-local row, partner lane = lane ^ 32) ----
+      // max over raw scores (scale > 0), exponent as one FMA: p = 2^(s*c2 - m)
       float mx = NEG_INF;
       if (flag == 2 || tail) {
         const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
@@ -137,40 +137,38 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            float v = s[tt][r] * c2;
-            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) v = NEG_INF;
-            s[tt][r] = v;
-            mx = fmaxf(mx, v);
+            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) s[tt][r] = NEG_INF;
+            mx = fmaxf(mx, s[tt][r]);
           }
       } else {
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = s[tt][r] * c2;
-            s[tt][r] = v;
-            mx = fmaxf(mx, v);
-          }
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c2;
       const float m_new = fmaxf(m_run, mx);
       const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      // rescale the running output only when some row of the wave raised its max
+      if (__any(m_new > m_run)) {
+        const float alpha = fast_exp2(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < DB; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      }
       m_run = m_new;
       float ls = 0.f;
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[tt][r] - m_use);
+          const float p = fast_exp2(__builtin_fmaf(s[tt][r], c2, -m_use));
           s[tt][r] = p;
           ls += p;
         }
-      l_run = l_run * alpha + ls;
-#pragma unroll
-      for (int i = 0; i < DB; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      l_run += ls;
       // ---- Oᵀ += V_colsᵀ · Pᵀ ----
       u32x4 pf[4];
 #pragma unroll
@@ -183,14 +181,14 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         for (int k4 = 0; k4 < 4; ++k4)
           o[db] = mfma32<DT>::run(tr_frag(vs, TRB, k4 * 16, db * 32, lane), pf[k4], o[db]);
     }
-    if (kt + 1 < NKT) store_tile(cur ^ 1);
+    if (kt + 1 < kt_end) store_tile(cur ^ 1);
     __syncthreads();
   }
 
   // ---- epilogue ----
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.f / l_tot;
-  if (row_ok) {
+  if (row_ok && a.nsplit == 1) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
@@ -202,14 +200,69 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = w;
       }
     if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
+  } else if (row_ok) {
+    // split partial: normalised fp32 output + its LSE; merged by flash_fwd_combine
+    float* op = a.opart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v = {o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
+        *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
+      }
+    if (hf == 0) a.lpart[(((int64_t)sp * a.B + b) * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
   }
+}
+
+// merge column-split partials: lse = log Σ_s e^{lse_s}, O = Σ_s e^{lse_s - lse} O_s.
+// A split that saw only masked columns has lse_s = -inf and contributes nothing; a row with
+// every split -inf is fully masked and yields NaN like the unsplit kernel.
+template <int DT, int D>
+__global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  const int C = a.H * D;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.R * (C / 4);
+  if (idx >= total) return;
+  const int c4 = (int)(idx % (C / 4));
+  const int64_t br = idx / (C / 4);
+  const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int h = (c4 * 4) / D;
+  const int64_t lstride = (int64_t)a.B * a.H * a.R;
+  const float* lp = a.lpart + ((int64_t)b * a.H + h) * a.R + row;
+  float mx = -__builtin_inff();
+  for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, lp[s * lstride]);
+  float sum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ostride = (int64_t)a.B * a.R * C;
+  const float* opp = a.opart + br * C + c4 * 4;
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float l = lp[s * lstride];
+    if (l == -__builtin_inff()) continue;
+    const float wgt = __expf(l - mx);
+    sum += wgt;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(opp + s * ostride);
+    acc += wgt * v;
+  }
+  const float inv = 1.f / sum;  // sum == 0 (fully masked row) -> NaN output, -inf lse
+  T16* op = reinterpret_cast<T16*>(a.out) + br * C + c4 * 4;
+  u32x2 w;
+  w[0] = pack2<DT>(acc[0] * inv, acc[1] * inv);
+  w[1] = pack2<DT>(acc[2] * inv, acc[3] * inv);
+  if (sum == 0.f) { w[0] = pack2<DT>(__builtin_nanf(""), __builtin_nanf("")); w[1] = w[0]; }
+  *reinterpret_cast<u32x2*>(op) = w;
+  if ((c4 * 4) % D == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
 }
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
   constexpr int STAGE = 64 * Geo<D>::ROWB + 64 * Geo<D>::TRB;
   const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
+  hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
+  if (a.nsplit > 1) {
+    const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
+    hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  }
 }
 
 }  // namespace fa

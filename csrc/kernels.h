@@ -37,15 +37,17 @@ struct Args {
 namespace fa {
 struct FwdArgs {
   const void* rows;        // (B, R, H*D)
-  const void* kc;          // gathered key side (N, B, Rc, H*D)
-  const void* vc;          // gathered value side
+  const void* kc;          // gathered key side (B, T, H*D)
+  const void* vc;          // gathered value side (B, T, H*D)
   void* out;               // (B, R, H*D)
   float* lse;              // (B, H, R) natural-log LSE
   const uint64_t* mbits;   // (B, R, NKT) bit k = col kt*64+k masked, or null
   const uint8_t* mflags;   // (B, ceil(R/32), NKT) 0 none / 1 all / 2 partial, or null
-  int B, H, R, T, Rc;      // Rc = rows per rank of the gathered side
-  int64_t cs, bs;          // gathered chunk stride, batch stride (elements)
+  int B, H, R, T;
   float scale;             // softmax scale (not log2-scaled)
+  int nsplit;              // column splits (>1: partials to opart/lpart, then combine)
+  float* opart;            // (nsplit, B, R, H*D) fp32 normalised partial outputs
+  float* lpart;            // (nsplit, B, H, R) partial LSE
 };
 
 struct BwdArgs {
@@ -56,13 +58,14 @@ struct BwdArgs {
   const float* lse;        // (B, H, R)
   const float* delta;      // (B, H, R) rowsum(dO * O)
   void* drows;             // (B, R, H*D)   grad of row side (out dtype)
-  float* dkc;              // (N, B, Rc, H*D) fp32 partials, gathered layout
-  float* dvc;              // (N, B, Rc, H*D) fp32 partials, gathered layout
+  float* dkc;              // (B, T, H*D) fp32 partial grads of the gathered key side
+  float* dvc;              // (B, T, H*D) fp32 partial grads of the gathered value side
   const uint64_t* mbits;
   const uint8_t* mflags;
-  int B, H, R, T, Rc;
-  int64_t cs, bs;
+  int B, H, R, T;
   float scale;
+  int nsplit;              // column splits of the row-side kernel
+  float* dpart;            // (nsplit, B, R, H*D) fp32 partial row-side grads (nsplit > 1)
 };
 
 }  // namespace fa
@@ -76,5 +79,6 @@ int xdot_softmax_fwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream
 int xdot_softmax_bwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_t* flags, int B, int R, int T, hipStream_t st);
 int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
-int xdot_flash_bwd_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);
+int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);
+int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 }

@@ -12,31 +12,39 @@
 
 namespace xdot {
 
-// one thread per (b, r, kt): gather 64 bytes -> one 64-bit word
+// 8 lanes per 64-bit word: lane c of a group packs bytes [8c, 8c+8) of the word's 64-byte
+// span into 8 bits, the group ORs its pieces with 3 xor-shuffles, lane 0 stores.  Each lane
+// issues one 8-byte load, consecutive lanes read consecutive bytes (coalesced; rows only need
+// 8-byte alignment, e.g. T = 25000).
 __global__ __launch_bounds__(256) void mask_bits_kernel(const uint8_t* __restrict__ m, uint64_t* __restrict__ bits,
-                                                         int64_t rows, int T, int NKT, bool vec) {
+                                                         int64_t rows, int T, int NKT, bool vec8) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * NKT) return;
-  const int64_t r = idx / NKT;
-  const int kt = (int)(idx - r * NKT);
-  const uint8_t* p = m + r * (int64_t)T + (int64_t)kt * 64;
-  const int n = min(64, T - kt * 64);
-  uint64_t w = 0;
-  if (vec && n == 64) {
+  const int64_t nthreads = rows * NKT * 8;
+  const int64_t w = idx >> 3;            // word index (row-major over (row, kt))
+  const int c = (int)(idx & 7);
+  uint64_t piece = 0;
+  if (idx < nthreads) {
+    const int64_t r = w / NKT;
+    const int kt = (int)(w - r * NKT);
+    const int e0 = kt * 64 + c * 8;
+    const uint8_t* p = m + r * (int64_t)T + e0;
+    if (vec8 && e0 + 8 <= T) {
+      const uint64_t x = *reinterpret_cast<const uint64_t*>(p);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * c);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
-          if ((v[e] >> (8 * bb)) & 0xff) w |= 1ull << (16 * c + 4 * e + bb);
+      for (int k = 0; k < 8; ++k) piece |= (uint64_t)(((x >> (8 * k)) & 0xff) != 0) << k;
+    } else {
+      for (int k = 0; k < 8 && e0 + k < T; ++k) piece |= (uint64_t)(p[k] != 0) << k;
     }
-  } else {
-    for (int k = 0; k < n; ++k)
-      if (p[k]) w |= 1ull << k;
+    piece <<= 8 * c;
   }
-  bits[idx] = w;
+  // OR-combine the 8 pieces of the group (all lanes participate in the shuffles)
+  uint32_t lo = (uint32_t)piece, hi = (uint32_t)(piece >> 32);
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    lo |= __shfl_xor(lo, o, 64);
+    hi |= __shfl_xor(hi, o, 64);
+  }
+  if (idx < nthreads && c == 0) bits[w] = ((uint64_t)hi << 32) | lo;
 }
 
 // one thread per (b, rb, kt)
@@ -67,10 +75,10 @@ extern "C" int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_
   using namespace xdot;
   const int NKT = (T + 63) / 64;
   const int64_t rows = (int64_t)B * R;
-  const bool vec = (T % 16 == 0) && ((reinterpret_cast<uintptr_t>(mask) & 15) == 0);
-  const int64_t n1 = rows * NKT;
+  const bool vec8 = (T % 8 == 0) && ((reinterpret_cast<uintptr_t>(mask) & 7) == 0);
+  const int64_t n1 = rows * NKT * 8;
   if (n1 == 0) return 0;
-  hipLaunchKernelGGL(mask_bits_kernel, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, mask, bits, rows, T, NKT, vec);
+  hipLaunchKernelGGL(mask_bits_kernel, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, mask, bits, rows, T, NKT, vec8);
   const int64_t n2 = (int64_t)B * ((R + 31) / 32) * NKT;
   hipLaunchKernelGGL(mask_flags_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, bits, flags, B, R, T, NKT);
   return 0;

@@ -70,14 +70,15 @@ def test_flash_fwd_bwd(gpu, dt, case, mask_kind):
         mask = mask.to(gpu)
     scale = 1.0 / math.sqrt(D)
     mk = flash.prepare_mask(mask, B, R, T)
-    out, lse = flash.fwd(rows, kc, vc, mk, H, scale)
+    out, lse = flash.fwd(rows, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), mk, H, scale)
     k, q, v, ref_o, ref_lse = _ref(rows, kc, vc, mask, H, scale)
     tol = 2e-2 if dt == torch.bfloat16 else 4e-3
     assert (out.float() - ref_o).abs().max().item() < tol * 4, "fwd out"
     assert (lse - ref_lse).abs().max().item() < 1e-2, "lse"
 
     do = torch.randn(B, R, C, generator=g).to(gpu, dt)
-    drows, dkc, dvc = flash.bwd(do, rows, kc, vc, out, lse, mk, H, scale)
+    drows, dkc, dvc = flash.bwd(do, rows, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), out, lse, mk, H, scale)
+    dkc, dvc = flash.btc_to_rank_major(dkc, N), flash.btc_to_rank_major(dvc, N)
     ref_o.backward(do.float())
     dk_ref = k.grad.transpose(1, 2).reshape(B, R, C)
     dq_ref = _to_gathered(q.grad, N, B, Rc, C)
@@ -99,7 +100,8 @@ def test_flash_fully_masked_row_nan(gpu):
     kc = torch.randn(N, B, Rc, H * D, device=gpu, dtype=torch.bfloat16)
     mask = torch.zeros(B, R, N * Rc, dtype=torch.bool, device=gpu)
     mask[0, 5] = True
-    out, lse = flash.fwd(rows, kc, kc, flash.prepare_mask(mask, B, R, N * Rc), H, 0.125)
+    kb = flash.gathered_to_btc(kc)
+    out, lse = flash.fwd(rows, kb, kb, flash.prepare_mask(mask, B, R, N * Rc), H, 0.125)
     assert torch.isnan(out[0, 5]).all()
     assert not torch.isnan(out[0, 4]).any()
 
@@ -118,3 +120,32 @@ def test_mask_pack_flags(gpu):
     assert f[1, 0, 1] == 2 and f[1, 1:, :].eq(0).all()
     bits = mk.bits.cpu().view(torch.int64)
     assert bits[1, 3, 1].item() == (1 << (100 - 64))
+
+
+@pytest.mark.parametrize("nsplit", [2, 5])
+@pytest.mark.parametrize("masked", [False, True])
+def test_flash_column_split(gpu, nsplit, masked):
+    """Column-split forward (+ combine) and split row-side backward match the unsplit kernels."""
+    from xdot.ops import flash
+
+    B, R, T, H, D = 1, 150, 1000, 2, 96
+    g = torch.Generator(device="cpu").manual_seed(nsplit)
+    rows = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
+    kc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
+    vc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
+    mask = None
+    if masked:
+        mask = (torch.rand(B, R, T, generator=g) < 0.5)
+        mask[:, :, :400] = True      # whole splits fully masked for every row
+        mask[..., -1] = False
+        mask = mask.to(gpu)
+    mk = flash.prepare_mask(mask, B, R, T)
+    o1, l1 = flash.fwd(rows, kc, vc, mk, H, 0.1, nsplit=1)
+    o2, l2 = flash.fwd(rows, kc, vc, mk, H, 0.1, nsplit=nsplit)
+    assert (o1.float() - o2.float()).abs().max().item() < 2e-2
+    assert (l1 - l2).abs().max().item() < 1e-3
+    do = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
+    dkc, dvc, delta = flash.bwd_cols(do, rows, kc, vc, o1, l1, mk, H, 0.1)
+    d1 = flash.bwd_rows(do, rows, kc, vc, l1, delta, mk, H, 0.1, nsplit=1)
+    d2 = flash.bwd_rows(do, rows, kc, vc, l1, delta, mk, H, 0.1, nsplit=nsplit)
+    assert (d1.float() - d2.float()).abs().max().item() <= 2e-2 * d1.float().abs().max().item()

@@ -2,7 +2,10 @@
 ``csrc/mask_pack.hip``).
 
 Tensors are head-interleaved: ``rows`` (B, R, H*D) local query-side rows, ``kc``/``vc``
-(N, B, Rc, H*D) the rank-major gathered key/value side (T = N*Rc columns).
+(B, T, H*D) the gathered key/value side.  The RCCL all-gather produces rank-major
+(N, B, Rc, H*D); :func:`gathered_to_btc` turns that into (B, T, H*D) (a free view for B = 1)
+and :func:`btc_to_rank_major` maps the fp32 key/value-side gradients back for the
+reduce-scatter.
 """
 from __future__ import annotations
 
@@ -35,20 +38,54 @@ def prepare_mask(mask: Optional[torch.Tensor], B: int, R: int, T: int) -> Option
     return PackedMask(bits, flags, mask.shape)
 
 
+def gathered_to_btc(g: torch.Tensor) -> torch.Tensor:
+    """(N, B, Rc, C) rank-major all-gather output -> (B, N*Rc, C)."""
+    N, B, Rc, C = g.shape
+    if B == 1:
+        return g.view(1, N * Rc, C)
+    return g.permute(1, 0, 2, 3).reshape(B, N * Rc, C)
+
+
+def btc_to_rank_major(x: torch.Tensor, N: int) -> torch.Tensor:
+    """(B, T, C) -> (N, B, T/N, C) contiguous (reduce-scatter send layout)."""
+    B, T, C = x.shape
+    if B == 1:
+        return x.view(N, 1, T // N, C)
+    return x.view(B, N, T // N, C).permute(1, 0, 2, 3).contiguous()
+
+
 def _mask_args(mk: Optional[PackedMask]):
     return (mk.bits, mk.flags) if mk is not None else (None, None)
 
 
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
-        scale: float) -> Tuple[torch.Tensor, torch.Tensor]:
-    """-> (out (B, R, H*D) in rows.dtype, lse (B, H, R) fp32 natural log)."""
+        scale: float, nsplit: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> (out (B, R, H*D) in rows.dtype, lse (B, H, R) fp32 natural log).
+
+    ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU)."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_fwd(rows.contiguous(), kc.contiguous(), vc.contiguous(), bits, flags, int(H), float(scale))
+    return _ext.ops().flash_fwd(rows.contiguous(), kc.contiguous(), vc.contiguous(), bits, flags, int(H),
+                                float(scale), int(nsplit))
+
+
+def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float):
+    """Gathered-side grads -> (d_kc, d_vc (B, T, H*D) fp32 partials, delta (B, H, R))."""
+    bits, flags = _mask_args(mk)
+    return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
+                                     out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))
+
+
+def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0):
+    """Row-side grad (B, R, H*D) in rows.dtype."""
+    bits, flags = _mask_args(mk)
+    return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
+                                     lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
+                                     int(nsplit))
 
 
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,
         lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float):
-    """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (N, B, Rc, H*D) fp32 partials)."""
+    """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads)."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
                                 out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))

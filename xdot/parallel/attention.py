@@ -137,7 +137,8 @@ class SeqParallelAttention(torch.autograd.Function):
         if use_hip:
             from ..ops import flash
 
-            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qg.shape[0] * qg.shape[2]) if mask is not None else None
+            qg, vg = flash.gathered_to_btc(qg), flash.gathered_to_btc(vg)
+            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qg.shape[1]) if mask is not None else None
             o, lse = flash.fwd(k, qg, vg, mk, H, scale)
         else:
             mk = mask
@@ -150,24 +151,32 @@ class SeqParallelAttention(torch.autograd.Function):
     def backward(ctx, do):
         k, qg, vg, o, lse = ctx.saved_tensors
         comm, H, scale = ctx.comm, ctx.H, ctx.scale
+        n = comm.world_size
         do = do.contiguous()
+
+        def reduce_async(parts):
+            if n == 1:
+                return None, parts[0]
+            out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
+            return comm.reduce_scatter(out, parts, async_op=True), out
+
         if ctx.use_hip:
             from ..ops import flash
 
-            dk, dq_parts, dv_parts = flash.bwd(do, k, qg, vg, o, lse, ctx.mk, H, scale)
+            # 1) gathered-side grads for all T columns, 2) their reduce-scatter runs on the
+            #    collective stream WHILE 3) the row-side kernel computes dk
+            dq_parts, dv_parts, delta = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale)
+            h1, dq = reduce_async(flash.btc_to_rank_major(dq_parts, n))
+            h2, dv = reduce_async(flash.btc_to_rank_major(dv_parts, n))
+            dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
         else:
             dk, dq_parts, dv_parts = _ref_bwd(do, k, qg, vg, o, lse, ctx.mk, H, scale)
-        n = comm.world_size
-        if n == 1:
-            dq, dv = dq_parts[0], dv_parts[0]
-        else:
-            dq = torch.empty(dq_parts.shape[1:], dtype=dq_parts.dtype, device=dq_parts.device)
-            dv = torch.empty(dv_parts.shape[1:], dtype=dv_parts.dtype, device=dv_parts.device)
-            h1 = comm.reduce_scatter(dq, dq_parts, async_op=True)
-            h2 = comm.reduce_scatter(dv, dv_parts, async_op=True)
-            h1.wait()
-            h2.wait()
-        return dk.to(k.dtype), dq.to(qg.dtype), dv.to(vg.dtype), None, None, None, None
+            h1, dq = reduce_async(dq_parts)
+            h2, dv = reduce_async(dv_parts)
+        for h in (h1, h2):
+            if h is not None:
+                h.wait()
+        return dk.to(k.dtype), dq.to(k.dtype), dv.to(k.dtype), None, None, None, None
 
 
 def seq_parallel_attention(k: Tensor, q: Tensor, v: Tensor, mask: Optional[Tensor], num_heads: int,
