@@ -1,0 +1,97 @@
+"""Kernel-level timing of the flash-attention kernels at the headline shape (per rank).
+
+    python benchmarks/bench_flash.py                       # T=25000, R=25000 (N=1), H=8, D=96
+    python benchmarks/bench_flash.py --R 3125              # the per-rank shape at N=8
+    python benchmarks/bench_flash.py --only fwd --iters 20 # (for rocprofv3 --pmc runs)
+
+Prints one JSON line per kernel: median ms over ``--iters`` HIP-event timed calls and the
+achieved TFLOP/s (fwd: 2 GEMMs, bwd_rows: 3, bwd_cols: 4; 2*R*T*H*D FLOP each), plus the
+materialised reference path (torch SDPA math on the same shape) when ``--torch`` is given.
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters, warmup=2):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", type=int, default=25000)
+    ap.add_argument("--R", type=int, default=None)
+    ap.add_argument("--H", type=int, default=8)
+    ap.add_argument("--D", type=int, default=96)
+    ap.add_argument("--B", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="all", choices=["all", "fwd", "bwd_cols", "bwd_rows", "mask"])
+    ap.add_argument("--mask", action="store_true", help="pass an all-False (B, R, T) mask")
+    ap.add_argument("--nsplit", type=int, default=0)
+    ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
+    a = ap.parse_args()
+    from xdot.ops import flash
+
+    dev = torch.device("cuda", 0)
+    B, T, H, D = a.B, a.T, a.H, a.D
+    R = a.R or T
+    C = H * D
+    g = torch.Generator(device=dev).manual_seed(0)
+    rows = torch.randn(B, R, C, device=dev, dtype=torch.bfloat16, generator=g)
+    qv = torch.randn(B, T, 2 * C, device=dev, dtype=torch.bfloat16, generator=g)
+    kc, vc = qv[..., :C], qv[..., C:]
+    do = torch.randn(B, R, C, device=dev, dtype=torch.bfloat16, generator=g)
+    mask = torch.zeros(B, R, T, dtype=torch.bool, device=dev) if a.mask else None
+    mk = flash.prepare_mask(mask, B, R, T)
+    scale = 1.0 / math.sqrt(D)
+    out, lse = flash.fwd(rows, kc, vc, mk, H, scale, a.nsplit)
+    dkv, delta = flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale)
+    gemm = 2.0 * B * R * T * H * D
+    res = []
+    if a.only in ("all", "mask") and mask is not None:
+        ms, mn = timeit(lambda: flash.prepare_mask(mask, B, R, T), a.iters)
+        res.append({"kernel": "mask_pack", "ms": ms, "min_ms": mn, "GB_s": B * R * T / ms / 1e6})
+    if a.only in ("all", "fwd"):
+        ms, mn = timeit(lambda: flash.fwd(rows, kc, vc, mk, H, scale, a.nsplit), a.iters)
+        res.append({"kernel": "flash_fwd", "ms": ms, "min_ms": mn, "TFLOPs": 2 * gemm / ms / 1e9})
+    if a.only in ("all", "bwd_cols"):
+        ms, mn = timeit(lambda: flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale), a.iters)
+        res.append({"kernel": "flash_bwd_cols", "ms": ms, "min_ms": mn, "TFLOPs": 4 * gemm / ms / 1e9})
+    if a.only in ("all", "bwd_rows"):
+        ms, mn = timeit(lambda: flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale, a.nsplit), a.iters)
+        res.append({"kernel": "flash_bwd_rows", "ms": ms, "min_ms": mn, "TFLOPs": 3 * gemm / ms / 1e9})
+    if a.torch and R == T:
+        q = rows.view(B, R, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+        k = kc.reshape(B, T, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+        v = vc.reshape(B, T, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+        f = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v)  # noqa: E731
+        ms, mn = timeit(f, a.iters)
+        res.append({"kernel": "torch_sdpa_fwd", "ms": ms, "min_ms": mn, "TFLOPs": 2 * gemm / ms / 1e9})
+        o = f()
+        gout = torch.randn_like(o)
+        ms, mn = timeit(lambda: torch.autograd.grad(f(), (q, k, v), gout), a.iters)
+        res.append({"kernel": "torch_sdpa_fwd+bwd", "ms": ms, "min_ms": mn, "TFLOPs": 7 * gemm / ms / 1e9})
+    for r in res:
+        r.update({"B": B, "R": R, "T": T, "H": H, "D": D})
+        print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
+if __name__ == "__main__":
+    main()

@@ -148,23 +148,31 @@ std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
 }
 
 struct FlashGeom {
-  int64_t B, R, C, T, D;
+  int64_t B, R, C, T, D, ld;
 };
 
+// rows: contiguous (B, R, C).  kc / vc: (B, T, C) views with unit inner stride and a common
+// row stride `ld` (C for separate tensors, 2C for the two halves of a packed [q | v]).
 FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc, int64_t H,
                       const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags) {
   TORCH_CHECK(rows.is_cuda() && kc.is_cuda() && vc.is_cuda(), "xdot.flash: GPU tensors required");
-  TORCH_CHECK(rows.is_contiguous() && kc.is_contiguous() && vc.is_contiguous(), "xdot.flash: contiguous tensors required");
+  TORCH_CHECK(rows.is_contiguous(), "xdot.flash: rows must be contiguous");
   TORCH_CHECK(rows.scalar_type() == kc.scalar_type() && rows.scalar_type() == vc.scalar_type(), "xdot.flash: dtype mismatch");
   TORCH_CHECK(rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kHalf, "xdot.flash: bf16/fp16 only");
   TORCH_CHECK(rows.dim() == 3 && kc.dim() == 3 && vc.sizes() == kc.sizes(), "xdot.flash: rows (B,R,C), cols (B,T,C)");
-  FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(1), 0};
+  FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(1), 0, kc.stride(1)};
   TORCH_CHECK(kc.size(0) == g.B && kc.size(2) == g.C, "xdot.flash: batch / feature mismatch");
   TORCH_CHECK(g.T > 0, "xdot.flash: empty key side");
+  for (const at::Tensor* t : {&kc, &vc}) {
+    TORCH_CHECK(t->stride(2) == 1 && t->stride(1) == g.ld && (g.B == 1 || t->stride(0) == g.T * g.ld),
+                "xdot.flash: key/value side must be (B, T, C) rows with a common row stride");
+    TORCH_CHECK((g.B - 1) * g.T * g.ld + (g.T - 1) * g.ld + g.C <= avail_elems(*t), "xdot.flash: key/value out of bounds");
+  }
+  TORCH_CHECK(g.ld % 8 == 0 && g.ld >= g.C, "xdot.flash: row stride must be a multiple of 8 elements");
   TORCH_CHECK(H > 0 && g.C % H == 0, "xdot.flash: C not divisible by heads");
   g.D = g.C / H;
   TORCH_CHECK(g.D == 32 || g.D == 64 || g.D == 96 || g.D == 128, "xdot.flash: head dim must be 32/64/96/128");
-  TORCH_CHECK(g.T < (1LL << 31) && g.R < (1LL << 31) && g.B * H * ((g.R + 127) / 128) < (1LL << 31), "xdot.flash: too large");
+  TORCH_CHECK(g.T < (1LL << 31) && g.R < (1LL << 31) && g.B * H * ((g.R + 127) / 128) * 8 < (1LL << 31), "xdot.flash: too large");
   TORCH_CHECK(aligned16(rows.data_ptr()) && aligned16(kc.data_ptr()) && aligned16(vc.data_ptr()), "xdot.flash: 16-byte alignment");
   const bool hb = bits.has_value() && bits->defined(), hf = flags.has_value() && flags->defined();
   TORCH_CHECK(hb == hf, "xdot.flash: mask bits and flags go together");
@@ -206,6 +214,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
   a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
   a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.scale = (float)scale;
+  a.ldkv = g.ld;
   a.nsplit = ns;
   a.opart = ns > 1 ? opart.data_ptr<float>() : nullptr;
   a.lpart = ns > 1 ? lpart.data_ptr<float>() : nullptr;
@@ -228,12 +237,14 @@ xdot::fa::BwdArgs bwd_args(const FlashGeom& g, const at::Tensor& dout, const at:
   a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
   a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
   a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.scale = (float)scale;
+  a.ldkv = g.ld;
   a.nsplit = 1;
   return a;
 }
 
-// gathered-side grads (fp32 (B, T, C) partials for the reduce-scatter) + δ = rowsum(dO·O)
-std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const at::Tensor& rows,
+// gathered-side grads, packed fp32 (B, T, 2C) = [dq | dv] partials for ONE reduce-scatter,
+// + δ = rowsum(dO·O)
+std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const at::Tensor& rows,
                                                               const at::Tensor& kc, const at::Tensor& vc,
                                                               const at::Tensor& out, const at::Tensor& lse,
                                                               const c10::optional<at::Tensor>& bits,
@@ -243,15 +254,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& 
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
-  auto dkc = at::empty(kc.sizes(), kc.options().dtype(at::kFloat));
-  auto dvc = at::empty(vc.sizes(), vc.options().dtype(at::kFloat));
+  auto dkv = at::empty({g.B, g.T, 2 * g.C}, kc.options().dtype(at::kFloat));
   auto delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
-  a.dkc = dkc.data_ptr<float>(); a.dvc = dvc.data_ptr<float>();
+  a.dkc = dkv.data_ptr<float>(); a.dvc = dkv.data_ptr<float>() + g.C; a.ldg = 2 * g.C;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(rows.scalar_type()),
                                          (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
   check_launch(hipGetLastError(), "flash_bwd_cols");
-  return {dkc, dvc, delta};
+  return {dkv, delta};
 }
 
 // row-side grad (this rank's rows), column-split when the row count is small
@@ -279,9 +289,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd(const at::Tensor& dout,
                                                          const at::Tensor& vc, const at::Tensor& out, const at::Tensor& lse,
                                                          const c10::optional<at::Tensor>& bits,
                                                          const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
-  auto [dkc, dvc, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale);
+  auto [dkv, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale);
   auto drows = flash_bwd_rows(dout, rows, kc, vc, lse, delta, bits, flags, H, scale, 0);
-  return {drows, dkc, dvc};
+  const int64_t C = rows.size(2);
+  return {drows, dkv.narrow(2, 0, C), dkv.narrow(2, C, C)};
 }
 
 }  // namespace
@@ -295,7 +306,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor)");
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
-        "Tensor? flags, int H, float scale) -> (Tensor, Tensor, Tensor)");
+        "Tensor? flags, int H, float scale) -> (Tensor, Tensor)");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
   m.def("flash_bwd(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, Tensor? flags, "

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = min(kt * 64 + r, a.T - 1);
-      const int64_t off = col_off(t, b, a.T, C) + c * 8;
+      const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
       rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
       rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
     }
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
 
   u32x4 qf[KS], vf[KS];
   {
-    const int64_t off = col_off(col_ok ? col : 0, b, a.T, C) + h * D + 8 * hf;
+    const int64_t off = col_off(col_ok ? col : 0, b, a.T, a.ldkv) + h * D + 8 * hf;
     const T16* pq = reinterpret_cast<const T16*>(a.kc) + off;
     const T16* pv = reinterpret_cast<const T16*>(a.vc) + off;
 #pragma unroll
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
     __syncthreads();
   }
   if (col_ok) {
-    const int64_t off = col_off(col, b, a.T, C) + h * D;
+    const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
     float* pq = a.dkc + off;
     float* pv = a.dvc + off;
 #pragma unroll

@@ -4,8 +4,9 @@
 //   "rows"  = local query-side rows of this rank (the module's projected `keys`, R rows)
 //   "cols"  = gathered key-side rows (the module's projected `queries`/`values`, T rows)
 //   All tensors are head-interleaved (..., H*D) so no transpose copies exist anywhere.
-//   Gathered tensors are (B, T, C): col t of batch b lives at (b*T + t)*C + h*D (the RCCL
-//   all-gather output (N, 1, R, C) is exactly this layout for B = 1).
+//   Gathered tensors are (B, T, ld): col t of batch b lives at (b*T + t)*ld + h*D (the RCCL
+//   all-gather output (N, 1, R, ld) is exactly this layout for B = 1).  With the packed
+//   [q | v] projection ld = 2*H*D and v starts H*D elements after q.
 // MFMA: v_mfma_f32_32x32x16_{bf16,f16}.  For a 32x32 accumulator X, lane l holds column
 // l&31 and rows (r&3) + 8*(r>>2) + 4*(l>>5), r = 0..15 (CDNA4 C/D map).
 #pragma once
@@ -77,9 +78,9 @@ __device__ __forceinline__ u32x4 row_frag(const char* img, int row_stride, int r
   return *reinterpret_cast<const u32x4*>(img + (r0 + (lane & 31)) * row_stride + (16 * s + 8 * (lane >> 5)) * 2);
 }
 
-// global element offset of gathered col t (head offset excluded)
-__device__ __forceinline__ int64_t col_off(int t, int b, int T, int C) {
-  return ((int64_t)b * T + t) * C;
+// global element offset of gathered col t (head offset excluded); ld = row stride
+__device__ __forceinline__ int64_t col_off(int t, int b, int T, int64_t ld) {
+  return ((int64_t)b * T + t) * ld;
 }
 
 // v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;

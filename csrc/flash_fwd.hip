@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       // rows past T read row T-1: their scores are masked to -inf, so P = 0 multiplies
       // finite values (no branch around the loads)
       const int t = min(kt * 64 + r, a.T - 1);
-      const int64_t off = col_off(t, b, a.T, C) + c * 8;
+      const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
       rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
       rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
     }

@@ -37,13 +37,14 @@ struct Args {
 namespace fa {
 struct FwdArgs {
   const void* rows;        // (B, R, H*D)
-  const void* kc;          // gathered key side (B, T, H*D)
-  const void* vc;          // gathered value side (B, T, H*D)
+  const void* kc;          // gathered key side (B, T, ldkv), first H*D columns used
+  const void* vc;          // gathered value side (B, T, ldkv)
   void* out;               // (B, R, H*D)
   float* lse;              // (B, H, R) natural-log LSE
   const uint64_t* mbits;   // (B, R, NKT) bit k = col kt*64+k masked, or null
   const uint8_t* mflags;   // (B, ceil(R/32), NKT) 0 none / 1 all / 2 partial, or null
   int B, H, R, T;
+  int64_t ldkv;            // element stride between gathered rows (H*D, or 2*H*D when packed [q|v])
   float scale;             // softmax scale (not log2-scaled)
   int nsplit;              // column splits (>1: partials to opart/lpart, then combine)
   float* opart;            // (nsplit, B, R, H*D) fp32 normalised partial outputs
@@ -58,11 +59,13 @@ struct BwdArgs {
   const float* lse;        // (B, H, R)
   const float* delta;      // (B, H, R) rowsum(dO * O)
   void* drows;             // (B, R, H*D)   grad of row side (out dtype)
-  float* dkc;              // (B, T, H*D) fp32 partial grads of the gathered key side
-  float* dvc;              // (B, T, H*D) fp32 partial grads of the gathered value side
+  float* dkc;              // (B, T, ldkv) fp32 partial grads of the gathered key side
+  float* dvc;              // (B, T, ldkv) fp32 partial grads of the gathered value side
   const uint64_t* mbits;
   const uint8_t* mflags;
   int B, H, R, T;
+  int64_t ldkv;            // element stride between gathered input rows
+  int64_t ldg;             // element stride between rows of the fp32 dkc/dvc outputs
   float scale;
   int nsplit;              // column splits of the row-side kernel
   float* dpart;            // (nsplit, B, R, H*D) fp32 partial row-side grads (nsplit > 1)

@@ -74,17 +74,28 @@ class DistributedDotProductAttn(nn.Module):
 
     def forward(self, keys: Tensor, queries: Tensor, values: Tensor, attn_mask: Optional[Tensor] = None) -> Tensor:
         k = self.keys(keys)
-        q = self.queries(queries)
-        v = self.values(values)
         scale = 1.0 / math.sqrt(self.dim)
         impl = self._pick_impl(k)
         if impl == "flash":
-            from ..parallel.attention import seq_parallel_attention
+            from ..parallel.attention import seq_parallel_attention_packed
 
             comm = (self.comm or _comm.get_comm()) if self.distributed else _comm.LocalComm()
-            o = seq_parallel_attention(k, q, v, attn_mask, self.num_heads, scale, comm=comm)
-            return self.composition(o)
+            return self.composition(seq_parallel_attention_packed(k, self._project_qv(queries, values), attn_mask,
+                                                                  self.num_heads, scale, comm=comm))
+        q = self.queries(queries)
+        v = self.values(values)
         return self.composition(self._materialized(k, q, v, attn_mask, scale))
+
+    def _project_qv(self, queries: Tensor, values: Tensor) -> Tensor:
+        """[q | v] packed (B, R, 2C): ONE GEMM when ``queries is values`` (self-attention), so
+        the gathered side travels in one all-gather and its grads in one reduce-scatter."""
+        if queries is values and self.queries.in_features == self.values.in_features:
+            w = torch.cat([self.queries.weight, self.values.weight], 0)
+            b = None
+            if self.queries.bias is not None:
+                b = torch.cat([self.queries.bias, self.values.bias], 0)
+            return torch.nn.functional.linear(queries, w, b)
+        return torch.cat([self.queries(queries), self.values(values)], dim=-1)
 
     def _materialized(self, k, q, v, attn_mask, scale):
         H = self.num_heads

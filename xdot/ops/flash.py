@@ -54,6 +54,13 @@ def btc_to_rank_major(x: torch.Tensor, N: int) -> torch.Tensor:
     return x.view(B, N, T // N, C).permute(1, 0, 2, 3).contiguous()
 
 
+def _kv(x: torch.Tensor) -> torch.Tensor:
+    """key/value-side operand: (B, T, C) with unit inner stride (row stride may exceed C)."""
+    if x.dim() == 3 and x.stride(-1) == 1 and x.stride(1) % 8 == 0 and (x.shape[0] == 1 or x.stride(0) == x.shape[1] * x.stride(1)):
+        return x
+    return x.contiguous()
+
+
 def _mask_args(mk: Optional[PackedMask]):
     return (mk.bits, mk.flags) if mk is not None else (None, None)
 
@@ -64,21 +71,20 @@ def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[Pac
 
     ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU)."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_fwd(rows.contiguous(), kc.contiguous(), vc.contiguous(), bits, flags, int(H),
-                                float(scale), int(nsplit))
+    return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit))
 
 
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float):
-    """Gathered-side grads -> (d_kc, d_vc (B, T, H*D) fp32 partials, delta (B, H, R))."""
+    """Gathered-side grads -> (packed fp32 [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R))."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
+    return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0):
     """Row-side grad (B, R, H*D) in rows.dtype."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
+    return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
                                      int(nsplit))
 
@@ -87,5 +93,5 @@ def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tens
         lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float):
     """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads)."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_bwd(dout.contiguous(), rows.contiguous(), kc.contiguous(), vc.contiguous(),
+    return _ext.ops().flash_bwd(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                 out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))

@@ -35,7 +35,7 @@ from .. import _ext
 from ..utils import comm as _comm
 from ..utils.checks import check_consistent
 
-__all__ = ["seq_parallel_attention", "flash_supported", "SeqParallelAttention"]
+__all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "flash_supported", "SeqParallelAttention"]
 
 FLASH_HEAD_DIMS = (32, 64, 96, 128)
 
@@ -127,34 +127,38 @@ def _ref_bwd(do, k, qg, vg, o, lse, mask, H, scale):
 
 # ----------------------------------------------------------------------------------------
 class SeqParallelAttention(torch.autograd.Function):
+    """Fused seq-parallel attention on a PACKED gathered-side operand ``qv`` = [q | v]
+    (B, R, 2C): one all-gather in forward, one reduce-scatter in backward."""
+
     @staticmethod
-    def forward(ctx, k, q, v, mask, H, scale, comm):
-        check_consistent(comm, "seq_parallel_attention", k, q, v, H)
-        hq = _gather_rows(comm, q)
-        hv = _gather_rows(comm, v)
-        qg, vg = hq.wait(), hv.wait()
+    def forward(ctx, k, qv, mask, H, scale, comm):
+        check_consistent(comm, "seq_parallel_attention", k, qv, H)
+        C = k.shape[-1]
+        qvg = _gather_rows(comm, qv).wait()                    # (N, B, R, 2C)
         use_hip = _ext.use_hip(k) and k.dtype in (torch.bfloat16, torch.float16)
         if use_hip:
             from ..ops import flash
 
-            qg, vg = flash.gathered_to_btc(qg), flash.gathered_to_btc(vg)
-            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qg.shape[1]) if mask is not None else None
+            qvg = flash.gathered_to_btc(qvg)                    # (B, T, 2C), a view for B = 1
+            qg, vg = qvg[..., :C], qvg[..., C:]
+            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qvg.shape[1]) if mask is not None else None
             o, lse = flash.fwd(k, qg, vg, mk, H, scale)
         else:
             mk = mask
-            o, lse = _ref_fwd(k, qg, vg, mask, H, scale)
-        ctx.save_for_backward(k, qg, vg, o, lse)
+            o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
+        ctx.save_for_backward(k, qvg, o, lse)
         ctx.mk, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mk, H, scale, comm, use_hip
         return o
 
     @staticmethod
     def backward(ctx, do):
-        k, qg, vg, o, lse = ctx.saved_tensors
+        k, qvg, o, lse = ctx.saved_tensors
         comm, H, scale = ctx.comm, ctx.H, ctx.scale
         n = comm.world_size
+        C = k.shape[-1]
         do = do.contiguous()
 
-        def reduce_async(parts):
+        def reduce_async(parts):  # (N, B, R, 2C) rank-major fp32 partials
             if n == 1:
                 return None, parts[0]
             out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
@@ -163,20 +167,32 @@ class SeqParallelAttention(torch.autograd.Function):
         if ctx.use_hip:
             from ..ops import flash
 
-            # 1) gathered-side grads for all T columns, 2) their reduce-scatter runs on the
-            #    collective stream WHILE 3) the row-side kernel computes dk
-            dq_parts, dv_parts, delta = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale)
-            h1, dq = reduce_async(flash.btc_to_rank_major(dq_parts, n))
-            h2, dv = reduce_async(flash.btc_to_rank_major(dv_parts, n))
+            qg, vg = qvg[..., :C], qvg[..., C:]
+            # 1) gathered-side grads for all T columns -> 2) ONE reduce-scatter on the collective
+            #    stream, running WHILE 3) the row-side kernel computes dk
+            dkv, delta = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale)
+            h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
             dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
         else:
-            dk, dq_parts, dv_parts = _ref_bwd(do, k, qg, vg, o, lse, ctx.mk, H, scale)
-            h1, dq = reduce_async(dq_parts)
-            h2, dv = reduce_async(dv_parts)
-        for h in (h1, h2):
-            if h is not None:
-                h.wait()
-        return dk.to(k.dtype), dq.to(k.dtype), dv.to(k.dtype), None, None, None, None
+            dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mk, H, scale)
+            h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))
+        if h is not None:
+            h.wait()
+        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None
+
+
+def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,
+                                  comm: Optional[_comm.Communicator] = None) -> Tensor:
+    """Fused sequence-parallel attention with a packed gathered side ``qv = [q | v]`` (B, R, 2C)."""
+    comm = comm or _comm.get_comm()
+    if k.dim() != 3 or qv.dim() != 3 or qv.shape[-1] <= k.shape[-1]:
+        raise ValueError("seq_parallel_attention_packed expects k (B, R, C) and qv (B, R, C + Cv)")
+    if mask is not None:
+        T = qv.shape[1] * comm.world_size
+        if tuple(mask.shape) != (k.shape[0], k.shape[1], T):
+            raise ValueError(f"mask must be (B, R, T)=({k.shape[0]}, {k.shape[1]}, {T}), got {tuple(mask.shape)}")
+        mask = mask.to(torch.bool)
+    return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm)
 
 
 def seq_parallel_attention(k: Tensor, q: Tensor, v: Tensor, mask: Optional[Tensor], num_heads: int,
@@ -186,12 +202,6 @@ def seq_parallel_attention(k: Tensor, q: Tensor, v: Tensor, mask: Optional[Tenso
     ``k``: row side (local rows), ``q``/``v``: gathered side (local shards), ``mask``: bool
     (B, R, T) with True = masked, or None.  Returns (B, R, H*dv) in ``k``'s dtype.
     """
-    comm = comm or _comm.get_comm()
     if k.dim() != 3 or q.dim() != 3 or v.dim() != 3:
         raise ValueError("seq_parallel_attention expects (B, R, H*d) tensors")
-    if mask is not None:
-        T = q.shape[1] * comm.world_size
-        if tuple(mask.shape) != (k.shape[0], k.shape[1], T):
-            raise ValueError(f"mask must be (B, R, T)=({k.shape[0]}, {k.shape[1]}, {T}), got {tuple(mask.shape)}")
-        mask = mask.to(torch.bool)
-    return SeqParallelAttention.apply(k, q, v, mask, num_heads, float(scale), comm)
+    return seq_parallel_attention_packed(k, torch.cat([q, v], dim=-1), mask, num_heads, scale, comm)
