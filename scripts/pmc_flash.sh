@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC counters for the flash kernels (separate rocprofv3 pass per counter group; no tracing).
+set -o pipefail
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-pmc}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d $OUT/g$i -o pmc --output-format csv \
+    -- python3 $GRAFT_REPO_ROOT/benchmarks/bench_flash.py --iters 3 > $OUT/g$i.log 2>&1 || echo "group $i failed rc=$?" >> $OUT/errors.log
+done
