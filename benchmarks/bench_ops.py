@@ -34,7 +34,9 @@ sys.path.insert(0, ROOT)
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description="xdot distributed op benchmark (reference-compatible)")
-    ap.add_argument("--mode", default="nt", choices=["nt", "all", "tn"])
+    ap.add_argument("--mode", default="nt", choices=["nt", "all", "tn", "rightT_fb", "full_fb", "leftT_fb"],
+                    help="nt/all/tn: forward of the distributed product (reference modes); "
+                         "*_fb: forward+backward of the corresponding autograd op")
     ap.add_argument("--offset", type=int, default=None, help="chunk size (default: whole shard)")
     ap.add_argument("--scale", type=int, default=1, help="T = 75000 // scale (reference semantics)")
     ap.add_argument("--T", type=int, default=None)
@@ -111,8 +113,10 @@ def main(argv=None):
     torch.set_grad_enabled(False)
     rec = {"mode": a.mode, "world_size": n, "T": T, "D": D, "offset": a.offset, "dtype": a.dtype}
 
+    fb = a.mode.endswith("_fb")
+    torch.set_grad_enabled(fb)
     # single-GPU torch baseline on the full problem (reference: rank 0 only)
-    if rank == 0 and not a.no_local:
+    if rank == 0 and not a.no_local and not fb:
         _peak_reset()
         if a.mode == "nt":
             x = torch.rand(1, T, D, device=dev, dtype=dt)
@@ -141,11 +145,24 @@ def main(argv=None):
         left = torch.rand(1, R, T, device=dev, dtype=dt)
         right = torch.rand(1, R, D, device=dev, dtype=dt)
         fn = lambda l, r: F.distributed_matmul_all(l, r, a.offset)  # noqa: E731
-    else:
+    elif a.mode == "tn":
         left = torch.rand(1, R, T, device=dev, dtype=dt)
         right = torch.rand(1, R, D, device=dev, dtype=dt)
         fn = lambda l, r: F.distributed_matmul_tn(l, r)  # noqa: E731
-    fn.__name__ = f"distributed_matmul_{a.mode}"
+    else:
+        import xdot.parallel.autograd as A
+
+        op = {"rightT_fb": A.RightTransposeMultiplication, "full_fb": A.FullMultiplication,
+              "leftT_fb": A.LeftTransposeMultiplication}[a.mode]
+        lshape = (1, R, D) if a.mode == "rightT_fb" else (1, R, T)
+        left = torch.rand(*lshape, device=dev, dtype=dt, requires_grad=True)
+        right = torch.rand(1, R, D, device=dev, dtype=dt, requires_grad=True)
+
+        def fn(l, r):
+            out = op.apply(l, r, a.offset)
+            out.backward(torch.ones_like(out))
+            return out.detach()
+    fn.__name__ = f"distributed_{a.mode}"
     din = _mem()
     comm.barrier()
     y, t_cold, pk = cold_call(fn, left, right)

@@ -138,7 +138,7 @@ std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
   const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
   const int64_t NKT = (T + 63) / 64;
   auto bits = at::empty({B, R, NKT}, m.options().dtype(at::kLong));
-  auto flags = at::empty({B, (R + 31) / 32, NKT}, m.options().dtype(at::kByte));
+  auto flags = at::empty({B, (R + 31) / 32, (NKT + 3) & ~3}, m.options().dtype(at::kByte));
   TORCH_CHECK(B * R * NKT < (1LL << 40) && T < (1LL << 31), "xdot.mask_pack: too large");
   c10::DeviceGuard guard(m.device());
   xdot_mask_pack_launch(reinterpret_cast<const uint8_t*>(m.data_ptr()), reinterpret_cast<uint64_t*>(bits.data_ptr()),
@@ -179,7 +179,9 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   if (hb) {
     const int64_t NKT = (g.T + 63) / 64;
     TORCH_CHECK(bits->is_contiguous() && bits->numel() == g.B * g.R * NKT, "xdot.flash: mask bits shape");
-    TORCH_CHECK(flags->is_contiguous() && flags->numel() == g.B * ((g.R + 31) / 32) * NKT, "xdot.flash: mask flags shape");
+    TORCH_CHECK(flags->is_contiguous() && flags->numel() == g.B * ((g.R + 31) / 32) * ((NKT + 3) & ~3),
+                "xdot.flash: mask flags shape");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(flags->data_ptr()) & 3) == 0, "xdot.flash: flags alignment");
   }
   return g;
 }

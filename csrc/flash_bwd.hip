@@ -58,12 +58,12 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 template <int DT, int D>
 __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int ROWB = Geo<D>::ROWB;
-  constexpr int QS_BYTES = 64 * ROWB, STAGE = 2 * QS_BYTES;
+  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * QS_BYTES;
   constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const Lanes L = make_lanes<D>(lane);
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int rb = lin % nrb, bhs = lin / nrb;
@@ -96,13 +96,34 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   const float NEG_INF = -__builtin_inff();
 
   u32x4 rq[LPT], rv[LPT];
-  auto load_tile = [&](int kt) {
+  uint32_t soff[LPT];
+  int stoff[LPT];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = min(kt * 64 + r, a.T - 1);
-      const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
-      rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-      rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+  for (int i = 0; i < LPT; ++i) {
+    const int v = tid + 256 * i;
+    soff[i] = (uint32_t)(((v / CPR) * a.ldkv + (v % CPR) * 8) * 2);
+    stoff[i] = img_off<D>(v / CPR, v % CPR);
+  }
+  const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
+  const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
+  auto load_tile = [&](int kt) {
+    const int64_t t0 = (int64_t)kt * 64;
+    if (t0 + 64 <= a.T) {
+      const char* bq = kcb + t0 * a.ldkv * 2;
+      const char* bv = vcb + t0 * a.ldkv * 2;
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        rq[i] = *reinterpret_cast<const u32x4*>(bq + soff[i]);
+        rv[i] = *reinterpret_cast<const u32x4*>(bv + soff[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = min(kt * 64 + r, a.T - 1);
+        const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
+        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -111,8 +132,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(qs + r * ROWB + c * 16) = rq[i];
-      *reinterpret_cast<u32x4*>(vs + r * ROWB + c * 16) = rv[i];
+      *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
+      *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
     }
   };
 
@@ -121,7 +142,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   for (int i = 0; i < DB; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
-  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
+  const int NKT4 = (NKT + 3) & ~3;
+  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
   const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
   load_tile(kt_beg);
@@ -129,23 +151,23 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   __syncthreads();
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const int cur = (kt - kt_beg) & 1;
+    const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
+    const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
     if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
-    const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
-      const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
       const bool chk = flag == 2 || tail;
       // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        f32x16 s = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, 0, lane), kf[0], f32x16{});
-        f32x16 dp = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, 0, lane), df[0], f32x16{});
+        f32x16 s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, 0, L), kf[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, 0, L), df[0], f32x16{});
 #pragma unroll
         for (int ks = 1; ks < KS; ++ks) {
-          s = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s);
-          dp = mfma32<DT>::run(row_frag(vs, ROWB, tt * 32, ks, lane), df[ks], dp);
+          s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s);
+          dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, ks, L), df[ks], dp);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -159,8 +181,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
         const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
 #pragma unroll
         for (int db = 0; db < DB; ++db) {
-          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, tt * 32, db * 32, lane), f0, dk[db]);
-          dk[db] = mfma32<DT>::run(tr_frag(qs, ROWB, tt * 32 + 16, db * 32, lane), f1, dk[db]);
+          dk[db] = mfma32<DT>::run(tr_frag<D>(qs, tt * 32, db * 32, L), f0, dk[db]);
+          dk[db] = mfma32<DT>::run(tr_frag<D>(qs, tt * 32 + 16, db * 32, L), f1, dk[db]);
         }
       }
     }
@@ -195,13 +217,13 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
 template <int DT, int D>
 __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int ROWB = Geo<D>::ROWB;
-  constexpr int IMG = 64 * ROWB;
+  constexpr int IMG = Img<D>::BYTES;
   constexpr int STAGE = 2 * IMG + 64 * 4 * 2 + 64 * 8 * 2;  // K, dO, lse2[64], delta[64], words[2][64]
   constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const Lanes L = make_lanes<D>(lane);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int cb = lin % ncb, bh = lin / ncb;
@@ -236,14 +258,35 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
   const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
 
   u32x4 rk[LPT], rd[LPT];
-  auto load_tile = [&](int rt) {
+  uint32_t soff[LPT];
+  int stoff[LPT];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      // rows past R re-read row R-1 (finite); their lse = +inf below makes P = dS = 0
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = min(rt * 64 + r, a.R - 1);
-      const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
-      rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
-      rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
+  for (int i = 0; i < LPT; ++i) {
+    const int v = tid + 256 * i;
+    soff[i] = (uint32_t)(((v / CPR) * C + (v % CPR) * 8) * 2);
+    stoff[i] = img_off<D>(v / CPR, v % CPR);
+  }
+  const char* rowsb = reinterpret_cast<const char*>(rows + (int64_t)b * a.R * C);
+  const char* doutb = reinterpret_cast<const char*>(dout + (int64_t)b * a.R * C);
+  auto load_tile = [&](int rt) {
+    const int64_t r0t = (int64_t)rt * 64;
+    if (r0t + 64 <= a.R) {
+      const char* bk = rowsb + r0t * C * 2;
+      const char* bd = doutb + r0t * C * 2;
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        rk[i] = *reinterpret_cast<const u32x4*>(bk + soff[i]);
+        rd[i] = *reinterpret_cast<const u32x4*>(bd + soff[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        // rows past R re-read row R-1 (finite); their lse = +inf below makes P = dS = 0
+        const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = min(rt * 64 + r, a.R - 1);
+        const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
+        rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
+        rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
+      }
     }
   };
   // the per-row lse/δ/mask words go global -> LDS right here (short register lifetime)
@@ -256,8 +299,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(ks + r * ROWB + c * 16) = rk[i];
-      *reinterpret_cast<u32x4*>(ds + r * ROWB + c * 16) = rd[i];
+      *reinterpret_cast<u32x4*>(ks + stoff[i]) = rk[i];
+      *reinterpret_cast<u32x4*>(ds + stoff[i]) = rd[i];
     }
     if (tid < 64) {
       const int rr = rt * 64 + tid;
@@ -289,20 +332,22 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
     const uint64_t* ws = reinterpret_cast<const uint64_t*>(dls + 64);
     int flag = 0;
     if (a.mflags && c0 < a.T) {
-      const uint8_t* fl = a.mflags + (int64_t)b * NRB32 * NKT;
-      const int f0 = fl[(int64_t)(2 * rt) * NKT + kt_w];
-      const int f1 = (2 * rt + 1 < NRB32) ? fl[(int64_t)(2 * rt + 1) * NKT + kt_w] : 1;
+      const int NKT4 = (NKT + 3) & ~3;
+      const uint8_t* fl = a.mflags + (int64_t)b * NRB32 * NKT4;
+      const int ktw = __builtin_amdgcn_readfirstlane(kt_w);
+      const int f0 = tile_flag(fl + (int64_t)(2 * rt) * NKT4, ktw);
+      const int f1 = (2 * rt + 1 < NRB32) ? tile_flag(fl + (int64_t)(2 * rt + 1) * NKT4, ktw) : 1;
       flag = (f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2);
     }
     if (flag != 1 && c0 < a.T) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        f32x16 s = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, 0, lane), qf[0], f32x16{});
-        f32x16 dp = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, 0, lane), vf[0], f32x16{});
+        f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, 0, L), vf[0], f32x16{});
 #pragma unroll
         for (int kk = 1; kk < KS; ++kk) {
-          s = mfma32<DT>::run(row_frag(ks, ROWB, tt * 32, kk, lane), qf[kk], s);
-          dp = mfma32<DT>::run(row_frag(ds, ROWB, tt * 32, kk, lane), vf[kk], dp);
+          s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, kk, L), qf[kk], s);
+          dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, kk, L), vf[kk], dp);
         }
         // P and dS; rows of register r: tt*32 + (r&3) + 8*(r>>2) + 4*hf
 #pragma unroll
@@ -323,14 +368,15 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
             dp[r] = p * (dp[r] - d4[e]);
           }
         }
-        const u32x4 p0 = acc_to_frag<DT>(s, 0), p1 = acc_to_frag<DT>(s, 1);
-        const u32x4 g0 = acc_to_frag<DT>(dp, 0), g1 = acc_to_frag<DT>(dp, 1);
+        // one 16-row k-step at a time: only 2 packed operand fragments live
 #pragma unroll
-        for (int db = 0; db < DB; ++db) {
-          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, tt * 32, db * 32, lane), p0, dv[db]);
-          dv[db] = mfma32<DT>::run(tr_frag(ds, ROWB, tt * 32 + 16, db * 32, lane), p1, dv[db]);
-          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, tt * 32, db * 32, lane), g0, dq[db]);
-          dq[db] = mfma32<DT>::run(tr_frag(ks, ROWB, tt * 32 + 16, db * 32, lane), g1, dq[db]);
+        for (int sh = 0; sh < 2; ++sh) {
+          const u32x4 pf = acc_to_frag<DT>(s, sh), gf = acc_to_frag<DT>(dp, sh);
+#pragma unroll
+          for (int db = 0; db < DB; ++db) {
+            dv[db] = mfma32<DT>::run(tr_frag<D>(ds, tt * 32 + 16 * sh, db * 32, L), pf, dv[db]);
+            dq[db] = mfma32<DT>::run(tr_frag<D>(ks, tt * 32 + 16 * sh, db * 32, L), gf, dq[db]);
+          }
         }
       }
     }
@@ -375,17 +421,15 @@ static void launch_bwd_cols(const BwdArgs& a, const void* out, float* delta, hip
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
   BwdArgs a2 = a;
   a2.delta = delta;
-  constexpr int ROWB = Geo<D>::ROWB;
   const int ncb = (a.T + 127) / 128;
-  constexpr int STAGE = 2 * 64 * ROWB + 64 * 4 * 2 + 64 * 8 * 2;
+  constexpr int STAGE = 2 * Img<D>::BYTES + 64 * 4 * 2 + 64 * 8 * 2;
   hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a2);
 }
 
 template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
-  constexpr int ROWB = Geo<D>::ROWB;
   const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * 64 * ROWB), st, a);
+  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES), st, a);
   if (a.nsplit > 1) {
     const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
     hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);

@@ -58,12 +58,50 @@ __device__ __forceinline__ u32x4 acc_to_frag(const f32x16& x, int s) {
   return r;
 }
 
-// Transposed operand from a row-major [key][d] LDS image, matching acc_to_frag's k order:
+// ---- LDS tile images -------------------------------------------------------------------
+// One layout serves both ways a tile is read: rows of IMG_ROW bytes (D = 32/64/96/128 ->
+// 64/192/192/320) whose 16-byte chunks are XOR-swizzled by (row >> 2) & 3.  Checked against
+// the gfx950 LDS bank model (ds_read_b128: four 16-lane groups, ds_read_b64_tr_b16: two
+// 32-lane halves, banks (addr/4) % 64): both the row-operand reads and the transposed reads
+// below are conflict-free.
+template <int D> struct Img {
+  static constexpr int ROW = (D == 32) ? 64 : (D == 64 || D == 96) ? 192 : 320;
+  static constexpr int BYTES = 64 * ROW;  // one 64-row tile
+};
+template <int D>
+__device__ __forceinline__ int img_off(int row, int chunk) {
+  return row * Img<D>::ROW + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+
+// Per-lane byte bases into an image.  Every tile row offset used by the kernels (0, 16, 32,
+// 48) is a multiple of 16 rows, so the swizzle term of a read depends only on the lane:
+// two bases per read kind, everything else folds into the ds_read immediate offset.
+struct Lanes {
+  int rb0, rb1;  // row reads: even / odd k-step
+  int tb0, tb1;  // transposed reads: rows k0 + 4h + q, and the same + 8
+};
+template <int D>
+__device__ __forceinline__ Lanes make_lanes(int lane) {
+  constexpr int ROW = Img<D>::ROW;
+  Lanes L;
+  const int hf = lane >> 5, r = lane & 31, f = (r >> 2) & 3;
+  L.rb0 = r * ROW + ((hf ^ f) << 4);
+  L.rb1 = r * ROW + (((2 + hf) ^ f) << 4);
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int cl = 2 * (g & 1) + (p >> 1);  // chunk bits below the d0 block (d0/8 is a multiple of 4)
+  L.tb0 = (4 * hf + q) * ROW + ((cl ^ hf) << 4) + 8 * (p & 1);
+  L.tb1 = (4 * hf + q + 8) * ROW + ((cl ^ (2 + hf)) << 4) + 8 * (p & 1);
+  return L;
+}
+
+// Transposed operand from a [key][d] image, matching acc_to_frag's k order:
 // lane l (d = d0 + (l&31), h = l>>5) gets elements j <-> key k0 + 8*(j>>2) + 4h + (j&3).
-__device__ __forceinline__ u32x4 tr_frag(const char* img, int row_stride, int k0, int d0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
-  const char* a0 = img + (k0 + 4 * h + q) * row_stride + (d0 + (g & 1) * 16 + 4 * p) * 2;
-  const char* a1 = a0 + 8 * row_stride;
+// k0 must be a multiple of 16, d0 a multiple of 32.
+template <int D>
+__device__ __forceinline__ u32x4 tr_frag(const char* img, int k0, int d0, const Lanes& L) {
+  constexpr int ROW = Img<D>::ROW;
+  const char* a0 = img + L.tb0 + k0 * ROW + d0 * 2;
+  const char* a1 = img + L.tb1 + k0 * ROW + d0 * 2;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
   union { struct { s16x4 a, b; } s; u32x4 u; } c;
@@ -72,10 +110,11 @@ __device__ __forceinline__ u32x4 tr_frag(const char* img, int row_stride, int k0
   return c.u;
 }
 
-// Row-operand fragment (A or B of a 32x32x16 MFMA) from a row-major [row][d] LDS image:
-// lane l: row r0 + (l&31), d = 16*s + 8*(l>>5) .. +7.
-__device__ __forceinline__ u32x4 row_frag(const char* img, int row_stride, int r0, int s, int lane) {
-  return *reinterpret_cast<const u32x4*>(img + (r0 + (lane & 31)) * row_stride + (16 * s + 8 * (lane >> 5)) * 2);
+// Row-operand fragment (A or B of a 32x32x16 MFMA) from a [row][d] image:
+// lane l: row r0 + (l&31), d = 16*s + 8*(l>>5) .. +7.  r0 must be a multiple of 16.
+template <int D>
+__device__ __forceinline__ u32x4 row_frag(const char* img, int r0, int s, const Lanes& L) {
+  return *reinterpret_cast<const u32x4*>(img + ((s & 1) ? L.rb1 : L.rb0) + r0 * Img<D>::ROW + (s >> 1) * 64);
 }
 
 // global element offset of gathered col t (head offset excluded); ld = row stride
@@ -87,13 +126,15 @@ __device__ __forceinline__ int64_t col_off(int t, int b, int T, int64_t ld) {
 // arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// LDS row strides (bytes).  Row images read by ds_read_b128 use an odd number of 16-byte
-// slots (conflict-free for the b128 lane groups); images read with ds_read_b64_tr_b16 need
-// (stride/4) % 64 in {16, 48} (the 4 rows of a transposed read land in disjoint banks).
-template <int D> struct Geo {
-  static constexpr int ROWB = D * 2 + 16;                                        // b128 image
-  static constexpr int TRB = (D == 32) ? 64 : (D == 64 || D == 96) ? 192 : 320;  // tr image
-};
+// Flag of mask tile `kt` from a 4-byte padded flag row, fetched through the scalar cache
+// (wave-uniform address -> s_load_dword; it is counted by lgkmcnt, so it never waits for the
+// vector loads of the prefetched tile).
+__device__ __forceinline__ int tile_flag(const uint8_t* __restrict__ row, int kt) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(row);
+  const uint32_t v = __builtin_amdgcn_readfirstlane(w[__builtin_amdgcn_readfirstlane(kt >> 2)]);
+  return (v >> (8 * (kt & 3))) & 0xff;
+}
+
 
 }  // namespace fa
 }  // namespace xdot

@@ -32,8 +32,7 @@ namespace fa {
 template <int DT, int D>
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int ROWB = Geo<D>::ROWB, TRB = Geo<D>::TRB;
-  constexpr int QS_BYTES = 64 * ROWB, VS_BYTES = 64 * TRB, STAGE = QS_BYTES + VS_BYTES;
+  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * Img<D>::BYTES;
   constexpr int KS = D / 16;      // k-steps over the head dim
   constexpr int DB = D / 32;      // 32-wide d blocks of the output
   constexpr int CPR = D / 8;      // 16-byte chunks per row
@@ -43,6 +42,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const Lanes L = make_lanes<D>(lane);
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int rb = lin % nrb, bhs = lin / nrb;
@@ -67,19 +67,40 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     for (int s = 0; s < KS; ++s) kf[s] = row_ok ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0, 0, 0, 0};
   }
 
-  // staging of one 64-column tile (Q_cols and V_cols), global -> registers
+  // staging of one 64-column tile (Q_cols and V_cols), global -> registers.  Full tiles use a
+  // scalar tile base + a per-thread 32-bit byte offset (global_load v_off, s[base]).
   u32x4 rq[LPT], rv[LPT];
-  auto load_tile = [&](int kt) {
+  uint32_t soff[LPT];
+  int stoff[LPT];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / CPR, c = v % CPR;
-      // rows past T read row T-1: their scores are masked to -inf, so P = 0 multiplies
-      // finite values (no branch around the loads)
-      const int t = min(kt * 64 + r, a.T - 1);
-      const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
-      rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-      rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+  for (int i = 0; i < LPT; ++i) {
+    const int v = tid + 256 * i;
+    soff[i] = (uint32_t)(((v / CPR) * a.ldkv + (v % CPR) * 8) * 2);
+    stoff[i] = img_off<D>(v / CPR, v % CPR);
+  }
+  const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
+  const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
+  auto load_tile = [&](int kt) {
+    const int64_t t0 = (int64_t)kt * 64;
+    if (t0 + 64 <= a.T) {
+      const char* bq = kcb + t0 * a.ldkv * 2;
+      const char* bv = vcb + t0 * a.ldkv * 2;
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        rq[i] = *reinterpret_cast<const u32x4*>(bq + soff[i]);
+        rv[i] = *reinterpret_cast<const u32x4*>(bv + soff[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        // rows past T read row T-1: their scores are masked to -inf, so P = 0 multiplies
+        // finite values (no branch around the loads)
+        const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
+        const int t = min(kt * 64 + r, a.T - 1);
+        const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
+        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
+        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -89,8 +110,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     for (int i = 0; i < LPT; ++i) {
       const int v = tid + 256 * i;
       const int r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(qs + r * ROWB + c * 16) = rq[i];
-      *reinterpret_cast<u32x4*>(vs + r * TRB + c * 16) = rv[i];
+      *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
+      *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
     }
   };
 
@@ -103,7 +124,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
 
-  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + (r0 >> 5)) * NKT : nullptr;
+  const int NKT4 = (NKT + 3) & ~3;
+  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
   const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
   load_tile(kt_beg);
@@ -112,10 +134,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const int cur = (kt - kt_beg) & 1;
+    // mask state of this tile first (its vector load must not queue behind the prefetch)
+    const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
+    const uint64_t mword = (flag == 2 && bits) ? bits[kt] : 0ull;
     if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
-    const int flag = (flags && r0 < a.R) ? flags[kt] : 0;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
       // ---- Sᵀ = Q_cols · K_rowsᵀ : two 32x32 tiles (cols 0-31, 32-63) ----
@@ -125,13 +149,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[tt] = mfma32<DT>::run(row_frag(qs, ROWB, tt * 32, ks, lane), kf[ks], s[tt]);
+        for (int ks = 0; ks < KS; ++ks) s[tt] = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s[tt]);
       }
       // ---- online softmax (lane-local row, partner lane = lane ^ 32) ----
       // max over raw scores (scale > 0), exponent as one FMA: p = 2^(s*c2 - m)
       float mx = NEG_INF;
       if (flag == 2 || tail) {
-        const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
+        const uint64_t w = mword;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -179,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       for (int db = 0; db < DB; ++db)
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4)
-          o[db] = mfma32<DT>::run(tr_frag(vs, TRB, k4 * 16, db * 32, lane), pf[k4], o[db]);
+          o[db] = mfma32<DT>::run(tr_frag<D>(vs, k4 * 16, db * 32, L), pf[k4], o[db]);
     }
     if (kt + 1 < kt_end) store_tile(cur ^ 1);
     __syncthreads();
@@ -256,7 +280,7 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  constexpr int STAGE = 64 * Geo<D>::ROWB + 64 * Geo<D>::TRB;
+  constexpr int STAGE = 2 * Img<D>::BYTES;
   const int nrb = (a.R + 127) / 128;
   hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
   if (a.nsplit > 1) {

@@ -5,8 +5,11 @@
 // module.py:47-50, :66).  Here the mask is read ONCE per forward (R*T bytes, shared by all
 // heads and by the backward) and turned into
 //   bits  (B, R, NKT) uint64 : bit k of word kt = mask[b, r, 64*kt + k]
-//   flags (B, ceil(R/32), NKT) uint8 : per 32-row x 64-col tile, 0 = nothing masked,
-//         1 = everything masked (tile skipped), 2 = partial (bits applied per element).
+//   flags (B, ceil(R/32), NKT4) uint8, NKT4 = NKT rounded up to 4: per 32-row x 64-col tile,
+//         0 = nothing masked, 1 = everything masked (tile skipped), 2 = partial (bits applied
+//         per element).  Rows are padded to 4 bytes so the kernels fetch a tile's flag with a
+//         wave-uniform scalar load (s_load_dword), which does not wait on the vector-memory
+//         counter that tracks their prefetched K/V tiles.
 // An all-False mask (the reference example/benchmark) therefore costs the kernels nothing.
 #include "common.h"
 
@@ -51,10 +54,12 @@ __global__ __launch_bounds__(256) void mask_bits_kernel(const uint8_t* __restric
 __global__ __launch_bounds__(256) void mask_flags_kernel(const uint64_t* __restrict__ bits, uint8_t* __restrict__ flags,
                                                           int B, int R, int T, int NKT) {
   const int NRB = (R + 31) / 32;
+  const int NKT4 = (NKT + 3) & ~3;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)B * NRB * NKT) return;
-  const int kt = (int)(idx % NKT);
-  const int64_t brb = idx / NKT;
+  if (idx >= (int64_t)B * NRB * NKT4) return;
+  const int kt = (int)(idx % NKT4);
+  const int64_t brb = idx / NKT4;
+  if (kt >= NKT) { flags[idx] = 1; return; }
   const int rb = (int)(brb % NRB), b = (int)(brb / NRB);
   const int n = min(64, T - kt * 64);
   const uint64_t full = n == 64 ? ~0ull : ((1ull << n) - 1);
@@ -79,7 +84,7 @@ extern "C" int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_
   const int64_t n1 = rows * NKT * 8;
   if (n1 == 0) return 0;
   hipLaunchKernelGGL(mask_bits_kernel, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, mask, bits, rows, T, NKT, vec8);
-  const int64_t n2 = (int64_t)B * ((R + 31) / 32) * NKT;
+  const int64_t n2 = (int64_t)B * ((R + 31) / 32) * ((NKT + 3) & ~3);
   hipLaunchKernelGGL(mask_flags_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, bits, flags, B, R, T, NKT);
   return 0;
 }
