@@ -43,6 +43,9 @@ def parse(argv=None):
     ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random"])
     ap.add_argument("--no-optim", action="store_true", help="(diagnostic) skip the optimizer step")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"],
+                    help="collective backend (auto = RCCL on GPU); gloo lets several ranks share one GPU "
+                         "for rehearsals")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     return ap.parse_args(argv)
 
@@ -54,7 +57,7 @@ def main(argv=None):
     from xdot.utils import comm as C
     from xdot.parallel import GradSync
 
-    comm = C.init("auto")
+    comm = C.init(a.backend)
     n, rank = comm.world_size, comm.rank
     if n != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but world size {n}", file=sys.stderr)

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 template <int DT, int D>
 __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * QS_BYTES;
+  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * QS_BYTES + 128 * 8;  // Q, V, mask words
   constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -106,7 +106,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   }
   const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
+  // mask words travel with the tile through LDS (see flash_fwd.hip)
+  uint64_t mw = 0;
+  const uint64_t* mrow = (a.mbits && tid < 128 && rb * 128 + tid < a.R) ? a.mbits + ((int64_t)b * a.R + rb * 128 + tid) * NKT : nullptr;
   auto load_tile = [&](int kt) {
+    if (mrow) mw = mrow[kt];
     const int64_t t0 = (int64_t)kt * 64;
     if (t0 + 64 <= a.T) {
       const char* bq = kcb + t0 * a.ldkv * 2;
@@ -135,6 +139,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
       *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
       *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
     }
+    if (a.mbits && tid < 128) reinterpret_cast<uint64_t*>(qs + 2 * QS_BYTES)[tid] = mw;
   };
 
   f32x16 dk[DB];
@@ -144,7 +149,6 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
     for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
   const int NKT4 = (NKT + 3) & ~3;
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
-  const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
   load_tile(kt_beg);
   store_tile(0);
@@ -152,13 +156,13 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const int cur = (kt - kt_beg) & 1;
     const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
-    const uint64_t w = (flag == 2 && bits) ? bits[kt] : 0ull;
     if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
       const bool chk = flag == 2 || tail;
+      const uint64_t w = flag == 2 ? reinterpret_cast<const uint64_t*>(qs + 2 * QS_BYTES)[wave * 32 + (lane & 31)] : 0ull;
       // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -429,7 +433,7 @@ static void launch_bwd_cols(const BwdArgs& a, const void* out, float* delta, hip
 template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES), st, a);
+  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
   if (a.nsplit > 1) {
     const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
     hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);

@@ -122,6 +122,16 @@ __device__ __forceinline__ int64_t col_off(int t, int b, int T, int64_t ld) {
   return ((int64_t)b * T + t) * ld;
 }
 
+// combine a value with the partner lane (lane ^ 32) through v_permlane32_swap (no LDS)
+__device__ __forceinline__ float pair_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+  return __builtin_fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float pair_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
 // v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;
 // arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

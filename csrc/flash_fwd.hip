@@ -32,7 +32,7 @@ namespace fa {
 template <int DT, int D>
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * Img<D>::BYTES;
+  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * Img<D>::BYTES + 128 * 8;  // Q, V, mask words
   constexpr int KS = D / 16;      // k-steps over the head dim
   constexpr int DB = D / 32;      // 32-wide d blocks of the output
   constexpr int CPR = D / 8;      // 16-byte chunks per row
@@ -80,7 +80,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   }
   const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
+  // the 64-bit mask word of (row, tile) travels with the tile through LDS: a per-lane global
+  // load inside the loop would make the compiler wait vmcnt(0), i.e. for the prefetch too
+  uint64_t mw = 0;
+  const uint64_t* mrow = (a.mbits && tid < 128 && rb * 128 + tid < a.R) ? a.mbits + ((int64_t)b * a.R + rb * 128 + tid) * NKT : nullptr;
   auto load_tile = [&](int kt) {
+    if (mrow) mw = mrow[kt];
     const int64_t t0 = (int64_t)kt * 64;
     if (t0 + 64 <= a.T) {
       const char* bq = kcb + t0 * a.ldkv * 2;
@@ -113,6 +118,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
       *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
     }
+    if (a.mbits && tid < 128) reinterpret_cast<uint64_t*>(qs + 2 * Img<D>::BYTES)[tid] = mw;
   };
 
   const float c2 = a.scale * LOG2E;
@@ -126,7 +132,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 
   const int NKT4 = (NKT + 3) & ~3;
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
-  const uint64_t* bits = a.mbits ? a.mbits + ((int64_t)b * a.R + (row_ok ? row : 0)) * NKT : nullptr;
 
   load_tile(kt_beg);
   store_tile(0);
@@ -136,7 +141,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     const int cur = (kt - kt_beg) & 1;
     // mask state of this tile first (its vector load must not queue behind the prefetch)
     const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
-    const uint64_t mword = (flag == 2 && bits) ? bits[kt] : 0ull;
     if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* qs = smem + cur * STAGE;
     const char* vs = qs + QS_BYTES;
@@ -144,18 +148,22 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     if (flag != 1 && r0 < a.R) {
       // ---- Sᵀ = Q_cols · K_rowsᵀ : two 32x32 tiles (cols 0-31, 32-63) ----
       f32x16 s[2];
+      {
+        u32x4 qa = row_frag<D>(qs, 0, 0, L);
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[tt][r] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[tt] = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s[tt]);
+        for (int i = 0; i < 2 * KS; ++i) {
+          const int tt = i / KS, ks = i % KS;
+          u32x4 qn = qa;
+          if (i + 1 < 2 * KS) qn = row_frag<D>(qs, ((i + 1) / KS) * 32, (i + 1) % KS, L);
+          s[tt] = mfma32<DT>::run(qa, kf[ks], ks == 0 ? f32x16{} : s[tt]);
+          qa = qn;
+        }
       }
       // ---- online softmax (lane-local row, partner lane = lane ^ 32) ----
       // max over raw scores (scale > 0), exponent as one FMA: p = 2^(s*c2 - m)
       float mx = NEG_INF;
       if (flag == 2 || tail) {
-        const uint64_t w = mword;
+        const uint64_t w = flag == 2 ? reinterpret_cast<const uint64_t*>(qs + 2 * Img<D>::BYTES)[wave * 32 + (lane & 31)] : 0ull;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -170,7 +178,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c2;
+      mx = pair_max(mx) * c2;
       const float m_new = fmaxf(m_run, mx);
       const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
       // rescale the running output only when some row of the wave raised its max
@@ -199,18 +207,23 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) pf[tt * 2 + sh] = acc_to_frag<DT>(s[tt], sh);
+      // operand reads run one MFMA ahead of their use
+      u32x4 va = tr_frag<D>(vs, 0, 0, L);
 #pragma unroll
-      for (int db = 0; db < DB; ++db)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-          o[db] = mfma32<DT>::run(tr_frag<D>(vs, k4 * 16, db * 32, L), pf[k4], o[db]);
+      for (int i = 0; i < 4 * DB; ++i) {
+        const int db = i >> 2, k4 = i & 3;
+        u32x4 vn = va;
+        if (i + 1 < 4 * DB) vn = tr_frag<D>(vs, ((i + 1) & 3) * 16, ((i + 1) >> 2) * 32, L);
+        o[db] = mfma32<DT>::run(va, pf[k4], o[db]);
+        va = vn;
+      }
     }
     if (kt + 1 < kt_end) store_tile(cur ^ 1);
     __syncthreads();
   }
 
   // ---- epilogue ----
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = pair_sum(l_run);
   const float inv = 1.f / l_tot;
   if (row_ok && a.nsplit == 1) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
@@ -280,7 +293,7 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  constexpr int STAGE = 2 * Img<D>::BYTES;
+  constexpr int STAGE = 2 * Img<D>::BYTES + 128 * 8;
   const int nrb = (a.R + 127) / 128;
   hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
   if (a.nsplit > 1) {

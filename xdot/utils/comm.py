@@ -379,9 +379,8 @@ def init(backend: str = "auto", timeout_s: Optional[float] = None, set_device: b
     if dist.is_available() and dist.is_initialized():
         _DEFAULT = TorchDistComm()
         return _DEFAULT
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1 or "MASTER_ADDR" not in os.environ:
-        _DEFAULT = LocalComm()
+    if "WORLD_SIZE" not in os.environ or "MASTER_ADDR" not in os.environ:
+        _DEFAULT = LocalComm()  # plain `python script.py`: one rank, no process group
         return _DEFAULT
     be = resolve_backend(backend)
     if be == "nccl":
