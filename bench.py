@@ -50,14 +50,17 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def main(argv=None):
+def main(argv=None, comm=None):
+    """``comm``: optional communicator override (``benchmarks/bench_rank.py`` passes an
+    :class:`xdot.utils.comm.EmulatedComm` to run one rank of an N-GPU step on one GPU)."""
     a = parse(argv)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import xdot
     from xdot.utils import comm as C
     from xdot.parallel import GradSync
 
-    comm = C.init(a.backend)
+    emulated = comm is not None
+    comm = comm or C.init(a.backend)
     n, rank = comm.world_size, comm.rank
     if n != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but world size {n}", file=sys.stderr)
@@ -72,7 +75,8 @@ def main(argv=None):
     R = T // n
 
     torch.manual_seed(1234)  # identical weights on every rank
-    model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl).to(dev, dt)
+    model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl,
+                                        comm=comm).to(dev, dt)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
     sync = GradSync(model, comm=comm)
     crit = torch.nn.MSELoss()
@@ -126,7 +130,7 @@ def main(argv=None):
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
 
     ms = (t1 - t0) * 1e3 / max(1, a.steps)
-    t = torch.tensor([ms], dtype=torch.float64, device=dev if comm.backend == "nccl" else "cpu")
+    t = torch.tensor([ms], dtype=torch.float64, device=dev if comm.backend in ("nccl", "emulated") else "cpu")
     comm.all_reduce(t, op="max")
     ms = float(t.item())
     lossv = float(loss.float().item())
@@ -152,8 +156,13 @@ def main(argv=None):
             "tokens_per_s": round(a.batch * T / (ms / 1e3), 1),
             "loss": lossv,
         }
+        if emulated:
+            rec["metric"] = "EMULATED per-rank step (no transport; diagnostics only): " + METRIC
+            rec["config"]["parallelism"] += "-emulated"
         print(json.dumps(rec), flush=True)
-    C.destroy()
+    if not emulated:
+        C.destroy()
+    return ms
 
 
 if __name__ == "__main__":

@@ -186,15 +186,24 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   return g;
 }
 
-// Column split so small row counts (e.g. T/N = 3125 rows at N = 8: 200 workgroups) still put
-// >= `target` workgroups on the 256 CUs; every split keeps >= 8 column tiles.
-int pick_split(int64_t blocks, int64_t T, int64_t target, int64_t req) {
+// Column split of the row-block grid.  Every workgroup of a flash kernel does the same
+// work, so the launch runs in ceil(workgroups / slots) equal rounds (slots = 2 per CU x 256
+// CUs) and a last round that is barely occupied costs a whole round: T = 25000, H = 8 gives
+// 1568 row blocks = 3.06 rounds -> 24 % idle.  Pick the split s (<= 8, >= 8 column tiles per
+// split) minimising rounds(s) x (tiles / s + fixed per-workgroup cost ~ 8 tiles: prologue,
+// epilogue, the combine pass); ties keep fewer splits.
+int pick_split(int64_t blocks, int64_t T, int64_t slots, int64_t req) {
   const int64_t nkt = (T + 63) / 64;
   if (req > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(req, nkt));
-  if (blocks >= target) return 1;
-  int64_t s = (target + blocks - 1) / blocks;
-  s = std::min<int64_t>(s, std::max<int64_t>(1, nkt / 8));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 8));
+  int best = 1;
+  double best_cost = 1e300;
+  for (int s = 1; s <= 8; ++s) {
+    if (s > 1 && nkt / s < 8) break;
+    const int64_t rounds = (blocks * s + slots - 1) / slots;
+    const double cost = (double)rounds * ((double)nkt / s + 8.0);
+    if (cost < best_cost * 0.985) { best_cost = cost; best = s; }
+  }
+  return best;
 }
 
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
@@ -251,19 +260,49 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const at::Tensor& out, const at::Tensor& lse,
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
-                                                              double scale) {
+                                                              double scale, const c10::optional<at::Tensor>& delta_in) {
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   auto dkv = at::empty({g.B, g.T, 2 * g.C}, kc.options().dtype(at::kFloat));
-  auto delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  const bool have_delta = delta_in.has_value() && delta_in->defined();
+  at::Tensor delta;
+  if (have_delta) {
+    delta = *delta_in;
+    TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R &&
+                    delta.device() == rows.device(), "xdot.flash_bwd_cols: delta");
+  } else {
+    delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  }
   a.dkc = dkv.data_ptr<float>(); a.dvc = dkv.data_ptr<float>() + g.C; a.ldg = 2 * g.C;
+  a.delta = delta.data_ptr<float>();
   c10::DeviceGuard guard(rows.device());
-  TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(rows.scalar_type()),
-                                         (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
+  const int dt = dt_code(rows.scalar_type());
+  if (!have_delta)
+    TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt, (int)g.D, cur_stream(rows)) == 0,
+                "xdot.flash_bwd_cols: config");
+  TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, dt, (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
   check_launch(hipGetLastError(), "flash_bwd_cols");
   return {dkv, delta};
+}
+
+// δ = rowsum(dO ⊙ O) per (b, h, row), fp32 (B, H, R)
+at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_t H) {
+  TORCH_CHECK(dout.is_cuda() && dout.dim() == 3 && dout.is_contiguous() && out.sizes() == dout.sizes() &&
+                  out.is_contiguous() && out.scalar_type() == dout.scalar_type() && out.device() == dout.device(),
+              "xdot.flash_bwd_delta: dout/out must be matching contiguous (B, R, H*D) device tensors");
+  TORCH_CHECK(H > 0 && dout.size(2) % H == 0, "xdot.flash_bwd_delta: H");
+  xdot::fa::BwdArgs a{};
+  a.dout = dout.data_ptr();
+  a.B = (int)dout.size(0); a.R = (int)dout.size(1); a.H = (int)H;
+  auto delta = at::empty({dout.size(0), H, dout.size(1)}, dout.options().dtype(at::kFloat));
+  c10::DeviceGuard guard(dout.device());
+  TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(dout.scalar_type()),
+                                          (int)(dout.size(2) / H), cur_stream(dout)) == 0,
+              "xdot.flash_bwd_delta: unsupported dtype/head dim");
+  check_launch(hipGetLastError(), "flash_bwd_delta");
+  return delta;
 }
 
 // row-side grad (this rank's rows), column-split when the row count is small
@@ -291,7 +330,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd(const at::Tensor& dout,
                                                          const at::Tensor& vc, const at::Tensor& out, const at::Tensor& lse,
                                                          const c10::optional<at::Tensor>& bits,
                                                          const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
-  auto [dkv, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale);
+  auto [dkv, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale, c10::nullopt);
   auto drows = flash_bwd_rows(dout, rows, kc, vc, lse, delta, bits, flags, H, scale, 0);
   const int64_t C = rows.size(2);
   return {drows, dkv.narrow(2, 0, C), dkv.narrow(2, C, C)};
@@ -308,7 +347,8 @@ TORCH_LIBRARY(xdot, m) {
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor)");
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
-        "Tensor? flags, int H, float scale) -> (Tensor, Tensor)");
+        "Tensor? flags, int H, float scale, Tensor? delta=None) -> (Tensor, Tensor)");
+  m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
   m.def("flash_bwd(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, Tensor? flags, "
@@ -324,4 +364,5 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd", &flash_bwd);
   m.impl("flash_bwd_cols", &flash_bwd_cols);
   m.impl("flash_bwd_rows", &flash_bwd_rows);
+  m.impl("flash_bwd_delta", &flash_bwd_delta);
 }

@@ -55,14 +55,15 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 
 // ---------------------------------------------------------------------------------------
 // grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols.
-template <int DT, int D>
-__global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
+template <int DT, int D, int WPS = 2>
+__global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * QS_BYTES + 128 * 8;  // Q, V, mask words
   constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
   const Lanes L = make_lanes<D>(lane);
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -218,15 +219,16 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // grads of the gathered side.  4 waves x 32 columns; 64-row tiles of K_rows / dO.
-template <int DT, int D>
-__global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
+template <int DT, int D, int WPS = 2>
+__global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   constexpr int IMG = Img<D>::BYTES;
   constexpr int STAGE = 2 * IMG + 64 * 4 * 2 + 64 * 8 * 2;  // K, dO, lse2[64], delta[64], words[2][64]
   constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
   const Lanes L = make_lanes<D>(lane);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols_kernel(BwdArgs a) {
       const int ktw = __builtin_amdgcn_readfirstlane(kt_w);
       const int f0 = tile_flag(fl + (int64_t)(2 * rt) * NKT4, ktw);
       const int f1 = (2 * rt + 1 < NRB32) ? tile_flag(fl + (int64_t)(2 * rt + 1) * NKT4, ktw) : 1;
-      flag = (f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2);
+      flag = __builtin_amdgcn_readfirstlane((f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2));
     }
     if (flag != 1 && c0 < a.T) {
 #pragma unroll
@@ -420,20 +422,24 @@ __global__ __launch_bounds__(256) void flash_bwd_rows_sum(BwdArgs a) {
 }
 
 template <int DT, int D>
-static void launch_bwd_cols(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
+static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
   const int64_t n0 = (int64_t)a.B * a.R * a.H;
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
-  BwdArgs a2 = a;
-  a2.delta = delta;
+}
+
+template <int DT, int D>
+static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
   constexpr int STAGE = 2 * Img<D>::BYTES + 64 * 4 * 2 + 64 * 8 * 2;
-  hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a2);
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
+  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
 }
 
 template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
+  else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
   if (a.nsplit > 1) {
     const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
     hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
@@ -454,12 +460,21 @@ static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   if (dt == DT_F16 && D == 128) { CALL(DT_F16, 128); return 0; }                                 \
   return -1;
 
-extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
-                                          hipStream_t st) {
+extern "C" int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
+                                           hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+#define XP(DTV, DV) launch_bwd_delta<DTV, DV>(*a, out, delta, st)
+  XB_DISPATCH(XP)
+#undef XP
+}
+
+extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st) {
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
-#define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, out, delta, st)
+#define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
 #undef XC
 }

@@ -29,8 +29,8 @@
 namespace xdot {
 namespace fa {
 
-template <int DT, int D>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
+template <int DT, int D, int WPS = 2>
+__global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * Img<D>::BYTES + 128 * 8;  // Q, V, mask words
   constexpr int KS = D / 16;      // k-steps over the head dim
@@ -41,7 +41,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
   const Lanes L = make_lanes<D>(lane);
   const int nrb = (a.R + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -295,7 +296,8 @@ template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
   constexpr int STAGE = 2 * Img<D>::BYTES + 128 * 8;
   const int nrb = (a.R + 127) / 128;
-  hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
   if (a.nsplit > 1) {
     const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
     hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);

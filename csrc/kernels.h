@@ -82,6 +82,9 @@ int xdot_softmax_fwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream
 int xdot_softmax_bwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_t* flags, int B, int R, int T, hipStream_t st);
 int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
-int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);
+// δ = rowsum(dO ⊙ O) (reads a->dout, a->B/R/H)
+int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);
+// gathered-side grads; a->delta must hold δ
+int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 }

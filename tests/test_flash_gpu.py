@@ -149,3 +149,23 @@ def test_flash_column_split(gpu, nsplit, masked):
     d1 = flash.bwd_rows(do, rows, kc, vc, l1, delta, mk, H, 0.1, nsplit=1)
     d2 = flash.bwd_rows(do, rows, kc, vc, l1, delta, mk, H, 0.1, nsplit=nsplit)
     assert (d1.float() - d2.float()).abs().max().item() <= 2e-2 * d1.float().abs().max().item()
+
+
+def test_flash_bwd_delta_and_given_delta(gpu):
+    """δ op == rowsum(dO·O) in fp32; passing δ to bwd_cols gives the same gradients."""
+    from xdot.ops import flash
+
+    B, R, T, H, D = 2, 70, 300, 4, 64
+    g = torch.Generator(device="cpu").manual_seed(7)
+    rows = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
+    kc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
+    vc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
+    do = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
+    o, lse = flash.fwd(rows, kc, vc, None, H, 0.125)
+    delta = flash.bwd_delta(do, o, H)
+    ref = (do.float() * o.float()).view(B, R, H, D).sum(-1).transpose(1, 2)
+    torch.testing.assert_close(delta, ref, rtol=1e-4, atol=1e-4)
+    dkv1, d1 = flash.bwd_cols(do, rows, kc, vc, o, lse, None, H, 0.125)
+    dkv2, d2 = flash.bwd_cols(do, rows, kc, vc, o, lse, None, H, 0.125, delta)
+    assert d2.data_ptr() == delta.data_ptr()
+    assert torch.equal(d1, delta) and torch.equal(dkv1, dkv2)

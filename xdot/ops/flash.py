@@ -74,11 +74,19 @@ def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[Pac
     return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit))
 
 
-def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float):
-    """Gathered-side grads -> (packed fp32 [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R))."""
+def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
+    """δ = rowsum(dO ⊙ O) per (b, h, row): fp32 (B, H, R)."""
+    return _ext.ops().flash_bwd_delta(dout.contiguous(), out.contiguous(), int(H))
+
+
+def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
+             delta: Optional[torch.Tensor] = None):
+    """Gathered-side grads -> (packed fp32 [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
+
+    ``delta`` (from :func:`bwd_delta`) is computed here when not given."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
-                                     out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))
+                                     out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta)
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0):

@@ -125,6 +125,17 @@ def _ref_bwd(do, k, qg, vg, o, lse, mask, H, scale):
     return dk, rank_major(dq_all, dh), rank_major(dv_all, dv)
 
 
+_SIDE = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """Per-device second compute stream of the backward (created once)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _SIDE:
+        _SIDE[i] = torch.cuda.Stream(device=i)
+    return _SIDE[i]
+
+
 # ----------------------------------------------------------------------------------------
 class SeqParallelAttention(torch.autograd.Function):
     """Fused seq-parallel attention on a PACKED gathered-side operand ``qv`` = [q | v]
@@ -168,11 +179,20 @@ class SeqParallelAttention(torch.autograd.Function):
             from ..ops import flash
 
             qg, vg = qvg[..., :C], qvg[..., C:]
-            # 1) gathered-side grads for all T columns -> 2) ONE reduce-scatter on the collective
-            #    stream, running WHILE 3) the row-side kernel computes dk
-            dkv, delta = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale)
+            # δ, then two independent kernels on two streams: 1) gathered-side grads for all T
+            # columns (then 2) ONE reduce-scatter on the collective stream) and 3) the row-side
+            # dk.  Running them concurrently lets each fill the other's partly occupied last
+            # round of workgroups; the reduce-scatter overlaps whatever of 3) is left.
+            delta = flash.bwd_delta(do, o, H)
+            cur = torch.cuda.current_stream(do.device)
+            side = _side_stream(do.device)
+            side.wait_stream(cur)
+            dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta)
+            with torch.cuda.stream(side):
+                dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
             h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
-            dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
+            cur.wait_stream(side)
+            dk.record_stream(cur)
         else:
             dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mk, H, scale)
             h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))

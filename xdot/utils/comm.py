@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = [
-    "Communicator", "TorchDistComm", "LocalComm", "ThreadComm", "ThreadGroup", "Handle",
+    "Communicator", "TorchDistComm", "LocalComm", "EmulatedComm", "ThreadComm", "ThreadGroup", "Handle",
     "init", "is_initialized", "get_comm", "use_comm", "get_world_size", "get_rank",
     "get_local_rank", "is_main_process", "synchronize", "destroy", "resolve_backend",
 ]
@@ -131,6 +131,36 @@ class LocalComm(Communicator):
 
     def barrier(self):
         return None
+
+
+class EmulatedComm(LocalComm):
+    """Rank ``rank`` of a pretend ``world_size``-rank job on ONE device (diagnostics only).
+
+    Collectives keep their shapes and are replaced by device-local copies (the gather
+    replicates the local shard, the reduce-scatter takes this rank's slice) so a single GPU
+    runs exactly the per-rank compute of an N-GPU step, without the transport.  Used by
+    ``benchmarks/bench_rank.py`` to study the N=8 per-rank step on the one-GPU box; never
+    by tests of numerical results (the math of an emulated job is not a real N-rank job).
+    """
+
+    def __init__(self, world_size: int, rank: int = 0):
+        self.world_size, self.rank = int(world_size), int(rank)
+
+    @property
+    def backend(self):
+        return "emulated"
+
+    def all_gather_into(self, out, inp, async_op=False):
+        _check_gather(out, inp, self.world_size)
+        out.view(self.world_size, -1).copy_(inp.reshape(1, -1).expand(self.world_size, -1))
+        return Handle(out=out) if async_op else None
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        out.view(-1).copy_(inp.reshape(self.world_size, -1)[self.rank])
+        return Handle(out=out) if async_op else None
+
+    def all_gather_object(self, obj):
+        return [obj] * self.world_size
 
 
 _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
