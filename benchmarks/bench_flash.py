@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--mask", action="store_true", help="pass an all-False (B, R, T) mask")
     ap.add_argument("--nsplit", type=int, default=0)
     ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="also time bwd_cols and bwd_rows launched together on two streams (cols on a normal "
+                         "and on a high-priority stream): when cols finishes and when both finish")
     a = ap.parse_args()
     from xdot.ops import flash
 
@@ -77,6 +80,27 @@ def main():
     if a.only in ("all", "bwd_rows"):
         ms, mn = timeit(lambda: flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale, a.nsplit), a.iters)
         res.append({"kernel": "flash_bwd_rows", "ms": ms, "min_ms": mn, "TFLOPs": 3 * gemm / ms / 1e9})
+    if a.concurrent:
+        for prio in (0, -1):
+            side = torch.cuda.Stream(device=dev, priority=prio)
+            cur = torch.cuda.current_stream(dev)
+            tc, tb = [], []
+            for it in range(a.iters + 2):
+                e0, ec, e1 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record()
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale, delta)
+                    ec.record()
+                flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale, a.nsplit)
+                cur.wait_stream(side)
+                e1.record()
+                e1.synchronize()
+                if it >= 2:
+                    tc.append(e0.elapsed_time(ec))
+                    tb.append(e0.elapsed_time(e1))
+            res.append({"kernel": f"cols||rows prio={prio}", "ms": statistics.median(tb),
+                        "cols_done_ms": statistics.median(tc), "min_ms": min(tb)})
     if a.torch and R == T:
         q = rows.view(B, R, H, D).transpose(1, 2).contiguous().requires_grad_(True)
         k = kc.reshape(B, T, H, D).transpose(1, 2).contiguous().requires_grad_(True)

@@ -73,15 +73,18 @@ class DistributedDotProductAttn(nn.Module):
         return "flash" if pa.flash_supported(x, self.dim, self.value_dim // self.num_heads) else "materialized"
 
     def forward(self, keys: Tensor, queries: Tensor, values: Tensor, attn_mask: Optional[Tensor] = None) -> Tensor:
-        k = self.keys(keys)
         scale = 1.0 / math.sqrt(self.dim)
-        impl = self._pick_impl(k)
-        if impl == "flash":
-            from ..parallel.attention import seq_parallel_attention_packed
+        if self._pick_impl(keys) == "flash":
+            from ..parallel.attention import seq_parallel_attention_packed, start_gather
 
             comm = (self.comm or _comm.get_comm()) if self.distributed else _comm.LocalComm()
-            return self.composition(seq_parallel_attention_packed(k, self._project_qv(queries, values), attn_mask,
-                                                                  self.num_heads, scale, comm=comm))
+            # gathered side first: its all-gather runs while the row-side GEMM computes
+            qv = self._project_qv(queries, values)
+            pending = start_gather(qv, comm)
+            k = self.keys(keys)
+            return self.composition(seq_parallel_attention_packed(k, qv, attn_mask, self.num_heads, scale,
+                                                                  comm=comm, pending=pending))
+        k = self.keys(keys)
         q = self.queries(queries)
         v = self.values(values)
         return self.composition(self._materialized(k, q, v, attn_mask, scale))

@@ -35,7 +35,8 @@ from .. import _ext
 from ..utils import comm as _comm
 from ..utils.checks import check_consistent
 
-__all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "flash_supported", "SeqParallelAttention"]
+__all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "start_gather", "flash_supported",
+           "SeqParallelAttention"]
 
 FLASH_HEAD_DIMS = (32, 64, 96, 128)
 
@@ -129,10 +130,10 @@ _SIDE = {}
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    """Per-device second compute stream of the backward (created once)."""
+    """Per-device high-priority compute stream of the backward (created once)."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
     if i not in _SIDE:
-        _SIDE[i] = torch.cuda.Stream(device=i)
+        _SIDE[i] = torch.cuda.Stream(device=i, priority=-1)
     return _SIDE[i]
 
 
@@ -142,20 +143,23 @@ class SeqParallelAttention(torch.autograd.Function):
     (B, R, 2C): one all-gather in forward, one reduce-scatter in backward."""
 
     @staticmethod
-    def forward(ctx, k, qv, mask, H, scale, comm):
+    def forward(ctx, k, qv, mask, H, scale, comm, pending=None):
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
-        qvg = _gather_rows(comm, qv).wait()                    # (N, B, R, 2C)
+        pending = pending if pending is not None else _gather_rows(comm, qv)
         use_hip = _ext.use_hip(k) and k.dtype in (torch.bfloat16, torch.float16)
         if use_hip:
             from ..ops import flash
 
-            qvg = flash.gathered_to_btc(qvg)                    # (B, T, 2C), a view for B = 1
+            # the mask is packed while the gather is in flight
+            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qv.shape[1] * comm.world_size) \
+                if mask is not None else None
+            qvg = flash.gathered_to_btc(pending.wait())          # (B, T, 2C), a view for B = 1
             qg, vg = qvg[..., :C], qvg[..., C:]
-            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qvg.shape[1]) if mask is not None else None
             o, lse = flash.fwd(k, qg, vg, mk, H, scale)
         else:
             mk = mask
+            qvg = pending.wait()                                 # (N, B, R, 2C)
             o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
         ctx.save_for_backward(k, qvg, o, lse)
         ctx.mk, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mk, H, scale, comm, use_hip
@@ -180,30 +184,42 @@ class SeqParallelAttention(torch.autograd.Function):
 
             qg, vg = qvg[..., :C], qvg[..., C:]
             # δ, then two independent kernels on two streams: 1) gathered-side grads for all T
-            # columns (then 2) ONE reduce-scatter on the collective stream) and 3) the row-side
-            # dk.  Running them concurrently lets each fill the other's partly occupied last
-            # round of workgroups; the reduce-scatter overlaps whatever of 3) is left.
+            # columns on a HIGH-priority stream, followed there by 2) the ONE reduce-scatter,
+            # and 3) the row-side dk on the current stream.  3) fills the partly occupied last
+            # workgroup rounds of 1) while the priority keeps 1) (and so the start of the
+            # collective) nearly as early as when it runs alone; 2) overlaps the rest of 3).
             delta = flash.bwd_delta(do, o, H)
             cur = torch.cuda.current_stream(do.device)
-            side = _side_stream(do.device)
-            side.wait_stream(cur)
-            dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta)
-            with torch.cuda.stream(side):
-                dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
-            h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
-            cur.wait_stream(side)
-            dk.record_stream(cur)
+            hi = _side_stream(do.device)
+            hi.wait_stream(cur)
+            with torch.cuda.stream(hi):
+                dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta)
+                h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
+            dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
+            cur.wait_stream(hi)
+            dqv.record_stream(cur)
         else:
             dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mk, H, scale)
             h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))
         if h is not None:
             h.wait()
-        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None
+        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None
+
+
+def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None) -> _comm.Handle:
+    """Issue the all-gather of the packed gathered side early (e.g. before the row-side
+    projection GEMM) and hand the handle to :func:`seq_parallel_attention_packed`."""
+    comm = comm or _comm.get_comm()
+    return _gather_rows(comm, qv.detach())
 
 
 def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,
-                                  comm: Optional[_comm.Communicator] = None) -> Tensor:
-    """Fused sequence-parallel attention with a packed gathered side ``qv = [q | v]`` (B, R, 2C)."""
+                                  comm: Optional[_comm.Communicator] = None,
+                                  pending: Optional[_comm.Handle] = None) -> Tensor:
+    """Fused sequence-parallel attention with a packed gathered side ``qv = [q | v]`` (B, R, 2C).
+
+    ``pending``: the handle of :func:`start_gather` on this ``qv`` (the gather is issued here
+    otherwise)."""
     comm = comm or _comm.get_comm()
     if k.dim() != 3 or qv.dim() != 3 or qv.shape[-1] <= k.shape[-1]:
         raise ValueError("seq_parallel_attention_packed expects k (B, R, C) and qv (B, R, C + Cv)")
@@ -212,7 +228,7 @@ def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor],
         if tuple(mask.shape) != (k.shape[0], k.shape[1], T):
             raise ValueError(f"mask must be (B, R, T)=({k.shape[0]}, {k.shape[1]}, {T}), got {tuple(mask.shape)}")
         mask = mask.to(torch.bool)
-    return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm)
+    return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm, pending)
 
 
 def seq_parallel_attention(k: Tensor, q: Tensor, v: Tensor, mask: Optional[Tensor], num_heads: int,
