@@ -137,7 +137,8 @@ std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
   auto m = mask.contiguous();
   const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
   const int64_t NKT = (T + 63) / 64;
-  auto bits = at::empty({B, R, NKT}, m.options().dtype(at::kLong));
+  // two spare words after the last row: the backward kernels DMA 16-byte word pairs
+  auto bits = at::empty({B * R * NKT + 2}, m.options().dtype(at::kLong)).narrow(0, 0, B * R * NKT).view({B, R, NKT});
   auto flags = at::empty({B, (R + 31) / 32, (NKT + 3) & ~3}, m.options().dtype(at::kByte));
   TORCH_CHECK(B * R * NKT < (1LL << 40) && T < (1LL << 31), "xdot.mask_pack: too large");
   c10::DeviceGuard guard(m.device());
@@ -179,6 +180,8 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   if (hb) {
     const int64_t NKT = (g.T + 63) / 64;
     TORCH_CHECK(bits->is_contiguous() && bits->numel() == g.B * g.R * NKT, "xdot.flash: mask bits shape");
+    TORCH_CHECK((int64_t)bits->storage().nbytes() >= (bits->storage_offset() + bits->numel() + 2) * 8,
+                "xdot.flash: mask bits need 2 spare words after the end (use mask_pack)");
     TORCH_CHECK(flags->is_contiguous() && flags->numel() == g.B * ((g.R + 31) / 32) * ((NKT + 3) & ~3),
                 "xdot.flash: mask flags shape");
     TORCH_CHECK((reinterpret_cast<uintptr_t>(flags->data_ptr()) & 3) == 0, "xdot.flash: flags alignment");

@@ -24,6 +24,8 @@
 // packed registers; the one operand that must be transposed is read with ds_read_b64_tr_b16.
 #include "flash_common.h"
 
+#include <type_traits>
+
 namespace xdot {
 namespace fa {
 
@@ -219,16 +221,62 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // grads of the gathered side.  4 waves x 32 columns; 64-row tiles of K_rows / dO.
+//
+// Staging is LDS-DMA (global_load_lds_dwordx4): no VGPRs hold a tile in flight, which is
+// what lets this kernel (qf/vf 48 + dq/dv 96 + S/dP 32 registers) keep its LDS fragment
+// reads ahead of the MFMAs instead of spilling.  The DMA destination is lane-linear, so the
+// swizzled image is produced by permuting the per-lane SOURCE addresses (position p of the
+// image holds chunk (p's chunk) ^ swizzle(row) of row p / ROW).  Per tile every wave issues
+// exactly NG DMAs (its share of the two images + one 256 B/1 KiB row-constant piece), so a
+// counted `s_waitcnt vmcnt(NG)` retires tile rt+1 while tile rt+2 stays in flight across the
+// raw barrier (3-deep ring; 2-deep when three stages do not fit twice in 160 KiB).
+template <int D> struct ColsCfg {
+  static constexpr int IMG = Img<D>::BYTES;
+  static constexpr int IPW = IMG / 4096;  // 1 KiB DMA pieces per wave per image
+  static constexpr int OFF_L = 2 * IMG, OFF_D = OFF_L + 256, OFF_W = OFF_D + 256, OFF_X = OFF_W + 1024;
+  static constexpr int STAGE = OFF_X + 256;
+  static constexpr int NBUF = (2 * 3 * STAGE <= 160 * 1024) ? 3 : 2;
+  static constexpr int PF = NBUF - 1;     // tiles in flight ahead of the one being computed
+  static constexpr int NG = 2 * IPW + 1;  // DMAs per wave per tile
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 / 4 bytes per lane: LDS[lds_wave_base + lane * size] <- global[base + off].
+// Inline asm on purpose: for the builtin, hipcc inserts `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 while any DMA is pending (it cannot prove they do not alias), which
+// would drain the prefetch ring every tile.  The kernel counts these DMAs itself (wait_vm).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
+}
+__device__ __forceinline__ void glds16(const void* base, uint32_t off, const char* lds_wave_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* base, uint32_t off, const char* lds_wave_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
+}
+
 template <int DT, int D, int WPS = 2>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int IMG = Img<D>::BYTES;
-  constexpr int STAGE = 2 * IMG + 64 * 4 * 2 + 64 * 8 * 2;  // K, dO, lse2[64], delta[64], words[2][64]
-  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
+  using CF = ColsCfg<D>;
+  constexpr int ROW = Img<D>::ROW, IMG = CF::IMG, IPW = CF::IPW, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
+  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Lanes L = make_lanes<D>(lane);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -242,6 +290,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   const bool col_ok = col < a.T;
   const int kt_w = c0 >> 6;           // this wave's 64-column mask tile
   const int bit0 = c0 & 63;
+  const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
 
   u32x4 qf[KS], vf[KS];
   {
@@ -253,70 +302,48 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       qf[s] = col_ok ? *reinterpret_cast<const u32x4*>(pq + 16 * s) : u32x4{0, 0, 0, 0};
       vf[s] = col_ok ? *reinterpret_cast<const u32x4*>(pv + 16 * s) : u32x4{0, 0, 0, 0};
     }
+    // consume the fragments here: the compiler's vmcnt bookkeeping then retires these loads
+    // before the first DMA instead of waiting vmcnt(0) (all DMAs in flight) inside the loop
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]), "+v"(vf[s]));
   }
-  const T16* rows = reinterpret_cast<const T16*>(a.rows) + h * D;
-  const T16* dout = reinterpret_cast<const T16*>(a.dout) + h * D;
-  const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;
-  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
   const int NRT = (a.R + 63) / 64;
-  const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
 
-  u32x4 rk[LPT], rd[LPT];
-  uint32_t soff[LPT];
-  int stoff[LPT];
+  // DMA source of this lane's image positions: row and byte offset of the chunk
+  int grow[IPW], gcol[IPW];
 #pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int v = tid + 256 * i;
-    soff[i] = (uint32_t)(((v / CPR) * C + (v % CPR) * 8) * 2);
-    stoff[i] = img_off<D>(v / CPR, v % CPR);
+  for (int i = 0; i < IPW; ++i) {
+    const int p = (wave * IPW + i) * 1024 + lane * 16, row = p / ROW;
+    int c = ((p % ROW) >> 4) ^ ((row >> 2) & 3);
+    if (c >= CPR) c = 0;  // padding positions of the image: any valid address
+    grow[i] = row;
+    gcol[i] = c * 16;
   }
-  const char* rowsb = reinterpret_cast<const char*>(rows + (int64_t)b * a.R * C);
-  const char* doutb = reinterpret_cast<const char*>(dout + (int64_t)b * a.R * C);
-  auto load_tile = [&](int rt) {
-    const int64_t r0t = (int64_t)rt * 64;
-    if (r0t + 64 <= a.R) {
-      const char* bk = rowsb + r0t * C * 2;
-      const char* bd = doutb + r0t * C * 2;
+  const char* rows_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.rows) + (int64_t)b * a.R * C + h * D);
+  const char* dout_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.dout) + (int64_t)b * a.R * C + h * D);
+  const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;
+  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
+  const uint64_t* mb = a.mbits ? a.mbits + (int64_t)b * a.R * NKT + kt0 : nullptr;  // 2 words per row (padded)
+
+  auto issue = [&](int rt) {
+    char* st = smem + (rt % NBUF) * CF::STAGE;
+    const int r0 = rt * 64;
+    const int rmax = a.R - 1 - r0;  // rows past R re-read row R-1; the compute masks them
+    const char* kb = rows_b + (int64_t)r0 * C * 2;
+    const char* db = dout_b + (int64_t)r0 * C * 2;
 #pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        rk[i] = *reinterpret_cast<const u32x4*>(bk + soff[i]);
-        rd[i] = *reinterpret_cast<const u32x4*>(bd + soff[i]);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        // rows past R re-read row R-1 (finite); their lse = +inf below makes P = dS = 0
-        const int v = tid + 256 * i, r = v / CPR, c = v % CPR, rr = min(rt * 64 + r, a.R - 1);
-        const int64_t off = ((int64_t)b * a.R + rr) * C + c * 8;
-        rk[i] = *reinterpret_cast<const u32x4*>(rows + off);
-        rd[i] = *reinterpret_cast<const u32x4*>(dout + off);
-      }
+    for (int i = 0; i < IPW; ++i) {
+      const uint32_t off = (uint32_t)(min(grow[i], rmax) * C * 2 + gcol[i]);
+      glds16(kb, off, st + (wave * IPW + i) * 1024);
+      glds16(db, off, st + IMG + (wave * IPW + i) * 1024);
     }
-  };
-  // the per-row lse/δ/mask words go global -> LDS right here (short register lifetime)
-  auto store_tile = [&](int buf, int rt) {
-    char* ks = smem + buf * STAGE;
-    char* ds = ks + IMG;
-    float* ls = reinterpret_cast<float*>(ds + IMG);
-    float* dls = ls + 64;
-    uint64_t* ws = reinterpret_cast<uint64_t*>(dls + 64);
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(ks + stoff[i]) = rk[i];
-      *reinterpret_cast<u32x4*>(ds + stoff[i]) = rd[i];
-    }
-    if (tid < 64) {
-      const int rr = rt * 64 + tid;
-      // rows past R: lse = +inf makes P = 0 for them
-      ls[tid] = rr < a.R ? lse[rr] * LOG2E : __builtin_inff();
-      dls[tid] = rr < a.R ? dlt[rr] : 0.f;
-    } else if (tid < 192 && a.mbits) {
-      const int r = (tid - 64) & 63, k = (tid - 64) >> 6, rr = rt * 64 + r;
-      ws[tid - 64] = (rr < a.R && kt0 + k < NKT) ? a.mbits[((int64_t)b * a.R + rr) * NKT + kt0 + k] : 0ull;
-    }
+    const uint32_t ro = (uint32_t)min(lane, rmax);  // offsets stay tile-relative (32-bit)
+    if (wave == 0) glds4(lse + r0, ro * 4, st + CF::OFF_L);
+    else if (wave == 1) glds4(dlt + r0, ro * 4, st + CF::OFF_D);
+    else if (wave == 2 && mb) glds16(mb + (int64_t)r0 * NKT, ro * (uint32_t)NKT * 8, st + CF::OFF_W);
+    else glds4(lse + r0, ro * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
   };
 
   f32x16 dq[DB], dv[DB];
@@ -325,17 +352,51 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dq[i][r] = 0.f; dv[i][r] = 0.f; }
 
-  load_tile(0);
-  store_tile(0, 0);
-  __syncthreads();
-  for (int rt = 0; rt < NRT; ++rt) {
-    const int cur = rt & 1;
-    if (rt + 1 < NRT) load_tile(rt + 1);
-    const char* ks = smem + cur * STAGE;
+#pragma unroll
+  for (int t = 0; t < PF; ++t)
+    if (t < NRT) issue(t);
+  if (PF > 1 && NRT > 1) wait_vm<NG * (PF - 1)>();
+  else wait_vm<0>();
+  raw_barrier();
+  // P and dS of one 32-row half tile in place (s <- P, dp <- dS); rows of register r:
+  // tt*32 + (r&3) + 8*(r>>2) + 4*hf.  Rows past R carry lse = +inf (patched below), so the
+  // unmasked path has no per-element test at all.
+  auto softmax_grad = [&](f32x16& s, f32x16& dp, const float* ls, const float* dls, const uint64_t* ws, int tt,
+                          bool masked) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int rbase = tt * 32 + 8 * g + 4 * hf;
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase) * LOG2E;
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + rbase);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        float x = __builtin_fmaf(s[r], c2, -l4[e]);
+        if (masked) {
+          const uint64_t wv = ws[2 * (rbase + e) + (kt_w - kt0)];
+          if ((wv >> (bit0 + (lane & 31))) & 1ull) x = NEG_INF;
+        }
+        const float p = fast_exp2(x);
+        s[r] = p;
+        dp[r] = p * (dp[r] - d4[e]);
+      }
+    }
+  };
+
+  // one row tile from ring stage BUF (a compile-time constant: every LDS address is a lane
+  // base + immediate, no per-read address arithmetic)
+  auto tile = [&](auto bufc, int rt) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (rt + PF < NRT) issue(rt + PF);
+    char* ks = smem + BUF * CF::STAGE;
     const char* ds = ks + IMG;
-    const float* ls = reinterpret_cast<const float*>(ds + IMG);
-    const float* dls = ls + 64;
-    const uint64_t* ws = reinterpret_cast<const uint64_t*>(dls + 64);
+    float* ls = reinterpret_cast<float*>(ks + CF::OFF_L);
+    const float* dls = reinterpret_cast<const float*>(ks + CF::OFF_D);
+    const uint64_t* ws = reinterpret_cast<const uint64_t*>(ks + CF::OFF_W);
+    if (rt * 64 + 64 > a.R) {  // last tile, partial: rows past R get lse = +inf -> P = dS = 0
+      if (wave == 0 && rt * 64 + lane >= a.R) ls[lane] = __builtin_inff();
+      __syncthreads();
+    }
     int flag = 0;
     if (a.mflags && c0 < a.T) {
       const int NKT4 = (NKT + 3) & ~3;
@@ -355,25 +416,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
           s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, kk, L), qf[kk], s);
           dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, kk, L), vf[kk], dp);
         }
-        // P and dS; rows of register r: tt*32 + (r&3) + 8*(r>>2) + 4*hf
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int rbase = tt * 32 + 8 * g + 4 * hf;
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + rbase);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            float x = __builtin_fmaf(s[r], c2, -l4[e]);
-            if (flag == 2) {
-              const uint64_t wv = ws[(kt_w - kt0) * 64 + rbase + e];
-              if ((wv >> (bit0 + (lane & 31))) & 1ull) x = NEG_INF;
-            }
-            const float p = fast_exp2(x);
-            s[r] = p;
-            dp[r] = p * (dp[r] - d4[e]);
-          }
-        }
+        if (flag == 2) softmax_grad(s, dp, ls, dls, ws, tt, true);
+        else softmax_grad(s, dp, ls, dls, ws, tt, false);
         // one 16-row k-step at a time: only 2 packed operand fragments live
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
@@ -386,8 +430,17 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
         }
       }
     }
-    if (rt + 1 < NRT) store_tile(cur ^ 1, rt + 1);
-    __syncthreads();
+    // tile rt+1 complete (this wave's DMAs), everyone done with tile rt, then rotate
+    if (rt + PF < NRT) wait_vm<NG * (PF - 1)>();
+    else wait_vm<0>();
+    raw_barrier();
+  };
+  for (int rt = 0; rt < NRT; rt += NBUF) {
+    tile(std::integral_constant<int, 0>{}, rt);
+    if (rt + 1 < NRT) tile(std::integral_constant<int, 1>{}, rt + 1);
+    if constexpr (NBUF > 2) {
+      if (rt + 2 < NRT) tile(std::integral_constant<int, 2>{}, rt + 2);
+    }
   }
   if (col_ok) {
     const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
@@ -430,9 +483,9 @@ static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hi
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
-  constexpr int STAGE = 2 * Img<D>::BYTES + 64 * 4 * 2 + 64 * 8 * 2;
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
-  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), 2 * STAGE, st, a);
+  constexpr int LDS = ColsCfg<D>::NBUF * ColsCfg<D>::STAGE;
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
+  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
 }
 
 template <int DT, int D>

@@ -148,12 +148,19 @@ __device__ __forceinline__ float pair_sum(float v) {
 // arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// Flag of mask tile `kt` from a 4-byte padded flag row, fetched through the scalar cache
-// (wave-uniform address -> s_load_dword; it is counted by lgkmcnt, so it never waits for the
-// vector loads of the prefetched tile).
+// Scalar (SMEM) load of one dword at a wave-uniform address.  hipcc only emits s_load for
+// memory it can prove unclobbered; otherwise it falls back to a vector load + readfirstlane
+// whose `s_waitcnt vmcnt(0)` would also drain every tile prefetch in flight.
+__device__ __forceinline__ uint32_t sload_u32(const uint32_t* p) {
+  uint32_t v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p));
+  return v;
+}
+
+// Flag of mask tile `kt` from a 4-byte padded flag row (wave-uniform row and kt).
 __device__ __forceinline__ int tile_flag(const uint8_t* __restrict__ row, int kt) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(row);
-  const uint32_t v = __builtin_amdgcn_readfirstlane(w[__builtin_amdgcn_readfirstlane(kt >> 2)]);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(row) + __builtin_amdgcn_readfirstlane(kt >> 2);
+  const uint32_t v = sload_u32(w);
   return (v >> (8 * (kt & 3))) & 0xff;
 }
 
