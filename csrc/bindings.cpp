@@ -132,20 +132,21 @@ at::Tensor softmax_bwd(const at::Tensor& y, const at::Tensor& dy, double scale) 
 }
 
 // ------------------------------------------------------------------------------------
-std::tuple<at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kBool && mask.dim() == 3, "xdot.mask_pack: (B, R, T) bool GPU mask");
   auto m = mask.contiguous();
   const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
-  const int64_t NKT = (T + 63) / 64;
-  // two spare words after the last row: the backward kernels DMA 16-byte word pairs
-  auto bits = at::empty({B * R * NKT + 2}, m.options().dtype(at::kLong)).narrow(0, 0, B * R * NKT).view({B, R, NKT});
+  const int64_t NKT = (T + 63) / 64, NRT = (R + 63) / 64, Tpad = (T + 127) / 128 * 128;
+  auto bits = at::empty({B, R, NKT}, m.options().dtype(at::kLong));
   auto flags = at::empty({B, (R + 31) / 32, (NKT + 3) & ~3}, m.options().dtype(at::kByte));
+  auto bitsT = at::empty({B, NRT, Tpad}, m.options().dtype(at::kLong));
   TORCH_CHECK(B * R * NKT < (1LL << 40) && T < (1LL << 31), "xdot.mask_pack: too large");
   c10::DeviceGuard guard(m.device());
   xdot_mask_pack_launch(reinterpret_cast<const uint8_t*>(m.data_ptr()), reinterpret_cast<uint64_t*>(bits.data_ptr()),
-                        flags.data_ptr<uint8_t>(), (int)B, (int)R, (int)T, cur_stream(m));
+                        reinterpret_cast<uint64_t*>(bitsT.data_ptr()), flags.data_ptr<uint8_t>(), (int)B, (int)R, (int)T,
+                        cur_stream(m));
   check_launch(hipGetLastError(), "mask_pack");
-  return {bits, flags};
+  return {bits, flags, bitsT};
 }
 
 struct FlashGeom {
@@ -154,8 +155,11 @@ struct FlashGeom {
 
 // rows: contiguous (B, R, C).  kc / vc: (B, T, C) views with unit inner stride and a common
 // row stride `ld` (C for separate tensors, 2C for the two halves of a packed [q | v]).
+// `bits`: the row-major (B, R, NKT) words, or with colmajor the (B, NRT, Tpad) words of the
+// backward column kernel (mask_pack's third output)
 FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc, int64_t H,
-                      const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags) {
+                      const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
+                      bool colmajor = false) {
   TORCH_CHECK(rows.is_cuda() && kc.is_cuda() && vc.is_cuda(), "xdot.flash: GPU tensors required");
   TORCH_CHECK(rows.is_contiguous(), "xdot.flash: rows must be contiguous");
   TORCH_CHECK(rows.scalar_type() == kc.scalar_type() && rows.scalar_type() == vc.scalar_type(), "xdot.flash: dtype mismatch");
@@ -179,9 +183,10 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   TORCH_CHECK(hb == hf, "xdot.flash: mask bits and flags go together");
   if (hb) {
     const int64_t NKT = (g.T + 63) / 64;
-    TORCH_CHECK(bits->is_contiguous() && bits->numel() == g.B * g.R * NKT, "xdot.flash: mask bits shape");
-    TORCH_CHECK((int64_t)bits->storage().nbytes() >= (bits->storage_offset() + bits->numel() + 2) * 8,
-                "xdot.flash: mask bits need 2 spare words after the end (use mask_pack)");
+    const int64_t nwords = colmajor ? g.B * ((g.R + 63) / 64) * ((g.T + 127) / 128 * 128) : g.B * g.R * NKT;
+    TORCH_CHECK(bits->is_contiguous() && bits->numel() == nwords && bits->element_size() == 8,
+                colmajor ? "xdot.flash_bwd_cols: mask needs the column-major bits (mask_pack output 3)"
+                         : "xdot.flash: mask bits shape");
     TORCH_CHECK(flags->is_contiguous() && flags->numel() == g.B * ((g.R + 31) / 32) * ((NKT + 3) & ~3),
                 "xdot.flash: mask flags shape");
     TORCH_CHECK((reinterpret_cast<uintptr_t>(flags->data_ptr()) & 3) == 0, "xdot.flash: flags alignment");
@@ -264,7 +269,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
                                                               double scale, const c10::optional<at::Tensor>& delta_in) {
-  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
@@ -329,16 +334,6 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   return drows;
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc,
-                                                         const at::Tensor& vc, const at::Tensor& out, const at::Tensor& lse,
-                                                         const c10::optional<at::Tensor>& bits,
-                                                         const c10::optional<at::Tensor>& flags, int64_t H, double scale) {
-  auto [dkv, delta] = flash_bwd_cols(dout, rows, kc, vc, out, lse, bits, flags, H, scale, c10::nullopt);
-  auto drows = flash_bwd_rows(dout, rows, kc, vc, lse, delta, bits, flags, H, scale, 0);
-  const int64_t C = rows.size(2);
-  return {drows, dkv.narrow(2, 0, C), dkv.narrow(2, C, C)};
-}
-
 }  // namespace
 
 TORCH_LIBRARY(xdot, m) {
@@ -347,15 +342,13 @@ TORCH_LIBRARY(xdot, m) {
         "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha) -> ()");
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
-  m.def("mask_pack(Tensor mask) -> (Tensor, Tensor)");
+  m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor? delta=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
-  m.def("flash_bwd(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, Tensor? flags, "
-        "int H, float scale) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
@@ -364,7 +357,6 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("softmax_bwd", &softmax_bwd);
   m.impl("mask_pack", &mask_pack);
   m.impl("flash_fwd", &flash_fwd);
-  m.impl("flash_bwd", &flash_bwd);
   m.impl("flash_bwd_cols", &flash_bwd_cols);
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);

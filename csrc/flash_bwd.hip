@@ -56,12 +56,14 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 }
 
 // ---------------------------------------------------------------------------------------
-// grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols.
+// grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols arrive by
+// LDS-DMA into the same ring as the forward's (RowsCfg).
 template <int DT, int D, int WPS = 2>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * QS_BYTES + 128 * 8;  // Q, V, mask words
-  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8, LPT = (64 * CPR) / 256;
+  using CF = RowsCfg<D>;
+  constexpr int IMG = CF::IMG, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
+  constexpr int KS = D / 16, DB = D / 32;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
@@ -79,8 +81,6 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   const int row = r0 + (lane & 31);
   const bool row_ok = row < a.R;
 
-  const T16* kc = reinterpret_cast<const T16*>(a.kc) + h * D;
-  const T16* vc = reinterpret_cast<const T16*>(a.vc) + h * D;
   u32x4 kf[KS], df[KS];
   {
     const int64_t off = ((int64_t)b * a.R + row) * C + h * D + 8 * hf;
@@ -93,56 +93,30 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     }
   }
   const int64_t lrow = ((int64_t)b * a.H + h) * a.R + (row_ok ? row : 0);
-  const float lse2 = row_ok ? a.lse[lrow] * LOG2E : 0.f;
-  const float dlt = row_ok ? a.delta[lrow] : 0.f;
+  float lse2 = row_ok ? a.lse[lrow] * LOG2E : 0.f;
+  float dlt = row_ok ? a.delta[lrow] : 0.f;
+  // retire these loads here, before the first DMA (else: vmcnt(0) inside the loop)
+#pragma unroll
+  for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(kf[s]), "+v"(df[s]));
+  asm volatile("" : "+v"(lse2), "+v"(dlt));
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
 
-  u32x4 rq[LPT], rv[LPT];
-  uint32_t soff[LPT];
-  int stoff[LPT];
-#pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int v = tid + 256 * i;
-    soff[i] = (uint32_t)(((v / CPR) * a.ldkv + (v % CPR) * 8) * 2);
-    stoff[i] = img_off<D>(v / CPR, v % CPR);
-  }
-  const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
-  const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
-  // mask words travel with the tile through LDS (see flash_fwd.hip)
-  uint64_t mw = 0;
-  const uint64_t* mrow = (a.mbits && tid < 128 && rb * 128 + tid < a.R) ? a.mbits + ((int64_t)b * a.R + rb * 128 + tid) * NKT : nullptr;
-  auto load_tile = [&](int kt) {
-    if (mrow) mw = mrow[kt];
+  ImgDma<D> dma;
+  dma.init(wave, lane);
+  const int ldb = a.ldkv * 2;
+  const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
+  const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
+  const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
+  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
+  auto issue = [&](int kt) {
+    char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
     const int64_t t0 = (int64_t)kt * 64;
-    if (t0 + 64 <= a.T) {
-      const char* bq = kcb + t0 * a.ldkv * 2;
-      const char* bv = vcb + t0 * a.ldkv * 2;
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        rq[i] = *reinterpret_cast<const u32x4*>(bq + soff[i]);
-        rv[i] = *reinterpret_cast<const u32x4*>(bv + soff[i]);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        const int v = tid + 256 * i, r = v / CPR, c = v % CPR, t = min(kt * 64 + r, a.T - 1);
-        const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
-        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* qs = smem + buf * STAGE;
-    char* vs = qs + QS_BYTES;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
-      *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
-    }
-    if (a.mbits && tid < 128) reinterpret_cast<uint64_t*>(qs + 2 * QS_BYTES)[tid] = mw;
+    const int rmax = a.T - 1 - (int)t0;
+    dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
+    dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
+    if (mwg) glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+    else glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
   };
 
   f32x16 dk[DB];
@@ -153,19 +127,16 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   const int NKT4 = (NKT + 3) & ~3;
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
 
-  load_tile(kt_beg);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
-    const int cur = (kt - kt_beg) & 1;
+  auto tile = [&](auto bufc, int kt) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (kt + PF < kt_end) issue(kt + PF);
+    const char* qs = smem + BUF * CF::STAGE;
+    const char* vs = qs + IMG;
     const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
-    if (kt + 1 < kt_end) load_tile(kt + 1);
-    const char* qs = smem + cur * STAGE;
-    const char* vs = qs + QS_BYTES;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
       const bool chk = flag == 2 || tail;
-      const uint64_t w = flag == 2 ? reinterpret_cast<const uint64_t*>(qs + 2 * QS_BYTES)[wave * 32 + (lane & 31)] : 0ull;
+      const uint64_t w = flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull;
       // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -176,14 +147,17 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
           s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s);
           dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, ks, L), df[ks], dp);
         }
+        if (chk) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = __builtin_fmaf(s[r], c2, -lse2);
-          if (chk) {
+          for (int r = 0; r < 16; ++r) {
+            float x = __builtin_fmaf(s[r], c2, -lse2);
             const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
             if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) x = NEG_INF;
+            s[r] = fast_exp2(x) * (dp[r] - dlt);  // dSᵀ (unscaled)
           }
-          s[r] = fast_exp2(x) * (dp[r] - dlt);  // dSᵀ (unscaled)
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(__builtin_fmaf(s[r], c2, -lse2)) * (dp[r] - dlt);
         }
         const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
 #pragma unroll
@@ -193,8 +167,23 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         }
       }
     }
-    if (kt + 1 < kt_end) store_tile(cur ^ 1);
-    __syncthreads();
+    if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
+    else wait_vm<0>();
+    raw_barrier();
+  };
+
+#pragma unroll
+  for (int t = 0; t < PF; ++t)
+    if (kt_beg + t < kt_end) issue(kt_beg + t);
+  if (PF > 1 && kt_beg + 1 < kt_end) wait_vm<NG * (PF - 1)>();
+  else wait_vm<0>();
+  raw_barrier();
+  for (int kt = kt_beg; kt < kt_end; kt += NBUF) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < kt_end) tile(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (NBUF > 2) {
+      if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
+    }
   }
   if (row_ok && a.nsplit > 1) {
     float* op = a.dpart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
@@ -240,39 +229,12 @@ template <int D> struct ColsCfg {
   static constexpr int NG = 2 * IPW + 1;  // DMAs per wave per tile
 };
 
-template <int N>
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// LDS-DMA of 16 / 4 bytes per lane: LDS[lds_wave_base + lane * size] <- global[base + off].
-// Inline asm on purpose: for the builtin, hipcc inserts `s_waitcnt vmcnt(0)` in front of every
-// ds_read_b64_tr_b16 while any DMA is pending (it cannot prove they do not alias), which
-// would drain the prefetch ring every tile.  The kernel counts these DMAs itself (wait_vm).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
-}
-__device__ __forceinline__ void glds16(const void* base, uint32_t off, const char* lds_wave_base) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
-}
-__device__ __forceinline__ void glds4(const void* base, uint32_t off, const char* lds_wave_base) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
-}
-
 template <int DT, int D, int WPS = 2>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = ColsCfg<D>;
   constexpr int ROW = Img<D>::ROW, IMG = CF::IMG, IPW = CF::IPW, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
-  constexpr int KS = D / 16, DB = D / 32, CPR = D / 8;
+  constexpr int KS = D / 16, DB = D / 32;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
@@ -289,8 +251,6 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   const int col = c0 + (lane & 31);
   const bool col_ok = col < a.T;
   const int kt_w = c0 >> 6;           // this wave's 64-column mask tile
-  const int bit0 = c0 & 63;
-  const int kt0 = (cb * 128) >> 6;    // first mask tile of the workgroup
 
   u32x4 qf[KS], vf[KS];
   {
@@ -311,38 +271,26 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   const float NEG_INF = -__builtin_inff();
   const int NRT = (a.R + 63) / 64;
 
-  // DMA source of this lane's image positions: row and byte offset of the chunk
-  int grow[IPW], gcol[IPW];
-#pragma unroll
-  for (int i = 0; i < IPW; ++i) {
-    const int p = (wave * IPW + i) * 1024 + lane * 16, row = p / ROW;
-    int c = ((p % ROW) >> 4) ^ ((row >> 2) & 3);
-    if (c >= CPR) c = 0;  // padding positions of the image: any valid address
-    grow[i] = row;
-    gcol[i] = c * 16;
-  }
+  ImgDma<D> dma;
+  dma.init(wave, lane);
   const char* rows_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.rows) + (int64_t)b * a.R * C + h * D);
   const char* dout_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.dout) + (int64_t)b * a.R * C + h * D);
   const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;
   const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
-  const uint64_t* mb = a.mbits ? a.mbits + (int64_t)b * a.R * NKT + kt0 : nullptr;  // 2 words per row (padded)
+  // column-major mask words (mask_pack's bits_t): one u64 per (64-row tile, column)
+  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
+  const uint64_t* mb = a.mbits ? a.mbits + (int64_t)b * NRT64 * TPAD + cb * 128 : nullptr;
 
   auto issue = [&](int rt) {
     char* st = smem + (rt % NBUF) * CF::STAGE;
     const int r0 = rt * 64;
     const int rmax = a.R - 1 - r0;  // rows past R re-read row R-1; the compute masks them
-    const char* kb = rows_b + (int64_t)r0 * C * 2;
-    const char* db = dout_b + (int64_t)r0 * C * 2;
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const uint32_t off = (uint32_t)(min(grow[i], rmax) * C * 2 + gcol[i]);
-      glds16(kb, off, st + (wave * IPW + i) * 1024);
-      glds16(db, off, st + IMG + (wave * IPW + i) * 1024);
-    }
+    dma.issue(rows_b + (int64_t)r0 * C * 2, C * 2, rmax, st, wave);
+    dma.issue(dout_b + (int64_t)r0 * C * 2, C * 2, rmax, st + IMG, wave);
     const uint32_t ro = (uint32_t)min(lane, rmax);  // offsets stay tile-relative (32-bit)
     if (wave == 0) glds4(lse + r0, ro * 4, st + CF::OFF_L);
     else if (wave == 1) glds4(dlt + r0, ro * 4, st + CF::OFF_D);
-    else if (wave == 2 && mb) glds16(mb + (int64_t)r0 * NKT, ro * (uint32_t)NKT * 8, st + CF::OFF_W);
+    else if (wave == 2 && mb) glds16(mb + (int64_t)rt * TPAD, (uint32_t)lane * 16, st + CF::OFF_W);
     else glds4(lse + r0, ro * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
   };
 
@@ -363,6 +311,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   // unmasked path has no per-element test at all.
   auto softmax_grad = [&](f32x16& s, f32x16& dp, const float* ls, const float* dls, const uint64_t* ws, int tt,
                           bool masked) {
+    // masked: this lane's column word over the tile's 64 rows, shifted to its row half
+    const uint32_t hw = masked ? (uint32_t)(ws[wave * 32 + (lane & 31)] >> (tt * 32)) >> (4 * hf) : 0u;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int rbase = tt * 32 + 8 * g + 4 * hf;
@@ -372,10 +322,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
         float x = __builtin_fmaf(s[r], c2, -l4[e]);
-        if (masked) {
-          const uint64_t wv = ws[2 * (rbase + e) + (kt_w - kt0)];
-          if ((wv >> (bit0 + (lane & 31))) & 1ull) x = NEG_INF;
-        }
+        if (masked && ((hw >> (8 * g + e)) & 1u)) x = NEG_INF;
         const float p = fast_exp2(x);
         s[r] = p;
         dp[r] = p * (dp[r] - d4[e]);
@@ -491,8 +438,9 @@ static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
 template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
-  else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * (2 * Img<D>::BYTES + 128 * 8), st, a);
+  constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+  else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   if (a.nsplit > 1) {
     const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
     hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);

@@ -144,6 +144,84 @@ __device__ __forceinline__ float pair_sum(float v) {
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
+
+// ---- LDS-DMA staging ---------------------------------------------------------------------
+// Tiles travel HBM -> LDS through global_load_lds (no VGPRs hold a tile in flight).  The DMA
+// destination is lane-linear (wave-uniform M0 base + lane * size), so a swizzled image is
+// produced by permuting the per-lane SOURCE addresses.  Kernels count their DMAs and wait
+// with a counted `s_waitcnt vmcnt(N)` + raw s_barrier so the next tiles stay in flight.
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 / 4 bytes per lane: LDS[lds_wave_base + lane * size] <- global[base + off].
+// Inline asm on purpose: for the builtin, hipcc inserts `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 while any DMA is pending (it cannot prove they do not alias), which
+// would drain the prefetch ring every tile.  The kernel counts these DMAs itself (wait_vm).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
+}
+__device__ __forceinline__ void glds16(const void* base, uint32_t off, const char* lds_wave_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* base, uint32_t off, const char* lds_wave_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_addr(lds_wave_base)) : "memory");
+}
+
+
+// Per-lane DMA sources of one 64-row swizzled image, filled by the 4 waves of a workgroup in
+// IPW 1-KiB pieces each: image position p holds chunk ((p % ROW) / 16) ^ ((row >> 2) & 3) of
+// tile row p / ROW (padding positions of D = 64/128 images load chunk 0: any valid address).
+template <int D> struct ImgDma {
+  static constexpr int IPW = Img<D>::BYTES / 4096;
+  int row[IPW], col[IPW];
+  __device__ __forceinline__ void init(int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int p = (wave * IPW + i) * 1024 + lane * 16, r = p / Img<D>::ROW;
+      int c = ((p % Img<D>::ROW) >> 4) ^ ((r >> 2) & 3);
+      if (c >= D / 8) c = 0;
+      row[i] = r;
+      col[i] = c * 16;
+    }
+  }
+  // tile rows past rmax re-read row rmax (callers mask them); base is the tile's first row
+  __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int wave) const {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i)
+      glds16(base, (uint32_t)(min(row[i], rmax) * stride_bytes + col[i]), img + (wave * IPW + i) * 1024);
+  }
+};
+
+// Ring stage of the row-block kernels (flash_fwd, flash_bwd_rows): the 64-column tile of the
+// key/value side as two images + the 64-bit mask words of the workgroup's 128 rows for that
+// column tile ([dword][128 rows]) + a 256-byte sink for the dummy DMA that keeps the count
+// per wave constant when there is no mask.
+template <int D> struct RowsCfg {
+  static constexpr int IMG = Img<D>::BYTES;
+  static constexpr int IPW = ImgDma<D>::IPW;
+  static constexpr int OFF_W = 2 * IMG, OFF_X = OFF_W + 1024;
+  static constexpr int STAGE = OFF_X + 256;
+  static constexpr int NBUF = (2 * 3 * STAGE <= 160 * 1024) ? 3 : 2;
+  static constexpr int PF = NBUF - 1;
+  static constexpr int NG = 2 * IPW + 1;
+};
+
+// mask word of workgroup row rr (0..127) for the staged column tile
+__device__ __forceinline__ uint64_t staged_word(const char* stage_w, int rr) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(stage_w);
+  return (uint64_t)w[rr] | ((uint64_t)w[128 + rr] << 32);
+}
+
 // v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;
 // arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

@@ -26,18 +26,18 @@
 // an XCD L2.
 #include "flash_common.h"
 
+#include <type_traits>
+
 namespace xdot {
 namespace fa {
 
 template <int DT, int D, int WPS = 2>
 __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  constexpr int QS_BYTES = Img<D>::BYTES, STAGE = 2 * Img<D>::BYTES + 128 * 8;  // Q, V, mask words
+  using CF = RowsCfg<D>;
+  constexpr int IMG = CF::IMG, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
   constexpr int KS = D / 16;      // k-steps over the head dim
   constexpr int DB = D / 32;      // 32-wide d blocks of the output
-  constexpr int CPR = D / 8;      // 16-byte chunks per row
-  constexpr int LPT = (64 * CPR) / 256;  // 16-byte loads per thread per operand per tile
-  static_assert((64 * CPR) % 256 == 0, "tile/thread mismatch");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -57,8 +57,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const bool row_ok = row < a.R;
 
   const T16* rows = reinterpret_cast<const T16*>(a.rows);
-  const T16* kc = reinterpret_cast<const T16*>(a.kc) + h * D;
-  const T16* vc = reinterpret_cast<const T16*>(a.vc) + h * D;
 
   // row-side fragments (B operand of Sᵀ): lane -> row, d = 16s + 8hf .. +7
   u32x4 kf[KS];
@@ -66,60 +64,27 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     const T16* p = rows + ((int64_t)b * a.R + row) * C + h * D + 8 * hf;
 #pragma unroll
     for (int s = 0; s < KS; ++s) kf[s] = row_ok ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0, 0, 0, 0};
+    // retire these loads here, before the first DMA (else: vmcnt(0) inside the loop)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(kf[s]));
   }
 
-  // staging of one 64-column tile (Q_cols and V_cols), global -> registers.  Full tiles use a
-  // scalar tile base + a per-thread 32-bit byte offset (global_load v_off, s[base]).
-  u32x4 rq[LPT], rv[LPT];
-  uint32_t soff[LPT];
-  int stoff[LPT];
-#pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int v = tid + 256 * i;
-    soff[i] = (uint32_t)(((v / CPR) * a.ldkv + (v % CPR) * 8) * 2);
-    stoff[i] = img_off<D>(v / CPR, v % CPR);
-  }
-  const char* kcb = reinterpret_cast<const char*>(kc + (int64_t)b * a.T * a.ldkv);
-  const char* vcb = reinterpret_cast<const char*>(vc + (int64_t)b * a.T * a.ldkv);
-  // the 64-bit mask word of (row, tile) travels with the tile through LDS: a per-lane global
-  // load inside the loop would make the compiler wait vmcnt(0), i.e. for the prefetch too
-  uint64_t mw = 0;
-  const uint64_t* mrow = (a.mbits && tid < 128 && rb * 128 + tid < a.R) ? a.mbits + ((int64_t)b * a.R + rb * 128 + tid) * NKT : nullptr;
-  auto load_tile = [&](int kt) {
-    if (mrow) mw = mrow[kt];
+  // ---- LDS-DMA ring: Q_cols / V_cols images + the workgroup rows' mask words ----
+  ImgDma<D> dma;
+  dma.init(wave, lane);
+  const int ldb = a.ldkv * 2;  // gathered row stride, bytes
+  const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
+  const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
+  const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
+  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
+  auto issue = [&](int kt) {
+    char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
     const int64_t t0 = (int64_t)kt * 64;
-    if (t0 + 64 <= a.T) {
-      const char* bq = kcb + t0 * a.ldkv * 2;
-      const char* bv = vcb + t0 * a.ldkv * 2;
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        rq[i] = *reinterpret_cast<const u32x4*>(bq + soff[i]);
-        rv[i] = *reinterpret_cast<const u32x4*>(bv + soff[i]);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) {
-        // rows past T read row T-1: their scores are masked to -inf, so P = 0 multiplies
-        // finite values (no branch around the loads)
-        const int v = tid + 256 * i, r = v / CPR, c = v % CPR;
-        const int t = min(kt * 64 + r, a.T - 1);
-        const int64_t off = col_off(t, b, a.T, a.ldkv) + c * 8;
-        rq[i] = *reinterpret_cast<const u32x4*>(kc + off);
-        rv[i] = *reinterpret_cast<const u32x4*>(vc + off);
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* qs = smem + buf * STAGE;
-    char* vs = qs + QS_BYTES;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / CPR, c = v % CPR;
-      *reinterpret_cast<u32x4*>(qs + stoff[i]) = rq[i];
-      *reinterpret_cast<u32x4*>(vs + stoff[i]) = rv[i];
-    }
-    if (a.mbits && tid < 128) reinterpret_cast<uint64_t*>(qs + 2 * Img<D>::BYTES)[tid] = mw;
+    const int rmax = a.T - 1 - (int)t0;  // columns past T re-read column T-1 (masked in compute)
+    dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
+    dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
+    if (mwg) glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+    else glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
   };
 
   const float c2 = a.scale * LOG2E;
@@ -134,17 +99,13 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const int NKT4 = (NKT + 3) & ~3;
   const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
 
-  load_tile(kt_beg);
-  store_tile(0);
-  __syncthreads();
-
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
-    const int cur = (kt - kt_beg) & 1;
-    // mask state of this tile first (its vector load must not queue behind the prefetch)
+  // one column tile from ring stage BUF (compile-time: LDS addresses = lane base + immediate)
+  auto tile = [&](auto bufc, int kt) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (kt + PF < kt_end) issue(kt + PF);
+    const char* qs = smem + BUF * CF::STAGE;
+    const char* vs = qs + IMG;
     const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
-    if (kt + 1 < kt_end) load_tile(kt + 1);
-    const char* qs = smem + cur * STAGE;
-    const char* vs = qs + QS_BYTES;
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
       // ---- Sᵀ = Q_cols · K_rowsᵀ : two 32x32 tiles (cols 0-31, 32-63) ----
@@ -164,7 +125,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       // max over raw scores (scale > 0), exponent as one FMA: p = 2^(s*c2 - m)
       float mx = NEG_INF;
       if (flag == 2 || tail) {
-        const uint64_t w = flag == 2 ? reinterpret_cast<const uint64_t*>(qs + 2 * Img<D>::BYTES)[wave * 32 + (lane & 31)] : 0ull;
+        const uint64_t w = flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull;
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -219,8 +180,24 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
         va = vn;
       }
     }
-    if (kt + 1 < kt_end) store_tile(cur ^ 1);
-    __syncthreads();
+    // tile kt+1 complete (this wave's DMAs), everyone done with tile kt, then rotate
+    if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
+    else wait_vm<0>();
+    raw_barrier();
+  };
+
+#pragma unroll
+  for (int t = 0; t < PF; ++t)
+    if (kt_beg + t < kt_end) issue(kt_beg + t);
+  if (PF > 1 && kt_beg + 1 < kt_end) wait_vm<NG * (PF - 1)>();
+  else wait_vm<0>();
+  raw_barrier();
+  for (int kt = kt_beg; kt < kt_end; kt += NBUF) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < kt_end) tile(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (NBUF > 2) {
+      if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
+    }
   }
 
   // ---- epilogue ----
@@ -294,10 +271,10 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  constexpr int STAGE = 2 * Img<D>::BYTES + 128 * 8;
+  constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
   const int nrb = (a.R + 127) / 128;
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
-  else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), 2 * STAGE, st, a);
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   if (a.nsplit > 1) {
     const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
     hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);

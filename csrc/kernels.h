@@ -80,7 +80,10 @@ int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out
                      int b_mc, int vec, hipStream_t st);
 int xdot_softmax_fwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 int xdot_softmax_bwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
-int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_t* flags, int B, int R, int T, hipStream_t st);
+// bool mask (B, R, T) -> row-major bits (B, R, NKT), column-major bits (B, ceil(R/64),
+// ceil(T/128)*128) and tile flags (B, ceil(R/32), NKT4); one read of the mask
+int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint64_t* bt, uint8_t* flags, int B, int R, int T,
+                          hipStream_t st);
 int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
 // δ = rowsum(dO ⊙ O) (reads a->dout, a->B/R/H)
 int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D, hipStream_t st);

@@ -5,6 +5,8 @@
 // module.py:47-50, :66).  Here the mask is read ONCE per forward (R*T bytes, shared by all
 // heads and by the backward) and turned into
 //   bits  (B, R, NKT) uint64 : bit k of word kt = mask[b, r, 64*kt + k]
+//   bitsT (B, NRT, Tpad) uint64: the same bits column-major per 64-row tile (backward
+//         column kernel: one word per lane covers its column's 64 rows)
 //   flags (B, ceil(R/32), NKT4) uint8, NKT4 = NKT rounded up to 4: per 32-row x 64-col tile,
 //         0 = nothing masked, 1 = everything masked (tile skipped), 2 = partial (bits applied
 //         per element).  Rows are padded to 4 bytes so the kernels fetch a tile's flag with a
@@ -15,76 +17,84 @@
 
 namespace xdot {
 
-// 8 lanes per 64-bit word: lane c of a group packs bytes [8c, 8c+8) of the word's 64-byte
-// span into 8 bits, the group ORs its pieces with 3 xor-shuffles, lane 0 stores.  Each lane
-// issues one 8-byte load, consecutive lanes read consecutive bytes (coalesced; rows only need
-// 8-byte alignment, e.g. T = 25000).
-__global__ __launch_bounds__(256) void mask_bits_kernel(const uint8_t* __restrict__ m, uint64_t* __restrict__ bits,
-                                                         int64_t rows, int T, int NKT, bool vec8) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nthreads = rows * NKT * 8;
-  const int64_t w = idx >> 3;            // word index (row-major over (row, kt))
-  const int c = (int)(idx & 7);
-  uint64_t piece = 0;
-  if (idx < nthreads) {
-    const int64_t r = w / NKT;
-    const int kt = (int)(w - r * NKT);
-    const int e0 = kt * 64 + c * 8;
-    const uint8_t* p = m + r * (int64_t)T + e0;
-    if (vec8 && e0 + 8 <= T) {
-      const uint64_t x = *reinterpret_cast<const uint64_t*>(p);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) piece |= (uint64_t)(((x >> (8 * k)) & 0xff) != 0) << k;
-    } else {
-      for (int k = 0; k < 8 && e0 + k < T; ++k) piece |= (uint64_t)(p[k] != 0) << k;
-    }
-    piece <<= 8 * c;
-  }
-  // OR-combine the 8 pieces of the group (all lanes participate in the shuffles)
-  uint32_t lo = (uint32_t)piece, hi = (uint32_t)(piece >> 32);
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    lo |= __shfl_xor(lo, o, 64);
-    hi |= __shfl_xor(hi, o, 64);
-  }
-  if (idx < nthreads && c == 0) bits[w] = ((uint64_t)hi << 32) | lo;
+// One wave per 64-row x 64-column block of one batch: lane i reads row i's 64 mask bytes
+// (eight 8-byte loads; rows only need 8-byte alignment, e.g. T = 25000), packs them into its
+// row word, stores it (bits), turns the 64 row words into 64 column words with a 6-step
+// butterfly transpose across lanes (bits_t) and derives both 32-row flags with two ballots.
+// The mask is read exactly once; column tiles kt in [NKT, KT_ALL) only write padding.
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
 }
 
-// one thread per (b, rb, kt)
-__global__ __launch_bounds__(256) void mask_flags_kernel(const uint64_t* __restrict__ bits, uint8_t* __restrict__ flags,
-                                                          int B, int R, int T, int NKT) {
-  const int NRB = (R + 31) / 32;
-  const int NKT4 = (NKT + 3) & ~3;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)B * NRB * NKT4) return;
-  const int kt = (int)(idx % NKT4);
-  const int64_t brb = idx / NKT4;
-  if (kt >= NKT) { flags[idx] = 1; return; }
-  const int rb = (int)(brb % NRB), b = (int)(brb / NRB);
-  const int n = min(64, T - kt * 64);
-  const uint64_t full = n == 64 ? ~0ull : ((1ull << n) - 1);
-  uint64_t all_and = full, any_or = 0;
-  const int r1 = min(R, rb * 32 + 32);
-  for (int r = rb * 32; r < r1; ++r) {
-    const uint64_t w = bits[((int64_t)b * R + r) * NKT + kt];
-    all_and &= w;
-    any_or |= w;
+__global__ __launch_bounds__(256) void mask_pack_kernel(const uint8_t* __restrict__ m, uint64_t* __restrict__ bits,
+                                                         uint64_t* __restrict__ bt, uint8_t* __restrict__ flags,
+                                                         int B, int R, int T, int NKT, int NKT4, int NRT, int Tpad,
+                                                         int KT_ALL, bool vec8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= (int64_t)B * NRT * KT_ALL) return;  // whole waves exit together
+  const int kt = (int)(blk % KT_ALL);
+  const int64_t brt = blk / KT_ALL;
+  const int rt = (int)(brt % NRT), b = (int)(brt / NRT);
+  const int r = rt * 64 + lane;
+  const bool row_ok = r < R;
+  uint64_t w = 0;
+  if (row_ok && kt < NKT) {
+    const int c0 = kt * 64;
+    const uint8_t* p = m + ((int64_t)b * R + r) * T + c0;
+    if (vec8 && c0 + 64 <= T) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t x = *reinterpret_cast<const uint64_t*>(p + 8 * q);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w |= (uint64_t)(((x >> (8 * k)) & 0xff) != 0) << (8 * q + k);
+      }
+    } else {
+      const int n = min(64, T - c0);
+      for (int k = 0; k < n; ++k) w |= (uint64_t)(p[k] != 0) << k;
+    }
+    bits[((int64_t)b * R + r) * NKT + kt] = w;
   }
-  flags[idx] = any_or == 0 ? 0 : (all_and == full ? 1 : 2);
+  // flags of the two 32-row halves (rows past R count as neither)
+  if (kt < NKT4) {
+    const int n = kt < NKT ? min(64, T - kt * 64) : 0;
+    const uint64_t full = n == 64 ? ~0ull : ((1ull << n) - 1);
+    const uint64_t any = __ballot(w != 0);
+    const uint64_t all = __ballot(!row_ok || w == full);
+    if ((lane & 31) == 0) {
+      const int half = lane >> 5, rb = rt * 2 + half;
+      if (rb < (R + 31) / 32) {
+        const uint32_t a = (uint32_t)(any >> (32 * half)), l = (uint32_t)(all >> (32 * half));
+        flags[((int64_t)b * ((R + 31) / 32) + rb) * NKT4 + kt] = kt >= NKT ? 1 : (a == 0 ? 0 : (l == 0xffffffffu ? 1 : 2));
+      }
+    }
+  }
+  // 64 x 64 bit transpose: lane c ends up with column c (bit i = row i)
+  if (kt * 64 < Tpad) {
+    const uint64_t M[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull, 0x00ff00ff00ff00ffull,
+                           0x0f0f0f0f0f0f0f0full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int j = 32 >> s;
+      const uint64_t o = shfl_xor64(w, j);
+      w = (lane & j) ? (((o >> j) & M[s]) | (w & ~M[s])) : ((w & M[s]) | ((o & M[s]) << j));
+    }
+    bt[((int64_t)b * NRT + rt) * Tpad + (int64_t)kt * 64 + lane] = w;
+  }
 }
 
 }  // namespace xdot
 
-extern "C" int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint8_t* flags, int B, int R, int T,
-                                     hipStream_t st) {
+extern "C" int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint64_t* bt, uint8_t* flags, int B, int R,
+                                     int T, hipStream_t st) {
   using namespace xdot;
-  const int NKT = (T + 63) / 64;
-  const int64_t rows = (int64_t)B * R;
+  const int NKT = (T + 63) / 64, NKT4 = (NKT + 3) & ~3, NRT = (R + 63) / 64, Tpad = (T + 127) / 128 * 128;
+  const int KT_ALL = max(NKT4, Tpad / 64);
   const bool vec8 = (T % 8 == 0) && ((reinterpret_cast<uintptr_t>(mask) & 7) == 0);
-  const int64_t n1 = rows * NKT * 8;
-  if (n1 == 0) return 0;
-  hipLaunchKernelGGL(mask_bits_kernel, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, st, mask, bits, rows, T, NKT, vec8);
-  const int64_t n2 = (int64_t)B * ((R + 31) / 32) * ((NKT + 3) & ~3);
-  hipLaunchKernelGGL(mask_flags_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, bits, flags, B, R, T, NKT);
+  const int64_t nblk = (int64_t)B * NRT * KT_ALL;
+  if (nblk == 0) return 0;
+  hipLaunchKernelGGL(mask_pack_kernel, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, mask, bits, bt, flags, B, R, T,
+                     NKT, NKT4, NRT, Tpad, KT_ALL, vec8);
   return 0;
 }

@@ -122,6 +122,25 @@ def test_mask_pack_flags(gpu):
     assert bits[1, 3, 1].item() == (1 << (100 - 64))
 
 
+@pytest.mark.parametrize("shape", [(2, 70, 150), (1, 200, 1000), (1, 64, 128)])
+def test_mask_pack_column_major(gpu, shape):
+    """bits_t (B, ceil(R/64), Tpad): bit i of word (b, rt, t) == mask[b, 64*rt + i, t]."""
+    from xdot.ops import flash
+
+    B, R, T = shape
+    g = torch.Generator(device="cpu").manual_seed(R)
+    mask = torch.rand(B, R, T, generator=g) < 0.3
+    mk = flash.prepare_mask(mask.to(gpu), B, R, T)
+    NRT, Tpad = (R + 63) // 64, (T + 127) // 128 * 128
+    assert mk.bits_t.shape == (B, NRT, Tpad)
+    bt = mk.bits_t.cpu().view(torch.int64)
+    ref = torch.zeros(B, NRT * 64, Tpad, dtype=torch.bool)
+    ref[:, :R, :T] = mask
+    ref = ref.view(B, NRT, 64, Tpad)
+    got = torch.stack([(bt >> i) & 1 for i in range(64)], dim=2).bool()   # (B, NRT, 64, Tpad)
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("nsplit", [2, 5])
 @pytest.mark.parametrize("masked", [False, True])
 def test_flash_column_split(gpu, nsplit, masked):

@@ -17,12 +17,15 @@ from .. import _ext
 
 
 class PackedMask:
-    """Boolean (B, R, T) mask compressed to per-row bit words + per-tile flags."""
+    """Boolean (B, R, T) mask compressed to per-row bit words ``bits`` (B, R, ceil(T/64)),
+    the same bits column-major per 64-row tile ``bits_t`` (B, ceil(R/64), Tpad) for the
+    backward column kernel, and per (32-row, 64-col) tile ``flags`` (0 none / 1 all / 2 some
+    masked)."""
 
-    __slots__ = ("bits", "flags", "shape")
+    __slots__ = ("bits", "flags", "bits_t", "shape")
 
-    def __init__(self, bits: torch.Tensor, flags: torch.Tensor, shape):
-        self.bits, self.flags, self.shape = bits, flags, tuple(shape)
+    def __init__(self, bits: torch.Tensor, flags: torch.Tensor, bits_t: torch.Tensor, shape):
+        self.bits, self.flags, self.bits_t, self.shape = bits, flags, bits_t, tuple(shape)
 
     @property
     def nothing_masked(self) -> bool:  # host sync; diagnostics only
@@ -34,8 +37,8 @@ def prepare_mask(mask: Optional[torch.Tensor], B: int, R: int, T: int) -> Option
         return None
     if tuple(mask.shape) != (B, R, T):
         raise ValueError(f"mask must be (B, R, T) = {(B, R, T)}, got {tuple(mask.shape)}")
-    bits, flags = _ext.ops().mask_pack(mask.to(torch.bool).contiguous())
-    return PackedMask(bits, flags, mask.shape)
+    bits, flags, bits_t = _ext.ops().mask_pack(mask.to(torch.bool).contiguous())
+    return PackedMask(bits, flags, bits_t, mask.shape)
 
 
 def gathered_to_btc(g: torch.Tensor) -> torch.Tensor:
@@ -84,7 +87,7 @@ def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, sca
     """Gathered-side grads -> (packed fp32 [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
     ``delta`` (from :func:`bwd_delta`) is computed here when not given."""
-    bits, flags = _mask_args(mk)
+    bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta)
 
@@ -100,6 +103,7 @@ def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, s
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,
         lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float):
     """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads)."""
-    bits, flags = _mask_args(mk)
-    return _ext.ops().flash_bwd(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
-                                out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale))
+    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale)
+    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale)
+    C = rows.shape[-1]
+    return drows, dkv[..., :C], dkv[..., C:]

@@ -188,13 +188,19 @@ class SeqParallelAttention(torch.autograd.Function):
             # and 3) the row-side dk on the current stream.  3) fills the partly occupied last
             # workgroup rounds of 1) while the priority keeps 1) (and so the start of the
             # collective) nearly as early as when it runs alone; 2) overlaps the rest of 3).
-            delta = flash.bwd_delta(do, o, H)
+            # δ runs on the priority stream too, so 1) is queued right behind it while 3)
+            # waits for δ: the column kernel reaches the GPU first and keeps the lead
             cur = torch.cuda.current_stream(do.device)
             hi = _side_stream(do.device)
             hi.wait_stream(cur)
             with torch.cuda.stream(hi):
+                delta = flash.bwd_delta(do, o, H)
+                ev = torch.cuda.Event()
+                ev.record(hi)
                 dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta)
                 h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
+            cur.wait_event(ev)
+            delta.record_stream(cur)
             dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
             cur.wait_stream(hi)
             dqv.record_stream(cur)
