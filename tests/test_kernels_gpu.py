@@ -89,3 +89,33 @@ def test_softmax_fully_masked_row_is_nan(gpu):
     mask[0, 1] = True
     y = scale_mask_softmax_fwd(x, mask, 1.0)
     assert torch.isnan(y[0, 0, 1]).all() and not torch.isnan(y[0, 0, 0]).any()
+
+
+@pytest.mark.parametrize("K,M,N", [(25000, 768, 1536), (3125, 768, 768), (300, 96, 200), (7, 64, 64)])
+def test_weight_grad_split_k(gpu, K, M, N):
+    """split-K dW = dyᵀ·x (bf16 in, fp32 accumulation) vs an fp32 torch reference."""
+    from xdot.ops.linear import weight_grad
+
+    g = torch.Generator(device="cpu").manual_seed(K)
+    dy = torch.randn(K, M, generator=g).to(gpu, torch.bfloat16)
+    x = torch.randn(K, N, generator=g).to(gpu, torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    got = weight_grad(dy, x, torch.float32)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item() ** 0.5)
+
+
+def test_linear_fn_grads(gpu):
+    from xdot.ops.linear import linear
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(2, 500, 96, generator=g).to(gpu, torch.bfloat16).requires_grad_(True)
+    w = (0.1 * torch.randn(64, 96, generator=g)).to(gpu, torch.bfloat16).requires_grad_(True)
+    b = torch.randn(64, generator=g).to(gpu, torch.bfloat16).requires_grad_(True)
+    dy = torch.randn(2, 500, 64, generator=g).to(gpu, torch.bfloat16)
+    y = linear(x, w, b)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.linear(xr, wr, br).backward(dy.float())
+    torch.testing.assert_close(y.float(), torch.nn.functional.linear(xr, wr, br), rtol=2e-2, atol=5e-2)
+    for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        torch.testing.assert_close(a.float(), r, rtol=2e-2, atol=2e-2 * r.abs().max().item())

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 
+from ..ops.linear import linear
 from ..ops.softmax import scale_mask_softmax
 from ..parallel.autograd import FullMultiplication, RightTransposeMultiplication
 from ..utils import comm as _comm
@@ -81,13 +82,18 @@ class DistributedDotProductAttn(nn.Module):
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
             pending = start_gather(qv, comm)
-            k = self.keys(keys)
-            return self.composition(seq_parallel_attention_packed(k, qv, attn_mask, self.num_heads, scale,
-                                                                  comm=comm, pending=pending))
+            k = self._proj(self.keys, keys)
+            o = seq_parallel_attention_packed(k, qv, attn_mask, self.num_heads, scale, comm=comm, pending=pending)
+            return self._proj(self.composition, o)
         k = self.keys(keys)
         q = self.queries(queries)
         v = self.values(values)
         return self.composition(self._materialized(k, q, v, attn_mask, scale))
+
+    @staticmethod
+    def _proj(layer: nn.Linear, x: Tensor) -> Tensor:
+        """``layer(x)`` with the split-K MFMA weight gradient (:mod:`xdot.ops.linear`)."""
+        return linear(x, layer.weight, layer.bias)
 
     def _project_qv(self, queries: Tensor, values: Tensor) -> Tensor:
         """[q | v] packed (B, R, 2C): ONE GEMM when ``queries is values`` (self-attention), so
@@ -97,8 +103,8 @@ class DistributedDotProductAttn(nn.Module):
             b = None
             if self.queries.bias is not None:
                 b = torch.cat([self.queries.bias, self.values.bias], 0)
-            return torch.nn.functional.linear(queries, w, b)
-        return torch.cat([self.queries(queries), self.values(values)], dim=-1)
+            return linear(queries, w, b)
+        return torch.cat([self._proj(self.queries, queries), self._proj(self.values, values)], dim=-1)
 
     def _materialized(self, k, q, v, attn_mask, scale):
         H = self.num_heads

@@ -1,0 +1,85 @@
+"""Projection ``Linear`` with a split-K weight gradient on the MFMA GEMM (``csrc/gemm.hip``).
+
+The four projections of the module (reference: ``distributed_dot_product/module.py:36-39``,
+applied at ``:43-45`` and ``:75``) are ordinary ``nn.Linear`` layers; their forward and the
+input gradient ``dX = dY·W`` are well served by hipBLASLt.  The weight gradient
+``dW = dYᵀ·X`` is not: its reduction runs over the sequence (K = T/N rows: 25000 at N = 1)
+while the output is only 768 x 768 (36 MFMA tiles of 128²) — hipBLASLt runs it at
+≈170-330 TF/s with most CUs idle.  Here K is split into S slabs that fill the 256 CUs, each
+slab writes an fp32 partial (bf16 inputs, fp32 accumulation), and one reduction sums them in
+fp32 before the cast to the parameter dtype.
+
+``linear(x, weight, bias)`` is a drop-in for ``torch.nn.functional.linear``; parameters stay
+in the caller's ``nn.Linear`` modules (``state_dict`` compatible with the reference).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from .gemm import strided_gemm
+
+__all__ = ["linear", "weight_grad", "LinearFn"]
+
+_SLOTS = 512       # 2 workgroups per CU x 256 CUs
+_MIN_SLAB = 256    # rows of K per split
+
+
+def _splits(M: int, N: int, K: int) -> int:
+    tiles = -(-M // 128) * -(-N // 128)
+    s = max(1, -(-_SLOTS // tiles))
+    return max(1, min(s, K // _MIN_SLAB, 64))
+
+
+def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """``dyᵀ·x`` for 2-D ``dy`` (K, M) and ``x`` (K, N) -> (M, N), fp32 accumulation."""
+    K, M = dy.shape
+    N = x.shape[1]
+    out_dtype = out_dtype or dy.dtype
+    if not (_ext.use_hip(dy, x) and dy.dtype == x.dtype and dy.dtype in (torch.bfloat16, torch.float16)):
+        return (dy.float().t() @ x.float()).to(out_dtype)
+    dy = dy.contiguous()
+    x = x.contiguous()
+    S = _splits(M, N, K)
+    slab = K // S
+    part = torch.empty(S + (1 if K % S else 0), M, N, dtype=torch.float32, device=dy.device)
+    if slab > 0:
+        strided_gemm(dy, x, part, M=M, N=N, K=slab, nb2=S, lda=M, ldb=N, ldc=N,
+                     sA2=slab * M, sB2=slab * N, sC2=M * N, a_mc=True, b_mc=True)
+    if K % S:
+        r0 = S * slab
+        strided_gemm(dy[r0:], x[r0:], part[S], M=M, N=N, K=K - r0, lda=M, ldb=N, ldc=N,
+                     a_mc=True, b_mc=True)
+    return part.sum(0).to(out_dtype) if part.shape[0] > 1 else part[0].to(out_dtype)
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = dw = db = None
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.float().sum(0).to(dy.dtype)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear`` with the split-K MFMA weight gradient for bf16/fp16 GPU tensors."""
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype \
+            and torch.is_grad_enabled() and _ext.use_hip(x):
+        return LinearFn.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
