@@ -12,7 +12,32 @@
 
 #include "kernels.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdlib>
+
 namespace {
+
+// roctx ranges around every op (visible in rocprofv3 --marker-trace timelines); enabled by
+// XDOT_ROCTX=1 so the default path pays one predictable branch.
+bool roctx_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("XDOT_ROCTX");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+struct Range {
+  bool on;
+  explicit Range(const char* name) : on(roctx_on()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~Range() {
+    if (on) roctxRangePop();
+  }
+};
+
+
 
 int dt_code(at::ScalarType t) {
   switch (t) {
@@ -45,6 +70,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
           int64_t K, int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb,
           int64_t ldc, int64_t sA1, int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1,
           int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha) {
+  Range rr_("xdot.gemm");
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "xdot.gemm: tensors must be on GPU");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "xdot.gemm: A/B dtype mismatch");
   TORCH_CHECK(M >= 0 && N >= 0 && K >= 0 && nseg >= 1 && nb1 >= 1 && nb2 >= 1, "xdot.gemm: bad sizes");
@@ -88,6 +114,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
 // ------------------------------------------------------------------------------------
 at::Tensor softmax_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& mask, double scale,
                        int64_t mdiv, int64_t mmul, int64_t mmod) {
+  Range rr_("xdot.softmax_fwd");
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "xdot.softmax_fwd: x must be a contiguous GPU tensor");
   const int64_t T = x.size(-1);
   const int64_t rows = T == 0 ? 0 : x.numel() / T;
@@ -116,6 +143,7 @@ at::Tensor softmax_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& mas
 }
 
 at::Tensor softmax_bwd(const at::Tensor& y, const at::Tensor& dy, double scale) {
+  Range rr_("xdot.softmax_bwd");
   TORCH_CHECK(y.is_cuda() && y.is_contiguous() && dy.is_contiguous(), "xdot.softmax_bwd: contiguous GPU tensors required");
   TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == dy.scalar_type(), "xdot.softmax_bwd: y/dy mismatch");
   const int64_t T = y.size(-1);
@@ -133,6 +161,7 @@ at::Tensor softmax_bwd(const at::Tensor& y, const at::Tensor& dy, double scale) 
 
 // ------------------------------------------------------------------------------------
 std::tuple<at::Tensor, at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask) {
+  Range rr_("xdot.mask_pack");
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kBool && mask.dim() == 3, "xdot.mask_pack: (B, R, T) bool GPU mask");
   auto m = mask.contiguous();
   const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
@@ -217,6 +246,7 @@ int pick_split(int64_t blocks, int64_t T, int64_t slots, int64_t req) {
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
                                              int64_t H, double scale, int64_t nsplit) {
+  Range rr_("xdot.flash_fwd");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   auto out = at::empty_like(rows);
   auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
@@ -269,6 +299,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
                                                               double scale, const c10::optional<at::Tensor>& delta_in) {
+  Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
@@ -295,8 +326,25 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   return {dkv, delta};
 }
 
+// Σ over the leading (split) dim of fp32 partials, cast to out_dtype, one pass
+at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
+  Range rr_("xdot.sum_partials");
+  TORCH_CHECK(part.is_cuda() && part.is_contiguous() && part.scalar_type() == at::kFloat && part.dim() >= 2,
+              "xdot.sum_partials: contiguous fp32 (S, ...) device tensor");
+  std::vector<int64_t> shape(part.sizes().begin() + 1, part.sizes().end());
+  auto out = at::empty(shape, part.options().dtype(out_dtype));
+  const int64_t n = out.numel();
+  TORCH_CHECK(n % 4 == 0 && aligned16(part.data_ptr()), "xdot.sum_partials: numel % 4 and 16-byte alignment");
+  c10::DeviceGuard guard(part.device());
+  TORCH_CHECK(xdot_sum_partials_launch(part.data_ptr<float>(), out.data_ptr(), (int)part.size(0), n, dt_code(out_dtype),
+                                       cur_stream(part)) == 0, "xdot.sum_partials: unsupported dtype");
+  check_launch(hipGetLastError(), "sum_partials");
+  return out;
+}
+
 // δ = rowsum(dO ⊙ O) per (b, h, row), fp32 (B, H, R)
 at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_t H) {
+  Range rr_("xdot.flash_bwd_delta");
   TORCH_CHECK(dout.is_cuda() && dout.dim() == 3 && dout.is_contiguous() && out.sizes() == dout.sizes() &&
                   out.is_contiguous() && out.scalar_type() == dout.scalar_type() && out.device() == dout.device(),
               "xdot.flash_bwd_delta: dout/out must be matching contiguous (B, R, H*D) device tensors");
@@ -317,6 +365,7 @@ at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_
 at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                           const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                           const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit) {
+  Range rr_("xdot.flash_bwd_rows");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
               "xdot.flash_bwd_rows: delta");
@@ -347,6 +396,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor? delta=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
+  m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
 }
@@ -360,4 +410,5 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_cols", &flash_bwd_cols);
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);
+  m.impl("sum_partials", &sum_partials);
 }

@@ -66,3 +66,23 @@ def test_flash_is_default_on_gpu_bf16(gpu):
     m = xdot.DistributedDotProductAttn(768, num_heads=8).to(gpu, torch.bfloat16)
     x = torch.zeros(1, 8, 768, device=gpu, dtype=torch.bfloat16)
     assert m._pick_impl(x) == "flash"
+
+
+def test_module_flash_deterministic(gpu):
+    """No atomics anywhere on the flash path: two identical steps are bitwise identical
+    (SURVEY §5.2 determinism check)."""
+    import xdot
+
+    torch.manual_seed(0)
+    m = xdot.DistributedDotProductAttn(768, num_heads=8, impl="flash").to(gpu, torch.bfloat16)
+    x = torch.rand(1, 3000, 768, device=gpu, dtype=torch.bfloat16)
+    mask = torch.rand(1, 3000, 3000, device=gpu) < 0.2
+    mask[..., 0] = False
+    res = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        y = m(x, x, x, mask)
+        y.float().square().mean().backward()
+        res.append([y.detach().clone()] + [p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -90,7 +90,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
     if force or jobs_list or _stale(OUT, objs):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT] + objs + [
             "-L", lib, "-Wl,-rpath," + lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-            "-lamdhip64"]
+            "-lamdhip64", "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx"]
         _run(link, verbose)
     return OUT
 

@@ -29,9 +29,14 @@ _MIN_SLAB = 256    # rows of K per split
 
 
 def _splits(M: int, N: int, K: int) -> int:
+    """K slabs: enough (tiles x S) workgroups to fill the GPU, >= _MIN_SLAB rows each; a
+    divisor of K when one is at least a third of the target (no remainder launch)."""
     tiles = -(-M // 128) * -(-N // 128)
-    s = max(1, -(-_SLOTS // tiles))
-    return max(1, min(s, K // _MIN_SLAB, 64))
+    s = max(1, min(-(-_SLOTS // tiles), K // _MIN_SLAB, 64))
+    for d in range(s, max(1, s // 3) - 1, -1):
+        if K % d == 0:
+            return d
+    return s
 
 
 def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
@@ -53,7 +58,9 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
         r0 = S * slab
         strided_gemm(dy[r0:], x[r0:], part[S], M=M, N=N, K=K - r0, lda=M, ldb=N, ldc=N,
                      a_mc=True, b_mc=True)
-    return part.sum(0).to(out_dtype) if part.shape[0] > 1 else part[0].to(out_dtype)
+    if (M * N) % 4 == 0:
+        return _ext.ops().sum_partials(part, out_dtype)
+    return part.sum(0).to(out_dtype)
 
 
 class LinearFn(torch.autograd.Function):
