@@ -109,14 +109,23 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
   const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
   const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
+  const int NKT4 = (NKT + 3) & ~3;
+  const int NRB32 = (a.R + 31) / 32;
+  const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
+  const int fn = min(4, NRB32 - rb * 4);
   auto issue = [&](int kt) {
     char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
     const int64_t t0 = (int64_t)kt * 64;
     const int rmax = a.T - 1 - (int)t0;
     dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
     dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
-    if (mwg) glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
-    else glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
+    if (mwg) {
+      glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
+    } else {  // keeps NG DMAs per wave per tile
+      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+    }
   };
 
   f32x16 dk[DB];
@@ -124,19 +133,18 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   for (int i = 0; i < DB; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
-  const int NKT4 = (NKT + 3) & ~3;
-  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
-
   auto tile = [&](auto bufc, int kt) {
     constexpr int BUF = decltype(bufc)::value;
     if (kt + PF < kt_end) issue(kt + PF);
     const char* qs = smem + BUF * CF::STAGE;
     const char* vs = qs + IMG;
-    const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
+    const int flag = r0 >= a.R ? 1 : (fwg ? staged_flag(qs + CF::OFF_F, wave, kt & 3) : 0);
     const bool tail = (kt + 1) * 64 > a.T;
     if (flag != 1 && r0 < a.R) {
       const bool chk = flag == 2 || tail;
-      const uint64_t w = flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull;
+      const uint64_t w = chk ? tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
+                                         a.T - kt * 64, hf)
+                             : 0ull;
       // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -151,8 +159,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             float x = __builtin_fmaf(s[r], c2, -lse2);
-            const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) x = NEG_INF;
+            if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
             s[r] = fast_exp2(x) * (dp[r] - dlt);  // dSᵀ (unscaled)
           }
         } else {
@@ -223,10 +230,11 @@ template <int D> struct ColsCfg {
   static constexpr int IMG = Img<D>::BYTES;
   static constexpr int IPW = IMG / 4096;  // 1 KiB DMA pieces per wave per image
   static constexpr int OFF_L = 2 * IMG, OFF_D = OFF_L + 256, OFF_W = OFF_D + 256, OFF_X = OFF_W + 1024;
-  static constexpr int STAGE = OFF_X + 256;
+  static constexpr int OFF_F = OFF_X + 256;  // tile flags of the two 32-row halves (glds_flags)
+  static constexpr int STAGE = OFF_F + 256;
   static constexpr int NBUF = (2 * 3 * STAGE <= 160 * 1024) ? 3 : 2;
   static constexpr int PF = NBUF - 1;     // tiles in flight ahead of the one being computed
-  static constexpr int NG = 2 * IPW + 1;  // DMAs per wave per tile
+  static constexpr int NG = 2 * IPW + 2;  // DMAs per wave per tile
 };
 
 template <int DT, int D, int WPS = 2>
@@ -247,6 +255,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   const int C = a.H * D;
   const int NKT = (a.T + 63) / 64;
   const int NRB32 = (a.R + 31) / 32;
+  const int NKT4 = (NKT + 3) & ~3;
   const int c0 = cb * 128 + wave * 32;
   const int col = c0 + (lane & 31);
   const bool col_ok = col < a.T;
@@ -292,6 +301,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     else if (wave == 1) glds4(dlt + r0, ro * 4, st + CF::OFF_D);
     else if (wave == 2 && mb) glds16(mb + (int64_t)rt * TPAD, (uint32_t)lane * 16, st + CF::OFF_W);
     else glds4(lse + r0, ro * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
+    if (a.mflags) glds_flags(a.mflags + ((int64_t)b * NRB32 + 2 * rt) * NKT4, NKT4, min(2, NRB32 - 2 * rt), cb >> 1,
+                             st + CF::OFF_F);
+    else glds4(lse + r0, ro * 4, st + CF::OFF_X);
   };
 
   f32x16 dq[DB], dv[DB];
@@ -346,11 +358,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     }
     int flag = 0;
     if (a.mflags && c0 < a.T) {
-      const int NKT4 = (NKT + 3) & ~3;
-      const uint8_t* fl = a.mflags + (int64_t)b * NRB32 * NKT4;
-      const int ktw = __builtin_amdgcn_readfirstlane(kt_w);
-      const int f0 = tile_flag(fl + (int64_t)(2 * rt) * NKT4, ktw);
-      const int f1 = (2 * rt + 1 < NRB32) ? tile_flag(fl + (int64_t)(2 * rt + 1) * NKT4, ktw) : 1;
+      const int f0 = staged_flag(ks + CF::OFF_F, 0, kt_w & 3);
+      const int f1 = (2 * rt + 1 < NRB32) ? staged_flag(ks + CF::OFF_F, 1, kt_w & 3) : 1;
       flag = __builtin_amdgcn_readfirstlane((f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2));
     }
     if (flag != 1 && c0 < a.T) {

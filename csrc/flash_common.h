@@ -112,10 +112,12 @@ __device__ __forceinline__ Lanes make_lanes(int lane) {
 template <int D>
 __device__ __forceinline__ u32x4 tr_frag(const char* img, int k0, int d0, const Lanes& L) {
   constexpr int ROW = Img<D>::ROW;
-  const char* a0 = img + L.tb0 + k0 * ROW + d0 * 2;
-  const char* a1 = img + L.tb1 + k0 * ROW + d0 * 2;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  // offsets added in the LDS address space: the constant part folds into the instruction's
+  // 16-bit offset instead of a precomputed address register per (k0, d0)
+  typedef const __attribute__((address_space(3))) char lds_char;
+  lds_char* base = (lds_char*)img;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + L.tb0 + (k0 * ROW + d0 * 2)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + L.tb1 + (k0 * ROW + d0 * 2)));
   union { struct { s16x4 a, b; } s; u32x4 u; } c;
   c.s.a = lo;
   c.s.b = hi;
@@ -209,17 +211,43 @@ template <int D> struct ImgDma {
 template <int D> struct RowsCfg {
   static constexpr int IMG = Img<D>::BYTES;
   static constexpr int IPW = ImgDma<D>::IPW;
-  static constexpr int OFF_W = 2 * IMG, OFF_X = OFF_W + 1024;
-  static constexpr int STAGE = OFF_X + 256;
+  static constexpr int OFF_W = 2 * IMG, OFF_X = OFF_W + 1024, OFF_F = OFF_X + 256;
+  static constexpr int STAGE = OFF_F + 256;
   static constexpr int NBUF = (2 * 3 * STAGE <= 160 * 1024) ? 3 : 2;
   static constexpr int PF = NBUF - 1;
-  static constexpr int NG = 2 * IPW + 1;
+  static constexpr int NG = 2 * IPW + 2;
 };
+
+// Tile flags travel with their tile through the LDS ring (a scalar load per tile would put
+// its ~µs latency and an lgkmcnt(0) on every iteration's critical path).  One 4-byte DMA per
+// wave: lane i < nrows fetches dword `dw` of flag row i (rows `stride` bytes apart) into
+// dst + 4 i (lanes >= nrows repeat row 0; the 256-byte area absorbs all 64 lanes).
+__device__ __forceinline__ void glds_flags(const uint8_t* row0, int stride, int nrows, int dw, char* dst) {
+  const int lane = threadIdx.x & 63;
+  glds4(row0 + dw * 4, (uint32_t)((lane < nrows ? lane : 0) * stride), dst);
+}
+// byte `byte` of staged flag dword `idx` (wave-uniform)
+__device__ __forceinline__ int staged_flag(const char* area, int idx, int byte) {
+  const uint32_t v = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(area)[idx]);
+  return (v >> (8 * byte)) & 0xff;
+}
 
 // mask word of workgroup row rr (0..127) for the staged column tile
 __device__ __forceinline__ uint64_t staged_word(const char* stage_w, int rr) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(stage_w);
   return (uint64_t)w[rr] | ((uint64_t)w[128 + rr] << 32);
+}
+
+// Masked-column bits of a 64-column tile for the lane's half (lane >> 5): bit j of the result
+// covers tile column (j & 3) + 8 (j >> 2)... in the MFMA C/D order, i.e. register r of sub-tile
+// tt tests bit tt*32 + (r&3) + 8*(r>>2) (constant positions: no per-lane column indices).
+// Columns past T (tail tile) count as masked.
+__device__ __forceinline__ uint64_t tile_bits(uint64_t w, int valid, int hf) {
+  if (valid < 64) w |= ~0ull << valid;
+  return w >> (4 * hf);
+}
+__device__ __forceinline__ bool bit_at(uint64_t w, int j) {
+  return j < 32 ? ((uint32_t)w >> j) & 1u : ((uint32_t)(w >> 32) >> (j - 32)) & 1u;
 }
 
 // v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;

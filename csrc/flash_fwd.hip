@@ -35,7 +35,7 @@ template <int DT, int D, int WPS = 2>
 __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
-  constexpr int IMG = CF::IMG, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
+  constexpr int IMG = CF::IMG;  // ring of 3 stages (the pipelined loop reads two of them)
   constexpr int KS = D / 16;      // k-steps over the head dim
   constexpr int DB = D / 32;      // 32-wide d blocks of the output
 
@@ -77,14 +77,29 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
   const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
   const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
-  auto issue = [&](int kt) {
-    char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
+  // two rings over the same 3 stages: Q(t) + mask words(t) and V(t) go to stage (t - kt_beg) % 3,
+  // but Q/mask are DMA'd one tile earlier than V (Q(kt+1) is read in iteration kt)
+  constexpr int NQ = ImgDma<D>::IPW + 2, NV = ImgDma<D>::IPW;  // DMAs per wave
+  const int NKT4 = (NKT + 3) & ~3;
+  const int NRB32 = (a.R + 31) / 32;
+  const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
+  const int fn = min(4, NRB32 - rb * 4);
+  auto issue_q = [&](int kt) {
+    char* st = smem + ((kt - kt_beg) % 3) * CF::STAGE;
     const int64_t t0 = (int64_t)kt * 64;
-    const int rmax = a.T - 1 - (int)t0;  // columns past T re-read column T-1 (masked in compute)
-    dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
-    dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
-    if (mwg) glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
-    else glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);  // keeps NG DMAs per wave per tile
+    dma.issue(kcb + t0 * ldb, ldb, a.T - 1 - (int)t0, st, wave);  // columns past T re-read T-1 (masked)
+    if (mwg) {
+      glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
+    } else {  // same DMA count with or without a mask
+      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+    }
+  };
+  auto issue_v = [&](int kt) {
+    char* st = smem + ((kt - kt_beg) % 3) * CF::STAGE;
+    const int64_t t0 = (int64_t)kt * 64;
+    dma.issue(vcb + t0 * ldb, ldb, a.T - 1 - (int)t0, st + IMG, wave);
   };
 
   const float c2 = a.scale * LOG2E;
@@ -96,108 +111,168 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
 
-  const int NKT4 = (NKT + 3) & ~3;
-  const uint8_t* flags = a.mflags ? a.mflags + ((int64_t)b * ((a.R + 31) / 32) + __builtin_amdgcn_readfirstlane(r0 >> 5)) * NKT4 : nullptr;
 
-  // one column tile from ring stage BUF (compile-time: LDS addresses = lane base + immediate)
-  auto tile = [&](auto bufc, int kt) {
-    constexpr int BUF = decltype(bufc)::value;
-    if (kt + PF < kt_end) issue(kt + PF);
-    const char* qs = smem + BUF * CF::STAGE;
-    const char* vs = qs + IMG;
-    const int flag = (flags && r0 < a.R) ? tile_flag(flags, kt) : 0;
-    const bool tail = (kt + 1) * 64 > a.T;
-    if (flag != 1 && r0 < a.R) {
-      // ---- Sᵀ = Q_cols · K_rowsᵀ : two 32x32 tiles (cols 0-31, 32-63) ----
-      f32x16 s[2];
-      {
-        u32x4 qa = row_frag<D>(qs, 0, 0, L);
+  // ---- software-pipelined sweep ----------------------------------------------------
+  // Iteration kt overlaps the MFMAs of one tile with the VALU work of another:
+  //   block A: Sᵀ(kt+1) = Q(kt+1)·Kᵀ (12 MFMAs)   ||  P(kt) = 2^(S(kt)·c2 - m), packed to bf16
+  //   block B: Oᵀ += V(kt)ᵀ·P(kt)ᵀ (12 MFMAs)     ||  row sums of P(kt), row max of S(kt+1)
+  // then the (rare, deferred) rescale for tile kt+1.  The score registers alternate between
+  // two sets (PAR) and the ring stage rotates over three (BUF): the loop is unrolled by 6 so
+  // both are compile-time.  Iteration kt DMAs Q(kt+3) and V(kt+2): each has one full
+  // iteration in flight before the wait at the bottom of the next one.
+  constexpr float RESCALE_LOG2 = 8.f;  // deferred max: p <= 2^8 between rescales (exact in fp32 / bf16)
+  f32x16 sv[2][2];
+  // flag of tile kt from the stage holding Q(kt) (1 = skip: wave past R / past the split)
+  auto flag_of = [&](int kt, const char* st) -> int {
+    if (r0 >= a.R || kt >= kt_end) return 1;
+    return fwg ? staged_flag(st + CF::OFF_F, wave, kt & 3) : 0;
+  };
+  auto s_tile = [&](f32x16 (&s)[2], const char* qs) {
+    u32x4 qa = row_frag<D>(qs, 0, 0, L);
 #pragma unroll
-        for (int i = 0; i < 2 * KS; ++i) {
-          const int tt = i / KS, ks = i % KS;
-          u32x4 qn = qa;
-          if (i + 1 < 2 * KS) qn = row_frag<D>(qs, ((i + 1) / KS) * 32, (i + 1) % KS, L);
-          s[tt] = mfma32<DT>::run(qa, kf[ks], ks == 0 ? f32x16{} : s[tt]);
-          qa = qn;
-        }
-      }
-      // ---- online softmax (lane-local row, partner lane = lane ^ 32) ----
-      // max over raw scores (scale > 0), exponent as one FMA: p = 2^(s*c2 - m)
-      float mx = NEG_INF;
-      if (flag == 2 || tail) {
-        const uint64_t w = flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kk = tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            if (((w >> kk) & 1ull) || kt * 64 + kk >= a.T) s[tt][r] = NEG_INF;
-            mx = fmaxf(mx, s[tt][r]);
-          }
-      } else {
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
-      }
-      mx = pair_max(mx) * c2;
-      const float m_new = fmaxf(m_run, mx);
-      const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
-      // rescale the running output only when some row of the wave raised its max
-      if (__any(m_new > m_run)) {
-        const float alpha = fast_exp2(m_run - m_use);
-        l_run *= alpha;
-#pragma unroll
-        for (int i = 0; i < DB; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-      }
-      m_run = m_new;
-      float ls = 0.f;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(__builtin_fmaf(s[tt][r], c2, -m_use));
-          s[tt][r] = p;
-          ls += p;
-        }
-      l_run += ls;
-      // ---- Oᵀ += V_colsᵀ · Pᵀ ----
-      u32x4 pf[4];
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int sh = 0; sh < 2; ++sh) pf[tt * 2 + sh] = acc_to_frag<DT>(s[tt], sh);
-      // operand reads run one MFMA ahead of their use
-      u32x4 va = tr_frag<D>(vs, 0, 0, L);
-#pragma unroll
-      for (int i = 0; i < 4 * DB; ++i) {
-        const int db = i >> 2, k4 = i & 3;
-        u32x4 vn = va;
-        if (i + 1 < 4 * DB) vn = tr_frag<D>(vs, ((i + 1) & 3) * 16, ((i + 1) >> 2) * 32, L);
-        o[db] = mfma32<DT>::run(va, pf[k4], o[db]);
-        va = vn;
-      }
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int tt = i / KS, ks = i % KS;
+      u32x4 qn = qa;
+      if (i + 1 < 2 * KS) qn = row_frag<D>(qs, ((i + 1) / KS) * 32, (i + 1) % KS, L);
+      s[tt] = mfma32<DT>::run(qa, kf[ks], ks == 0 ? f32x16{} : s[tt]);
+      qa = qn;
     }
-    // tile kt+1 complete (this wave's DMAs), everyone done with tile kt, then rotate
-    if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
+  };
+  // mask (partial words / tail columns) or blank (fully masked) a score tile in place
+  auto mask_tile = [&](f32x16 (&s)[2], int kt, int flag, const char* st) {
+    if (flag == 1) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[tt][r] = NEG_INF;
+      return;
+    }
+    const uint64_t w = tile_bits(flag == 2 ? staged_word(st + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
+                                 a.T - kt * 64, hf);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) s[tt][r] = NEG_INF;
+  };
+  auto row_max = [&](const f32x16 (&s)[2]) {
+    float mx = NEG_INF;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
+    return pair_max(mx) * c2;
+  };
+  auto rescale_to = [&](float mx) {
+    const float m_new = fmaxf(m_run, mx);
+    if (__any(m_new > m_run + RESCALE_LOG2)) {
+      const float alpha = fast_exp2(m_run - ((m_new == NEG_INF) ? 0.f : m_new));
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < DB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      m_run = m_new;
+    }
+  };
+
+  int flag_cur = 1;
+  auto iter = [&](auto bufc, auto parc, int kt) {
+    constexpr int BUF = decltype(bufc)::value, PAR = decltype(parc)::value;
+    f32x16 (&sc)[2] = sv[PAR];
+    f32x16 (&sn)[2] = sv[PAR ^ 1];
+    const bool dq = kt + 3 < kt_end, dv = kt + 2 < kt_end;
+    if (dq) issue_q(kt + 3);
+    if (dv) issue_v(kt + 2);
+    const char* cur = smem + BUF * CF::STAGE;             // V(kt)
+    const char* nxt = smem + ((BUF + 1) % 3) * CF::STAGE; // Q(kt+1), mask words (kt+1)
+    // flag(kt) was read one iteration ago (its stage is being refilled with Q(kt+3) now)
+    const int flag_c = flag_cur, flag_n = flag_of(kt + 1, nxt);
+    flag_cur = flag_n;
+    if (flag_c != 1 || flag_n != 1) {
+      const float m_use = (m_run == NEG_INF) ? 0.f : m_run;
+      // ---- block A: S(kt+1) MFMAs, each followed by its share of P(kt) = 2^(S·c2 - m) ----
+      // Written in issue order and fenced with sched_barrier so the compiler keeps the MFMA /
+      // VALU interleave (it otherwise clusters the MFMAs); operand reads run two MFMAs ahead.
+      constexpr int NA = 2 * KS, NB = 4 * DB;
+      u32x4 pf[4];
+      {
+        u32x4 q0 = row_frag<D>(nxt, 0, 0, L), q1 = row_frag<D>(nxt, (1 / KS) * 32, 1 % KS, L);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int tt = i / KS, ks = i % KS;
+          u32x4 q2 = q1;
+          if (i + 2 < NA) q2 = row_frag<D>(nxt, ((i + 2) / KS) * 32, (i + 2) % KS, L);
+          sn[tt] = mfma32<DT>::run(q0, kf[ks], ks == 0 ? f32x16{} : sn[tt]);
+#pragma unroll
+          for (int j = (i * 32) / NA; j < ((i + 1) * 32) / NA; ++j) {
+            sc[j >> 4][j & 15] = fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
+            if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          q0 = q1;
+          q1 = q2;
+        }
+      }
+      // ---- block B: P(kt)·V(kt) MFMAs, each followed by its share of the row sums ----
+      float ls = 0.f;
+      {
+        u32x4 v0 = tr_frag<D>(cur + IMG, 0, 0, L), v1 = tr_frag<D>(cur + IMG, 16, 0, L);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int db = i >> 2, k4 = i & 3;
+          u32x4 v2 = v1;
+          if (i + 2 < NB) v2 = tr_frag<D>(cur + IMG, ((i + 2) & 3) * 16, ((i + 2) >> 2) * 32, L);
+          o[db] = mfma32<DT>::run(v0, pf[k4], o[db]);
+#pragma unroll
+          for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
+          asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
+          __builtin_amdgcn_sched_barrier(0);
+          v0 = v1;
+          v1 = v2;
+        }
+      }
+      l_run += ls;
+      if (flag_n != 0 || (kt + 2) * 64 > a.T) mask_tile(sn, kt + 1, flag_n, nxt);
+      rescale_to(row_max(sn));
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sn[tt][r] = NEG_INF;
+    }
+    // Q(kt+2) and V(kt+1) (issued one iteration ago) complete; this iteration's DMAs fly on
+    if (dq) wait_vm<NQ + NV>();
+    else if (dv) wait_vm<NV>();
     else wait_vm<0>();
     raw_barrier();
   };
 
+  if (kt_beg < kt_end) {
 #pragma unroll
-  for (int t = 0; t < PF; ++t)
-    if (kt_beg + t < kt_end) issue(kt_beg + t);
-  if (PF > 1 && kt_beg + 1 < kt_end) wait_vm<NG * (PF - 1)>();
-  else wait_vm<0>();
-  raw_barrier();
-  for (int kt = kt_beg; kt < kt_end; kt += NBUF) {
-    tile(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < kt_end) tile(std::integral_constant<int, 1>{}, kt + 1);
-    if constexpr (NBUF > 2) {
-      if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
+    for (int t = 0; t < 3; ++t) {
+      if (kt_beg + t < kt_end) issue_q(kt_beg + t);
+      if (t < 2 && kt_beg + t < kt_end) issue_v(kt_beg + t);
     }
+    wait_vm<0>();
+    raw_barrier();
+    // prologue: S of the first tile, masked, its max sets m
+    const int f0 = flag_of(kt_beg, smem);
+    flag_cur = f0;
+    if (f0 != 1) s_tile(sv[0], smem);
+    if (f0 != 0 || (kt_beg + 1) * 64 > a.T) mask_tile(sv[0], kt_beg, f0, smem);
+    rescale_to(row_max(sv[0]));
+  }
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  for (int kt = kt_beg; kt < kt_end; kt += 6) {
+    iter(I0{}, I0{}, kt);
+    if (kt + 1 < kt_end) iter(I1{}, I1{}, kt + 1);
+    if (kt + 2 < kt_end) iter(I2{}, I0{}, kt + 2);
+    if (kt + 3 < kt_end) iter(I0{}, I1{}, kt + 3);
+    if (kt + 4 < kt_end) iter(I1{}, I0{}, kt + 4);
+    if (kt + 5 < kt_end) iter(I2{}, I1{}, kt + 5);
   }
 
   // ---- epilogue ----
@@ -271,7 +346,7 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
+  constexpr int LDS = 3 * RowsCfg<D>::STAGE;
   const int nrb = (a.R + 127) / 128;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
