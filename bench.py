@@ -78,7 +78,8 @@ def main(argv=None, comm=None):
     model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl,
                                         comm=comm).to(dev, dt)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
-    sync = GradSync(model, comm=comm)
+    sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
+    # projection's all-reduce overlaps the attention backward
     crit = torch.nn.MSELoss()
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)

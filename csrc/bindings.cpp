@@ -298,13 +298,14 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const at::Tensor& out, const at::Tensor& lse,
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
-                                                              double scale, const c10::optional<at::Tensor>& delta_in) {
+                                                              double scale, const c10::optional<at::Tensor>& delta_in,
+                                                              bool fp32_out) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
-  auto dkv = at::empty({g.B, g.T, 2 * g.C}, kc.options().dtype(at::kFloat));
+  auto dkv = at::empty({g.B, g.T, 2 * g.C}, fp32_out ? kc.options().dtype(at::kFloat) : kc.options());
   const bool have_delta = delta_in.has_value() && delta_in->defined();
   at::Tensor delta;
   if (have_delta) {
@@ -314,7 +315,8 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   } else {
     delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   }
-  a.dkc = dkv.data_ptr<float>(); a.dvc = dkv.data_ptr<float>() + g.C; a.ldg = 2 * g.C;
+  a.dkc = dkv.data_ptr(); a.dvc = static_cast<char*>(dkv.data_ptr()) + g.C * dkv.element_size(); a.ldg = 2 * g.C;
+  a.dkv16 = fp32_out ? 0 : 1;
   a.delta = delta.data_ptr<float>();
   c10::DeviceGuard guard(rows.device());
   const int dt = dt_code(rows.scalar_type());
@@ -394,7 +396,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
-        "Tensor? flags, int H, float scale, Tensor? delta=None) -> (Tensor, Tensor)");
+        "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "

@@ -398,10 +398,26 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       if (rt + 2 < NRT) tile(std::integral_constant<int, 2>{}, rt + 2);
     }
   }
-  if (col_ok) {
+  if (col_ok && a.dkv16) {  // input dtype: half the store (and reduce-scatter) bytes
     const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
-    float* pq = a.dkc + off;
-    float* pv = a.dvc + off;
+    T16* pq = reinterpret_cast<T16*>(a.dkc) + off;
+    T16* pv = reinterpret_cast<T16*>(a.dvc) + off;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 q2, v2;
+        q2[0] = pack2<DT>(dq[db][4 * g] * a.scale, dq[db][4 * g + 1] * a.scale);
+        q2[1] = pack2<DT>(dq[db][4 * g + 2] * a.scale, dq[db][4 * g + 3] * a.scale);
+        v2[0] = pack2<DT>(dv[db][4 * g], dv[db][4 * g + 1]);
+        v2[1] = pack2<DT>(dv[db][4 * g + 2], dv[db][4 * g + 3]);
+        *reinterpret_cast<u32x2*>(pq + db * 32 + 8 * g + 4 * hf) = q2;
+        *reinterpret_cast<u32x2*>(pv + db * 32 + 8 * g + 4 * hf) = v2;
+      }
+  } else if (col_ok) {
+    const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
+    float* pq = reinterpret_cast<float*>(a.dkc) + off;
+    float* pv = reinterpret_cast<float*>(a.dvc) + off;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll

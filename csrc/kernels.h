@@ -59,13 +59,14 @@ struct BwdArgs {
   const float* lse;        // (B, H, R)
   const float* delta;      // (B, H, R) rowsum(dO * O)
   void* drows;             // (B, R, H*D)   grad of row side (out dtype)
-  float* dkc;              // (B, T, ldkv) fp32 partial grads of the gathered key side
-  float* dvc;              // (B, T, ldkv) fp32 partial grads of the gathered value side
+  void* dkc;               // (B, T, ldg) partial grads of the gathered key side (fp32 or the input dtype)
+  void* dvc;               // (B, T, ldg) partial grads of the gathered value side
+  int dkv16;               // 1: dkc/dvc are in the input dtype (bf16/fp16), 0: fp32
   const uint64_t* mbits;
   const uint8_t* mflags;
   int B, H, R, T;
   int64_t ldkv;            // element stride between gathered input rows
-  int64_t ldg;             // element stride between rows of the fp32 dkc/dvc outputs
+  int64_t ldg;             // element stride between rows of the dkc/dvc outputs
   float scale;
   int nsplit;              // column splits of the row-side kernel
   float* dpart;            // (nsplit, B, R, H*D) fp32 partial row-side grads (nsplit > 1)

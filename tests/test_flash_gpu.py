@@ -188,3 +188,21 @@ def test_flash_bwd_delta_and_given_delta(gpu):
     dkv2, d2 = flash.bwd_cols(do, rows, kc, vc, o, lse, None, H, 0.125, delta)
     assert d2.data_ptr() == delta.data_ptr()
     assert torch.equal(d1, delta) and torch.equal(dkv1, dkv2)
+
+
+def test_flash_bwd_cols_input_dtype_output(gpu):
+    """fp32_out=False rounds the same fp32 accumulators once to bf16: bitwise equal to
+    casting the fp32 output."""
+    from xdot.ops import flash
+
+    B, R, T, H, D = 1, 130, 700, 2, 96
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rows, kc, vc, do = (torch.randn(B, n, H * D, generator=g).to(gpu, torch.bfloat16) for n in (R, T, T, R))
+    mask = (torch.rand(B, R, T, generator=g) < 0.3).to(gpu)
+    mask[..., 0] = False
+    mk = flash.prepare_mask(mask, B, R, T)
+    o, lse = flash.fwd(rows, kc, vc, mk, H, 0.1)
+    d32, _ = flash.bwd_cols(do, rows, kc, vc, o, lse, mk, H, 0.1)
+    d16, _ = flash.bwd_cols(do, rows, kc, vc, o, lse, mk, H, 0.1, fp32_out=False)
+    assert d32.dtype == torch.float32 and d16.dtype == torch.bfloat16
+    assert torch.equal(d16, d32.to(torch.bfloat16))

@@ -83,13 +83,15 @@ def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
 
 
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
-             delta: Optional[torch.Tensor] = None):
-    """Gathered-side grads -> (packed fp32 [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
+             delta: Optional[torch.Tensor] = None, fp32_out: bool = True):
+    """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
-    ``delta`` (from :func:`bwd_delta`) is computed here when not given."""
+    ``delta`` (from :func:`bwd_delta`) is computed here when not given.  The grads are fp32
+    (``fp32_out``) or rounded once to the input dtype in the kernel epilogue."""
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
-                                     out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta)
+                                     out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
+                                     bool(fp32_out))
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0):

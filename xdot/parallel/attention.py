@@ -34,6 +34,7 @@ from torch import Tensor
 from .. import _ext
 from ..utils import comm as _comm
 from ..utils.checks import check_consistent
+from ..utils.env import FLAGS
 
 __all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "start_gather", "flash_supported",
            "SeqParallelAttention"]
@@ -173,7 +174,7 @@ class SeqParallelAttention(torch.autograd.Function):
         C = k.shape[-1]
         do = do.contiguous()
 
-        def reduce_async(parts):  # (N, B, R, 2C) rank-major fp32 partials
+        def reduce_async(parts):  # (N, B, R, 2C) rank-major partials
             if n == 1:
                 return None, parts[0]
             out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
@@ -197,7 +198,9 @@ class SeqParallelAttention(torch.autograd.Function):
                 delta = flash.bwd_delta(do, o, H)
                 ev = torch.cuda.Event()
                 ev.record(hi)
-                dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta)
+                # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
+                # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
+                dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta, fp32_out=FLAGS.grad_fp32)
                 h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
             cur.wait_event(ev)
             delta.record_stream(cur)

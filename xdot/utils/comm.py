@@ -415,6 +415,9 @@ def init(backend: str = "auto", timeout_s: Optional[float] = None, set_device: b
     be = resolve_backend(backend)
     if be == "nccl":
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # RCCL's kernels share the CUs with long-running attention kernels: high-priority
+        # collective streams let their workgroups dispatch as soon as any slot frees
+        os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         if set_device and torch.cuda.is_available():
             torch.cuda.set_device(get_local_rank() % max(1, torch.cuda.device_count()))
     kw = {}

@@ -10,6 +10,11 @@
                                (default: fail loudly)
 ``XDOT_COMM_TIMEOUT_S``        collective timeout in seconds (default 600)
 ``XDOT_CHUNK_BUDGET_MB``       transient-buffer budget used by the chunk planner
+``XDOT_GRAD_FP32``             ``1``: the fused attention's gathered-side gradient partials are
+                               kept and reduce-scattered in fp32 (default: rounded once to
+                               the bf16/fp16 compute dtype in the kernel, half the bytes)
+``XDOT_ROCTX``                 ``1``: roctx ranges around every native op (rocprofv3 markers)
+``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
 from __future__ import annotations
@@ -35,6 +40,7 @@ class _Flags:
         self.backend = os.environ.get("XDOT_BACKEND", "auto").lower()
         self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
         self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
+        self.grad_fp32 = _flag("XDOT_GRAD_FP32")
 
 
 FLAGS = _Flags()
