@@ -102,9 +102,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
 
-  ImgDma<D> dma;
-  dma.init(wave, lane);
   const int ldb = a.ldkv * 2;
+  ImgDma<D> dma;
+  dma.init(wave, lane, ldb);
   const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
   const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   const int NRT = (a.R + 63) / 64;
 
   ImgDma<D> dma;
-  dma.init(wave, lane);
+  dma.init(wave, lane, C * 2);
   const char* rows_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.rows) + (int64_t)b * a.R * C + h * D);
   const char* dout_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.dout) + (int64_t)b * a.R * C + h * D);
   const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;

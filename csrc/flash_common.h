@@ -185,22 +185,29 @@ __device__ __forceinline__ void glds4(const void* base, uint32_t off, const char
 // tile row p / ROW (padding positions of D = 64/128 images load chunk 0: any valid address).
 template <int D> struct ImgDma {
   static constexpr int IPW = Img<D>::BYTES / 4096;
-  int row[IPW], col[IPW];
-  __device__ __forceinline__ void init(int wave, int lane) {
+  int off[IPW], row[IPW];  // per lane: byte offset of its chunk in a full tile, tile row
+  __device__ __forceinline__ void init(int wave, int lane, int stride_bytes) {
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const int p = (wave * IPW + i) * 1024 + lane * 16, r = p / Img<D>::ROW;
       int c = ((p % Img<D>::ROW) >> 4) ^ ((r >> 2) & 3);
       if (c >= D / 8) c = 0;
       row[i] = r;
-      col[i] = c * 16;
+      off[i] = r * stride_bytes + c * 16;
     }
   }
-  // tile rows past rmax re-read row rmax (callers mask them); base is the tile's first row
+  // base is the tile's first row; a full tile uses the precomputed offsets as the DMA's
+  // 32-bit VGPR offset (no per-DMA address arithmetic), rows past rmax (tail tile) re-read
+  // row rmax (callers mask them)
   __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int wave) const {
+    if (rmax >= 63) {
 #pragma unroll
-    for (int i = 0; i < IPW; ++i)
-      glds16(base, (uint32_t)(min(row[i], rmax) * stride_bytes + col[i]), img + (wave * IPW + i) * 1024);
+      for (int i = 0; i < IPW; ++i) glds16(base, (uint32_t)off[i], img + (wave * IPW + i) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < IPW; ++i)
+        glds16(base, (uint32_t)(off[i] - (row[i] - min(row[i], rmax)) * stride_bytes), img + (wave * IPW + i) * 1024);
+    }
   }
 };
 

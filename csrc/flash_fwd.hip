@@ -70,9 +70,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   }
 
   // ---- LDS-DMA ring: Q_cols / V_cols images + the workgroup rows' mask words ----
-  ImgDma<D> dma;
-  dma.init(wave, lane);
   const int ldb = a.ldkv * 2;  // gathered row stride, bytes
+  ImgDma<D> dma;
+  dma.init(wave, lane, ldb);
   const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
   const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
