@@ -250,7 +250,8 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   auto out = at::empty_like(rows);
   auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
-  const int ns = pick_split(((g.R + 127) / 128) * g.B * H, g.T, 512, nsplit);
+  const int rpw = xdot_flash_fwd_rows_per_wg();
+  const int ns = pick_split(((g.R + rpw - 1) / rpw) * g.B * H, g.T, 512, nsplit);
   at::Tensor opart, lpart;
   if (ns > 1) {
     opart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));

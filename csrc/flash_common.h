@@ -239,10 +239,11 @@ __device__ __forceinline__ int staged_flag(const char* area, int idx, int byte) 
   return (v >> (8 * byte)) & 0xff;
 }
 
-// mask word of workgroup row rr (0..127) for the staged column tile
+// mask word of workgroup row rr (0..ROWS-1) for the staged column tile ([dword][ROWS rows])
+template <int ROWS = 128>
 __device__ __forceinline__ uint64_t staged_word(const char* stage_w, int rr) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(stage_w);
-  return (uint64_t)w[rr] | ((uint64_t)w[128 + rr] << 32);
+  return (uint64_t)w[rr] | ((uint64_t)w[ROWS + rr] << 32);
 }
 
 // Masked-column bits of a 64-column tile for the lane's half (lane >> 5): bit j of the result

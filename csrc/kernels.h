@@ -93,4 +93,6 @@ int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStr
 int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 // out (n elements, dtype dto) = Σ_s part[s] (fp32 partials, n % 4 == 0)
 int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int dto, hipStream_t st);
+// rows per workgroup of the forward kernel (depends on XDOT_FWD_ROWS)
+int xdot_flash_fwd_rows_per_wg();
 }
