@@ -42,6 +42,8 @@ def parse(argv=None):
     ap.add_argument("--offset", type=int, default=None)
     ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random"])
     ap.add_argument("--no-optim", action="store_true", help="(diagnostic) skip the optimizer step")
+    ap.add_argument("--optim", default="xdot", choices=["xdot", "torch"],
+                    help="AdamW implementation: xdot.FusedAdamW (one HIP launch) or torch's fused AdamW")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"],
                     help="collective backend (auto = RCCL on GPU); gloo lets several ranks share one GPU "
@@ -77,7 +79,10 @@ def main(argv=None, comm=None):
     torch.manual_seed(1234)  # identical weights on every rank
     model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl,
                                         comm=comm).to(dev, dt)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
+    if a.optim == "xdot":
+        opt = xdot.FusedAdamW(model.parameters(), lr=1e-4)  # one multi-tensor HIP launch per step
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
     sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
     # projection's all-reduce overlaps the attention backward
     crit = torch.nn.MSELoss()

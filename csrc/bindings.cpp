@@ -14,6 +14,7 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <cmath>
 #include <cstdlib>
 
 namespace {
@@ -345,6 +346,49 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
   return out;
 }
 
+// one AdamW step for lists of same-dtype params / grads with fp32 moments (chunks of 32)
+void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_avg, at::TensorList exp_avg_sq,
+                double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+  Range rr_("xdot.adamw_step");
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n && exp_avg.size() == n && exp_avg_sq.size() == n, "xdot.adamw_step: list sizes");
+  TORCH_CHECK(step >= 1, "xdot.adamw_step: step counts from 1");
+  if (n == 0) return;
+  const auto dtype = params[0].scalar_type();
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(params[i].is_cuda() && params[i].is_contiguous() && params[i].scalar_type() == dtype,
+                "xdot.adamw_step: contiguous GPU params of one dtype");
+    TORCH_CHECK(grads[i].sizes() == params[i].sizes() && grads[i].is_contiguous() && grads[i].scalar_type() == dtype,
+                "xdot.adamw_step: grad shape/dtype");
+    for (const at::Tensor* s : {&exp_avg[i], &exp_avg_sq[i]})
+      TORCH_CHECK(s->numel() == params[i].numel() && s->is_contiguous() && s->scalar_type() == at::kFloat,
+                  "xdot.adamw_step: fp32 moments");
+  }
+  const float bc1 = 1.f - (float)std::pow(beta1, (double)step);
+  const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
+  c10::DeviceGuard guard(params[0].device());
+  for (size_t c0 = 0; c0 < n; c0 += xdot::ADAM_MAX_T) {
+    xdot::AdamArgs a{};
+    int blk = 0;
+    a.nt = (int)std::min<size_t>(xdot::ADAM_MAX_T, n - c0);
+    for (int i = 0; i < a.nt; ++i) {
+      const size_t k = c0 + i;
+      a.p[i] = params[k].data_ptr(); a.g[i] = grads[k].data_ptr();
+      a.m[i] = exp_avg[k].data_ptr<float>(); a.v[i] = exp_avg_sq[k].data_ptr<float>();
+      a.n[i] = params[k].numel();
+      a.blk0[i] = blk;
+      const int64_t nb = (a.n[i] + xdot::ADAM_BLOCK_ELEMS - 1) / xdot::ADAM_BLOCK_ELEMS;
+      TORCH_CHECK(blk + nb < (1LL << 31), "xdot.adamw_step: too many elements");
+      blk += (int)nb;
+    }
+    a.blk0[a.nt] = blk;
+    a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps; a.wd = (float)weight_decay;
+    a.bc1 = bc1; a.bc2_sqrt = std::sqrt(bc2);
+    TORCH_CHECK(xdot_adamw_launch(&a, dt_code(dtype), cur_stream(params[0])) == 0, "xdot.adamw_step: dtype");
+    check_launch(hipGetLastError(), "adamw_step");
+  }
+}
+
 // δ = rowsum(dO ⊙ O) per (b, h, row), fp32 (B, H, R)
 at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_t H) {
   Range rr_("xdot.flash_bwd_delta");
@@ -400,6 +444,8 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
+  m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
+        "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
 }
@@ -414,4 +460,5 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);
   m.impl("sum_partials", &sum_partials);
+  m.impl("adamw_step", &adamw_step);
 }

@@ -76,6 +76,22 @@ struct BwdArgs {
 
 }  // namespace xdot
 
+namespace xdot {
+// multi-tensor AdamW (csrc/optim.hip): up to ADAM_MAX_T tensors per launch
+constexpr int ADAM_MAX_T = 32;
+constexpr int ADAM_BLOCK_ELEMS = 256 * 4;
+struct AdamArgs {
+  void* p[ADAM_MAX_T];
+  const void* g[ADAM_MAX_T];
+  float* m[ADAM_MAX_T];
+  float* v[ADAM_MAX_T];
+  int64_t n[ADAM_MAX_T];
+  int blk0[ADAM_MAX_T + 1];  // first block of each tensor (prefix sum)
+  int nt;
+  float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
+};
+}  // namespace xdot
+
 extern "C" {
 int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc,
                      int b_mc, int vec, hipStream_t st);
@@ -95,4 +111,6 @@ int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStr
 int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int dto, hipStream_t st);
 // rows per workgroup of the forward kernel (depends on XDOT_FWD_ROWS)
 int xdot_flash_fwd_rows_per_wg();
+// one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
+int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
 }

@@ -1,0 +1,54 @@
+// xdot — multi-tensor fused AdamW for gfx950: ONE launch updates every parameter.
+//
+// The module's parameters are four projection matrices (reference: distributed_dot_product/
+// module.py:36-39); the reference trains them with a stock optimizer.  torch's fused AdamW
+// takes ≈50 µs on MI355X for these 2.4M parameters — more than the 14 B/parameter of memory
+// traffic the update needs (≈6 µs at HBM rate).  Here one kernel walks all tensors: the
+// per-tensor pointers and the block -> tensor map travel in the (by-value) kernel argument,
+// each thread updates 4 elements with fp32 math and fp32 moments (exp_avg, exp_avg_sq), and the
+// parameter is written back in its own dtype.  Semantics match torch.optim.AdamW
+// (decoupled weight decay, bias-corrected moments, amsgrad = False).
+#include "common.h"
+
+namespace xdot {
+
+template <int DT>
+__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
+  using TP = typename dt_traits<DT>::T;
+  const int blk = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.nt && blk >= a.blk0[t + 1]) ++t;  // wave-uniform search over <= 32 entries
+  const int64_t base = (int64_t)(blk - a.blk0[t]) * ADAM_BLOCK_ELEMS + threadIdx.x * 4;
+  const int64_t n = a.n[t];
+  TP* p = reinterpret_cast<TP*>(a.p[t]);
+  const TP* g = reinterpret_cast<const TP*>(a.g[t]);
+  float* m = a.m[t];
+  float* v = a.v[t];
+  const float step_size = a.lr / a.bc1, decay = 1.f - a.lr * a.wd;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = base + e;
+    if (i >= n) break;
+    const float gi = (float)g[i];
+    const float mi = a.beta1 * m[i] + (1.f - a.beta1) * gi;
+    const float vi = a.beta2 * v[i] + (1.f - a.beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float pi = (float)p[i] * decay;
+    p[i] = (TP)(pi - step_size * mi / (__builtin_sqrtf(vi) / a.bc2_sqrt + a.eps));
+  }
+}
+
+}  // namespace xdot
+
+extern "C" int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st) {
+  using namespace xdot;
+  if (a->nt <= 0) return 0;
+  const dim3 grid((unsigned)a->blk0[a->nt]);
+  if (grid.x == 0) return 0;
+  if (dt == DT_F32) hipLaunchKernelGGL(adamw_kernel<DT_F32>, grid, dim3(256), 0, st, *a);
+  else if (dt == DT_BF16) hipLaunchKernelGGL(adamw_kernel<DT_BF16>, grid, dim3(256), 0, st, *a);
+  else if (dt == DT_F16) hipLaunchKernelGGL(adamw_kernel<DT_F16>, grid, dim3(256), 0, st, *a);
+  else return -1;
+  return 0;
+}

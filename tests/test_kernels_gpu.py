@@ -119,3 +119,27 @@ def test_linear_fn_grads(gpu):
     torch.testing.assert_close(y.float(), torch.nn.functional.linear(xr, wr, br), rtol=2e-2, atol=5e-2)
     for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         torch.testing.assert_close(a.float(), r, rtol=2e-2, atol=2e-2 * r.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_adamw_kernel(gpu, dtype):
+    """One multi-tensor HIP launch == torch.optim.AdamW on fp32 copies (fp32 moments)."""
+    from xdot.ops.optim import FusedAdamW
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    shapes = [(768, 768), (1536, 768), (3,), (1000, 7)]
+    p32 = [torch.randn(*s, generator=g) for s in shapes]
+    gr = [torch.randn(*s, generator=g) for s in shapes]
+    kw = dict(lr=3e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.05)
+    ours = [p.to(gpu, dtype).requires_grad_(True) for p in p32]
+    ref = [p.to(gpu).requires_grad_(True) for p in p32]
+    o1, o2 = FusedAdamW(ours, **kw), torch.optim.AdamW(ref, **kw)
+    for s in range(3):
+        for p, q, x in zip(ours, ref, gr):
+            p.grad = (x * (s + 1)).to(gpu, dtype)
+            q.grad = p.grad.float()
+        o1.step()
+        o2.step()
+    for p, q in zip(ours, ref):
+        tol = 1e-6 if dtype == torch.float32 else 2e-2
+        torch.testing.assert_close(p.float(), q.detach(), rtol=tol, atol=tol)

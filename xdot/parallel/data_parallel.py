@@ -117,7 +117,11 @@ class GradSync:
 
     def _launch(self, i):
         b = self.buckets[i]
-        flat = torch.cat([p.grad.reshape(-1) for p in b])
+        g0 = b[0].grad
+        if len(b) == 1 and g0.is_contiguous():
+            flat = g0  # one-tensor bucket: reduce the gradient in place (no flatten / copy back)
+        else:
+            flat = torch.cat([p.grad.reshape(-1) for p in b])
         h = self.comm.all_reduce(flat, op="sum", async_op=True)
         self._handles.append((i, flat, h))
 
@@ -128,8 +132,11 @@ class GradSync:
             h.wait()
             if self.op == "avg":
                 flat.div_(ws)
+            b = self.buckets[i]
+            if len(b) == 1 and flat is b[0].grad:
+                continue
             off = 0
-            for p in self.buckets[i]:
+            for p in b:
                 n = p.numel()
                 p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
