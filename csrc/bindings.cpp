@@ -430,6 +430,104 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   return drows;
 }
 
+// ---- chunked launches (gather / reduce-scatter pipelining) ----------------------------
+// column splits the row-block kernels would use for (R rows, T columns) — the caller sizes the
+// partial buffers with it
+int64_t flash_splits(int64_t B, int64_t R, int64_t T, int64_t H, bool rows_kernel) {
+  const int rpw = rows_kernel ? 128 : xdot_flash_fwd_rows_per_wg();
+  return pick_split(((R + rpw - 1) / rpw) * B * H, T, 512, 0);
+}
+
+void check_part(const at::Tensor& t, int64_t slots_needed, int64_t per_slot, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.dim() >= 1 &&
+                  t.size(0) >= slots_needed && t.numel() == t.size(0) * per_slot,
+              "xdot: partial buffer ", what, " has the wrong shape/dtype");
+}
+
+// forward over this column chunk into partial slots [sp0, sp0 + nsplit) of opart / lpart
+void flash_fwd_partial(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
+                       const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags, int64_t H,
+                       double scale, at::Tensor& opart, at::Tensor& lpart, int64_t sp0, int64_t nsplit) {
+  Range rr_("xdot.flash_fwd_partial");
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  TORCH_CHECK(sp0 >= 0 && nsplit >= 1, "xdot.flash_fwd_partial: slots");
+  const int ns = pick_split(1, g.T, 1, nsplit);  // clamps nsplit to the column tiles
+  check_part(opart, sp0 + ns, g.B * g.R * g.C, "opart");
+  check_part(lpart, sp0 + ns, g.B * H * g.R, "lpart");
+  xdot::fa::FwdArgs a{};
+  a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr();
+  const bool hb = bits.has_value() && bits->defined();
+  a.mbits = hb ? reinterpret_cast<const uint64_t*>(bits->data_ptr()) : nullptr;
+  a.mflags = hb ? flags->data_ptr<uint8_t>() : nullptr;
+  a.B = (int)g.B; a.H = (int)H; a.R = (int)g.R; a.T = (int)g.T; a.scale = (float)scale;
+  a.ldkv = g.ld;
+  a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1;
+  a.opart = opart.data_ptr<float>(); a.lpart = lpart.data_ptr<float>();
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
+              "xdot.flash_fwd_partial: config");
+  check_launch(hipGetLastError(), "flash_fwd_partial");
+}
+
+// merge all slots of opart / lpart -> (out in like's dtype, lse)
+std::tuple<at::Tensor, at::Tensor> flash_fwd_combine(const at::Tensor& opart, const at::Tensor& lpart, int64_t H,
+                                                     const at::Tensor& like) {
+  Range rr_("xdot.flash_fwd_combine");
+  TORCH_CHECK(like.dim() == 3 && like.is_cuda(), "xdot.flash_fwd_combine: like (B, R, C)");
+  const int64_t B = like.size(0), R = like.size(1), C = like.size(2), S = opart.size(0);
+  TORCH_CHECK(H > 0 && C % H == 0, "xdot.flash_fwd_combine: H");
+  check_part(opart, S, B * R * C, "opart");
+  check_part(lpart, S, B * H * R, "lpart");
+  auto out = at::empty_like(like);
+  auto lse = at::empty({B, H, R}, like.options().dtype(at::kFloat));
+  xdot::fa::FwdArgs a{};
+  a.out = out.data_ptr(); a.lse = lse.data_ptr<float>();
+  a.B = (int)B; a.H = (int)H; a.R = (int)R; a.nsplit = (int)S;
+  a.opart = opart.data_ptr<float>(); a.lpart = lpart.data_ptr<float>();
+  c10::DeviceGuard guard(like.device());
+  TORCH_CHECK(xdot_flash_fwd_combine_launch(&a, dt_code(like.scalar_type()), (int)(C / H), cur_stream(like)) == 0,
+              "xdot.flash_fwd_combine: config");
+  check_launch(hipGetLastError(), "flash_fwd_combine");
+  return {out, lse};
+}
+
+// row-side grads of this column chunk into partial slots [sp0, sp0 + nsplit) of dpart
+void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
+                            const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
+                            const c10::optional<at::Tensor>& flags, int64_t H, double scale, at::Tensor& dpart,
+                            int64_t sp0, int64_t nsplit) {
+  Range rr_("xdot.flash_bwd_rows_partial");
+  const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
+              "xdot.flash_bwd_rows_partial: delta");
+  TORCH_CHECK(sp0 >= 0 && nsplit >= 1, "xdot.flash_bwd_rows_partial: slots");
+  const int ns = pick_split(1, g.T, 1, nsplit);
+  check_part(dpart, sp0 + ns, g.B * g.R * g.C, "dpart");
+  auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
+  a.delta = delta.data_ptr<float>();
+  a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1; a.dpart = dpart.data_ptr<float>();
+  c10::DeviceGuard guard(rows.device());
+  TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
+              "xdot.flash_bwd_rows_partial: config");
+  check_launch(hipGetLastError(), "flash_bwd_rows_partial");
+}
+
+// Σ of all dpart slots -> (B, R, C) in like's dtype
+at::Tensor flash_bwd_rows_sum(const at::Tensor& dpart, int64_t H, const at::Tensor& like) {
+  Range rr_("xdot.flash_bwd_rows_sum");
+  const int64_t B = like.size(0), R = like.size(1), C = like.size(2), S = dpart.size(0);
+  check_part(dpart, S, B * R * C, "dpart");
+  auto out = at::empty_like(like);
+  xdot::fa::BwdArgs a{};
+  a.drows = out.data_ptr(); a.dpart = dpart.data_ptr<float>();
+  a.B = (int)B; a.H = (int)H; a.R = (int)R; a.nsplit = (int)S;
+  c10::DeviceGuard guard(like.device());
+  TORCH_CHECK(xdot_flash_bwd_rows_sum_launch(&a, dt_code(like.scalar_type()), (int)(C / H), cur_stream(like)) == 0,
+              "xdot.flash_bwd_rows_sum: config");
+  check_launch(hipGetLastError(), "flash_bwd_rows_sum");
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(xdot, m) {
@@ -444,10 +542,21 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
+  m.def("flash_splits(int B, int R, int T, int H, bool rows_kernel) -> int");
+  m.def("flash_fwd_partial(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, "
+        "Tensor(a!) opart, Tensor(b!) lpart, int sp0, int nsplit) -> ()");
+  m.def("flash_fwd_combine(Tensor opart, Tensor lpart, int H, Tensor like) -> (Tensor, Tensor)");
+  m.def("flash_bwd_rows_partial(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
+        "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit) -> ()");
+  m.def("flash_bwd_rows_sum(Tensor dpart, int H, Tensor like) -> Tensor");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
+  m.impl("flash_splits", &flash_splits);
 }
 
 TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
@@ -460,5 +569,9 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);
   m.impl("sum_partials", &sum_partials);
+  m.impl("flash_fwd_partial", &flash_fwd_partial);
+  m.impl("flash_fwd_combine", &flash_fwd_combine);
+  m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);
+  m.impl("flash_bwd_rows_sum", &flash_bwd_rows_sum);
   m.impl("adamw_step", &adamw_step);
 }

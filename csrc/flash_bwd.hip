@@ -192,8 +192,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
       if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
     }
   }
-  if (row_ok && a.nsplit > 1) {
-    float* op = a.dpart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
+  if (row_ok && (a.nsplit > 1 || a.force_partial)) {
+    float* op = a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -461,15 +461,18 @@ static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
 }
 
 template <int DT, int D>
+static void launch_rows_sum(const BwdArgs& a, hipStream_t st) {
+  const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
+  hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
+}
+
+template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
   constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-  if (a.nsplit > 1) {
-    const int64_t n4 = (int64_t)a.B * a.R * a.H * D / 4;
-    hipLaunchKernelGGL((flash_bwd_rows_sum<DT, D>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
-  }
+  if (a.nsplit > 1 && !a.force_partial) launch_rows_sum<DT, D>(a, st);
 }
 
 }  // namespace fa
@@ -503,6 +506,16 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
 #define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
 #undef XC
+}
+
+// sum a->nsplit slots of dpart into drows (input dtype)
+extern "C" int xdot_flash_bwd_rows_sum_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+#define XS(DTV, DV) launch_rows_sum<DTV, DV>(*a, st)
+  XB_DISPATCH(XS)
+#undef XS
 }
 
 extern "C" int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st) {

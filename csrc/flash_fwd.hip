@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   // ---- epilogue ----
   const float l_tot = pair_sum(l_run);
   const float inv = 1.f / l_tot;
-  if (row_ok && a.nsplit == 1) {
+  if (row_ok && a.nsplit == 1 && !a.force_partial) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
   } else if (row_ok) {
     // split partial: normalised fp32 output + its LSE; merged by flash_fwd_combine
-    float* op = a.opart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
+    float* op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
         f32x4 v = {o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
         *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
       }
-    if (hf == 0) a.lpart[(((int64_t)sp * a.B + b) * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
+    if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
   }
 }
 
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
     const int row = r0 + 32 * u + (lane & 31);
     const float l_tot = pair_sum(l_run[u]);
     const float inv = 1.f / l_tot;
-    if (row < a.R && a.nsplit == 1) {
+    if (row < a.R && a.nsplit == 1 && !a.force_partial) {
       T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
 #pragma unroll
       for (int db = 0; db < DB; ++db)
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
         }
       if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run[u] + __log2f(l_tot)) * LN2;
     } else if (row < a.R) {
-      float* op = a.opart + (((int64_t)sp * a.B + b) * a.R + row) * C + h * D;
+      float* op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
 #pragma unroll
       for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
           f32x4 v = {o[u][db][4 * g] * inv, o[u][db][4 * g + 1] * inv, o[u][db][4 * g + 2] * inv, o[u][db][4 * g + 3] * inv};
           *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
         }
-      if (hf == 0) a.lpart[(((int64_t)sp * a.B + b) * a.H + h) * a.R + row] = (m_run[u] + __log2f(l_tot)) * LN2;
+      if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = (m_run[u] + __log2f(l_tot)) * LN2;
     }
   }
 }
@@ -560,6 +560,12 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
   if ((c4 * 4) % D == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
 }
 
+template <int DT, int D>
+static void launch_combine(const FwdArgs& a, hipStream_t st) {
+  const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
+  hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+}
+
 // rows per wave of the forward kernel: 32 (flash_fwd_kernel, default) or 64
 // (flash_fwd64_kernel, XDOT_FWD_ROWS=64; read once per process).  Measured on MI355X at the
 // headline shapes: 64 rows/wave is 2 % faster at R = 25000 but 6 % slower at R = 3125 (256-row
@@ -584,10 +590,7 @@ static void launch_fwd(const FwdArgs& a, hipStream_t st) {
     if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
     else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   }
-  if (a.nsplit > 1) {
-    const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
-    hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
-  }
+  if (a.nsplit > 1 && !a.force_partial) launch_combine<DT, D>(a, st);
 }
 
 }  // namespace fa
@@ -595,6 +598,18 @@ static void launch_fwd(const FwdArgs& a, hipStream_t st) {
 
 // rows per workgroup of the forward kernel (grid / split planning on the host)
 extern "C" int xdot_flash_fwd_rows_per_wg() { return 4 * xdot::fa::fwd_rows_per_wave(); }
+
+// merge a->nsplit partial slots of opart/lpart into out/lse
+extern "C" int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+#define XF(DTV, DV) if (dt == DTV && D == DV) { launch_combine<DTV, DV>(*a, st); return 0; }
+  XF(DT_BF16, 32) XF(DT_BF16, 64) XF(DT_BF16, 96) XF(DT_BF16, 128)
+  XF(DT_F16, 32) XF(DT_F16, 64) XF(DT_F16, 96) XF(DT_F16, 128)
+#undef XF
+  return -1;
+}
 
 extern "C" int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st) {
   using namespace xdot;

@@ -47,8 +47,10 @@ struct FwdArgs {
   int64_t ldkv;            // element stride between gathered rows (H*D, or 2*H*D when packed [q|v])
   float scale;             // softmax scale (not log2-scaled)
   int nsplit;              // column splits (>1: partials to opart/lpart, then combine)
-  float* opart;            // (nsplit, B, R, H*D) fp32 normalised partial outputs
-  float* lpart;            // (nsplit, B, H, R) partial LSE
+  float* opart;            // (slots, B, R, H*D) fp32 normalised partial outputs
+  float* lpart;            // (slots, B, H, R) partial LSE
+  int sp0;                 // first partial slot of this launch (chunked launches)
+  int force_partial;       // 1: write partials even with nsplit == 1 (no combine here)
 };
 
 struct BwdArgs {
@@ -69,7 +71,9 @@ struct BwdArgs {
   int64_t ldg;             // element stride between rows of the dkc/dvc outputs
   float scale;
   int nsplit;              // column splits of the row-side kernel
-  float* dpart;            // (nsplit, B, R, H*D) fp32 partial row-side grads (nsplit > 1)
+  float* dpart;            // (slots, B, R, H*D) fp32 partial row-side grads (nsplit > 1)
+  int sp0;                 // first partial slot of this launch (chunked launches)
+  int force_partial;       // 1: write partials even with nsplit == 1 (summed separately)
 };
 
 }  // namespace fa
@@ -113,4 +117,8 @@ int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
 int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
+// merge a->nsplit partial slots (a->opart, a->lpart) into a->out / a->lse
+int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
+// sum a->nsplit slots of a->dpart into a->drows
+int xdot_flash_bwd_rows_sum_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 }

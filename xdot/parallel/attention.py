@@ -26,7 +26,7 @@ schedule with a torch reference implementation of steps 2-5.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -62,6 +62,53 @@ def _gather_rows(comm, x: Tensor, async_op: bool = True):
     out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
     h = comm.all_gather_into(out, x, async_op=async_op)
     return h if async_op else out
+
+
+def _row_chunks(n: int, R: int, hip: bool) -> List[Tuple[int, int]]:
+    """Row chunks (r0, rc) of every rank's shard for the pipelined gather of the fused path:
+    with several ranks the gathered side can travel in ``XDOT_GATHER_CHUNKS`` all-gathers so
+    chunk c+1 is in flight while the kernels consume chunk c (and, in backward, chunk c's
+    reduce-scatter runs while chunk c+1's gradients are computed).  Default 1: measured on
+    one MI355X with emulated 8-rank shapes, 2 chunks cost ≈0.23 ms more compute per step
+    (per-chunk mask copies, split partials, half-occupied last workgroup rounds), about what
+    the overlap can save over xGMI."""
+    nc = FLAGS.gather_chunks if (hip and n > 1) else 1
+    nc = max(1, min(nc, R // 64))
+    base, extra = divmod(R, nc)
+    out, r0 = [], 0
+    for c in range(nc):
+        rc = base + (1 if c < extra else 0)
+        out.append((r0, rc))
+        r0 += rc
+    return out
+
+
+class _PendingGather:
+    """All-gathers of the row chunks of one packed operand, issued back to back on the
+    collective stream; ``wait(c)`` orders the current stream after chunk c only."""
+
+    def __init__(self, comm, x: Tensor, chunks: List[Tuple[int, int]]):
+        self.chunks = chunks
+        self.n = comm.world_size
+        x = x.contiguous()
+        self.handles = []
+        for r0, rc in chunks:
+            self.handles.append(_gather_rows(comm, x[:, r0:r0 + rc]))
+        self._bufs: List[Optional[Tensor]] = [None] * len(chunks)
+
+    def wait(self, c: int) -> Tensor:
+        if self._bufs[c] is None:
+            self._bufs[c] = self.handles[c].wait()          # (N, B, rc, 2C)
+        return self._bufs[c]
+
+    def wait_all(self) -> List[Tensor]:
+        return [self.wait(c) for c in range(len(self.chunks))]
+
+
+def _chunk_columns(n: int, R: int, r0: int, rc: int, device) -> Tensor:
+    """global columns of a gathered chunk, in its rank-major order: j*R + r0 + i"""
+    j = torch.arange(n, device=device).view(n, 1) * R
+    return (j + r0 + torch.arange(rc, device=device).view(1, rc)).reshape(-1)
 
 
 def _as_global(g: Tensor) -> Tensor:
@@ -141,90 +188,148 @@ def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
 # ----------------------------------------------------------------------------------------
 class SeqParallelAttention(torch.autograd.Function):
     """Fused seq-parallel attention on a PACKED gathered-side operand ``qv`` = [q | v]
-    (B, R, 2C): one all-gather in forward, one reduce-scatter in backward."""
+    (B, R, 2C): all-gather(s) in forward, reduce-scatter(s) in backward.  With several ranks
+    the gathered side moves in row chunks (:func:`_row_chunks`): the kernels run per chunk
+    into split partials (merged by one combine) so communication overlaps compute."""
 
     @staticmethod
     def forward(ctx, k, qv, mask, H, scale, comm, pending=None):
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
-        pending = pending if pending is not None else _gather_rows(comm, qv)
+        B, R = k.shape[0], k.shape[1]
+        n = comm.world_size
         use_hip = _ext.use_hip(k) and k.dtype in (torch.bfloat16, torch.float16)
+        if pending is None:
+            pending = _PendingGather(comm, qv, _row_chunks(n, qv.shape[1], use_hip))
+        chunks = pending.chunks
         if use_hip:
             from ..ops import flash
 
-            # the mask is packed while the gather is in flight
-            mk = flash.prepare_mask(mask, k.shape[0], k.shape[1], qv.shape[1] * comm.world_size) \
-                if mask is not None else None
-            qvg = flash.gathered_to_btc(pending.wait())          # (B, T, 2C), a view for B = 1
-            qg, vg = qvg[..., :C], qvg[..., C:]
-            o, lse = flash.fwd(k, qg, vg, mk, H, scale)
+            # masks are packed per chunk while the gathers are in flight
+            mks = []
+            for r0, rc in chunks:
+                if mask is None:
+                    mks.append(None)
+                    continue
+                mc = mask if len(chunks) == 1 else mask.index_select(2, _chunk_columns(n, R, r0, rc, mask.device))
+                mks.append(flash.prepare_mask(mc, B, R, n * rc))
+            if len(chunks) == 1:
+                qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
+                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mks[0], H, scale)
+                bufs = [qvg]
+            else:
+                ops = _ext.ops()
+                ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, False))
+                opart = torch.empty(len(chunks) * ns, B, R, C, dtype=torch.float32, device=k.device)
+                lpart = torch.empty(len(chunks) * ns, B, H, R, dtype=torch.float32, device=k.device)
+                bufs = []
+                for c in range(len(chunks)):
+                    g = flash.gathered_to_btc(pending.wait(c))   # (B, N*rc, 2C)
+                    bufs.append(g)
+                    bits, flags = (mks[c].bits, mks[c].flags) if mks[c] is not None else (None, None)
+                    ops.flash_fwd_partial(k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
+                                          float(scale), opart, lpart, c * ns, ns)
+                o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
         else:
-            mk = mask
-            qvg = pending.wait()                                 # (N, B, R, 2C)
+            mks = [mask]
+            qvg = torch.cat(pending.wait_all(), dim=2) if len(chunks) > 1 else pending.wait(0)  # (N, B, R, 2C)
             o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
-        ctx.save_for_backward(k, qvg, o, lse)
-        ctx.mk, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mk, H, scale, comm, use_hip
+            bufs = [qvg]
+        ctx.save_for_backward(k, o, lse, *bufs)
+        ctx.mks, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, chunks, H, scale, comm, use_hip
         return o
 
     @staticmethod
     def backward(ctx, do):
-        k, qvg, o, lse = ctx.saved_tensors
-        comm, H, scale = ctx.comm, ctx.H, ctx.scale
+        k, o, lse, *bufs = ctx.saved_tensors
+        comm, H, scale, chunks = ctx.comm, ctx.H, ctx.scale, ctx.chunks
         n = comm.world_size
         C = k.shape[-1]
+        B, R = k.shape[0], k.shape[1]
         do = do.contiguous()
 
-        def reduce_async(parts):  # (N, B, R, 2C) rank-major partials
+        def reduce_async(parts, out=None):  # (N, B, rc, 2C) rank-major partials -> (B, rc, 2C)
             if n == 1:
                 return None, parts[0]
-            out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
+            if out is None:
+                out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
             return comm.reduce_scatter(out, parts, async_op=True), out
 
         if ctx.use_hip:
             from ..ops import flash
 
-            qg, vg = qvg[..., :C], qvg[..., C:]
-            # δ, then two independent kernels on two streams: 1) gathered-side grads for all T
-            # columns on a HIGH-priority stream, followed there by 2) the ONE reduce-scatter,
-            # and 3) the row-side dk on the current stream.  3) fills the partly occupied last
-            # workgroup rounds of 1) while the priority keeps 1) (and so the start of the
-            # collective) nearly as early as when it runs alone; 2) overlaps the rest of 3).
-            # δ runs on the priority stream too, so 1) is queued right behind it while 3)
-            # waits for δ: the column kernel reaches the GPU first and keeps the lead
+            # δ, then two independent streams: 1) gathered-side grads, chunk by chunk, on a
+            # HIGH-priority stream, each chunk followed there by ITS reduce-scatter (chunk c's
+            # collective overlaps chunk c+1's kernel), and 2) the row-side dk on the current
+            # stream.  2) fills the partly occupied last workgroup rounds of 1) while the
+            # priority keeps 1) (and so the collectives) nearly as early as when it runs
+            # alone.  δ runs on the priority stream too, so 1) reaches the GPU first.
             cur = torch.cuda.current_stream(do.device)
             hi = _side_stream(do.device)
             hi.wait_stream(cur)
+            handles, outs = [], []
             with torch.cuda.stream(hi):
                 delta = flash.bwd_delta(do, o, H)
                 ev = torch.cuda.Event()
                 ev.record(hi)
-                # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
-                # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
-                dkv, _ = flash.bwd_cols(do, k, qg, vg, o, lse, ctx.mk, H, scale, delta, fp32_out=FLAGS.grad_fp32)
-                h, dqv = reduce_async(flash.btc_to_rank_major(dkv, n))
+                dqv = None
+                if n > 1 and len(chunks) > 1 and B == 1:
+                    dqv = torch.empty(B, R, 2 * C, dtype=k.dtype if not FLAGS.grad_fp32 else torch.float32,
+                                      device=k.device)
+                for c, (r0, rc) in enumerate(chunks):
+                    g = bufs[c]
+                    # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
+                    # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
+                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[c], H, scale, delta,
+                                            fp32_out=FLAGS.grad_fp32)
+                    h, oc = reduce_async(flash.btc_to_rank_major(dkv, n), None if dqv is None else dqv[:, r0:r0 + rc])
+                    handles.append(h)
+                    outs.append(oc)
             cur.wait_event(ev)
             delta.record_stream(cur)
-            dk = flash.bwd_rows(do, k, qg, vg, lse, delta, ctx.mk, H, scale)
+            if len(chunks) == 1:
+                g = bufs[0]
+                dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, ctx.mks[0], H, scale)
+            else:
+                ops = _ext.ops()
+                ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))
+                dpart = torch.empty(len(chunks) * ns, B, R, C, dtype=torch.float32, device=k.device)
+                for c in range(len(chunks)):
+                    g = bufs[c]
+                    mk = ctx.mks[c]
+                    bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
+                    ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
+                                               flags, int(H), float(scale), dpart, c * ns, ns)
+                dk = ops.flash_bwd_rows_sum(dpart, int(H), k)
             cur.wait_stream(hi)
-            dqv.record_stream(cur)
+            for oc in outs:
+                oc.record_stream(cur)
+            if dqv is None:
+                dqv = outs[0] if len(outs) == 1 else torch.cat(outs, dim=1)
+            else:
+                dqv.record_stream(cur)
         else:
-            dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mk, H, scale)
+            qvg = bufs[0]
+            dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mks[0], H, scale)
             h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))
-        if h is not None:
-            h.wait()
+            handles = [h]
+        for h in handles:
+            if h is not None:
+                h.wait()
         return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None
 
 
-def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None) -> _comm.Handle:
-    """Issue the all-gather of the packed gathered side early (e.g. before the row-side
-    projection GEMM) and hand the handle to :func:`seq_parallel_attention_packed`."""
+def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None) -> "_PendingGather":
+    """Issue the all-gather(s) of the packed gathered side early (e.g. before the row-side
+    projection GEMM) and hand the result to :func:`seq_parallel_attention_packed`."""
     comm = comm or _comm.get_comm()
-    return _gather_rows(comm, qv.detach())
+    hip = _ext.use_hip(qv) and qv.dtype in (torch.bfloat16, torch.float16)
+    return _PendingGather(comm, qv.detach(), _row_chunks(comm.world_size, qv.shape[1], hip))
 
 
 def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,
                                   comm: Optional[_comm.Communicator] = None,
-                                  pending: Optional[_comm.Handle] = None) -> Tensor:
+                                  pending: Optional["_PendingGather"] = None) -> Tensor:
     """Fused sequence-parallel attention with a packed gathered side ``qv = [q | v]`` (B, R, 2C).
 
     ``pending``: the handle of :func:`start_gather` on this ``qv`` (the gather is issued here

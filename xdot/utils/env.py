@@ -14,6 +14,10 @@
                                kept and reduce-scattered in fp32 (default: rounded once to
                                the bf16/fp16 compute dtype in the kernel, half the bytes)
 ``XDOT_ROCTX``                 ``1``: roctx ranges around every native op (rocprofv3 markers)
+``XDOT_GATHER_CHUNKS``         row chunks of the fused attention's all-gather / reduce-scatter
+                               pipeline with several ranks (default 1 = one collective each; 2+
+                               overlaps them with the kernels at ~0.2 ms extra compute per
+                               8-rank step: worth it only on a slow interconnect)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
@@ -41,6 +45,7 @@ class _Flags:
         self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
         self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
+        self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
 
 
 FLAGS = _Flags()
