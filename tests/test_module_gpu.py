@@ -86,3 +86,11 @@ def test_module_flash_deterministic(gpu):
         res.append([y.detach().clone()] + [p.grad.clone() for p in m.parameters()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_module_multi_rank_gather_chunks(gpu, monkeypatch, chunks):
+    """The chunked all-gather / reduce-scatter pipeline (XDOT_GATHER_CHUNKS) gives the same
+    outputs and input gradients as the dense reference (2 ranks sharing the GPU over gloo)."""
+    monkeypatch.setenv("XDOT_GATHER_CHUNKS", str(chunks))
+    run_gloo(_module_case, 2, "flash", True, timeout=400)
