@@ -46,6 +46,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-local", action="store_true", help="skip the single-GPU torch.matmul baseline")
     ap.add_argument("--file", default=None, help="JSON list to append the record to")
+    ap.add_argument("--emulate", type=int, default=None, metavar="N",
+                    help="run ONE rank of an N-rank job on this device (EmulatedComm: collectives are "
+                         "device-local copies) -- per-rank compute of the reference's N=3 setup on 1 GPU")
     return ap.parse_args(argv)
 
 
@@ -99,7 +102,9 @@ def main(argv=None):
     from xdot.utils import comm as C
     import xdot.parallel.functional as F
 
-    comm = C.init("auto")
+    comm = C.EmulatedComm(a.emulate) if a.emulate else C.init("auto")
+    ctx = C.use_comm(comm)  # the functional ops pick up the thread's communicator
+    ctx.__enter__()
     n, rank = comm.world_size, comm.rank
     dev = torch.device("cuda", C.get_local_rank() % max(1, torch.cuda.device_count())) \
         if torch.cuda.is_available() else torch.device("cpu")
@@ -111,12 +116,12 @@ def main(argv=None):
     R, D = T // n, a.dim
     torch.manual_seed(111)
     torch.set_grad_enabled(False)
-    rec = {"mode": a.mode, "world_size": n, "T": T, "D": D, "offset": a.offset, "dtype": a.dtype}
+    rec = {"mode": a.mode, "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype}
 
     fb = a.mode.endswith("_fb")
     torch.set_grad_enabled(fb)
     # single-GPU torch baseline on the full problem (reference: rank 0 only)
-    if rank == 0 and not a.no_local and not fb:
+    if rank == 0 and not a.no_local and not fb and not a.emulate:
         _peak_reset()
         if a.mode == "nt":
             x = torch.rand(1, T, D, device=dev, dtype=dt)
@@ -188,7 +193,9 @@ def main(argv=None):
             data.append(rec)
             json.dump(data, open(a.file, "w"), indent=1)
     comm.barrier()
-    C.destroy()
+    ctx.__exit__(None, None, None)
+    if not a.emulate:
+        C.destroy()
 
 
 if __name__ == "__main__":
