@@ -14,6 +14,7 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -62,6 +63,18 @@ int64_t avail_elems(const at::Tensor& t) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// XDOT_GEMM: 0 = auto (default), 1 = always the 128x128 v1 kernel, 2 = v2 whenever legal
+int gemm_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM");
+    if (!e) return 0;
+    if (e[0] == 'v' && e[1] == '1') return 1;
+    if (e[0] == 'v' && e[1] == '2') return 2;
+    return 0;
+  }();
+  return v;
+}
+
 void check_launch(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "xdot: ", what, " launch failed: ", hipGetErrorString(e));
 }
@@ -70,7 +83,7 @@ void check_launch(hipError_t e, const char* what) {
 void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N,
           int64_t K, int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb,
           int64_t ldc, int64_t sA1, int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1,
-          int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha) {
+          int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha, double beta) {
   Range rr_("xdot.gemm");
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "xdot.gemm: tensors must be on GPU");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "xdot.gemm: A/B dtype mismatch");
@@ -104,8 +117,33 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   g.M = (int)M; g.N = (int)N; g.K = (int)K; g.nseg = (int)nseg; g.nb2 = (int)nb2;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.sA1 = sA1; g.sA2 = sA2; g.sB1 = sB1; g.sB2 = sB2; g.sC1 = sC1; g.sC2 = sC2;
-  g.sAseg = sAseg; g.sBseg = sBseg; g.alpha = (float)alpha;
+  g.sAseg = sAseg; g.sBseg = sBseg; g.alpha = (float)alpha; g.beta = (float)beta;
   c10::DeviceGuard guard(A.device());
+  // v2 (256x256 tiles, LDS-DMA, csrc/gemm2.hip) for 16-bit operands whose layout meets its
+  // alignment rules and whose output fills 256-wide tiles; split-K when the tiles alone would
+  // leave CUs idle.  XDOT_GEMM=v1|v2 forces a path (v2 still needs the layout rules).
+  const int mode = gemm_mode();
+  const bool half = A.element_size() == 2;
+  bool v2 = half && vec && mode != 1;
+  if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;
+  if (v2 && a_mc) v2 = M % 8 == 0;
+  if (v2 && b_mc) v2 = N % 8 == 0;
+  if (v2 && mode != 2) v2 = M >= 192 && N >= 192;
+  if (v2 && K > 0) {
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb1 * nb2;
+    const int64_t ktiles = nseg * ((K + 31) / 32);
+    int64_t S = 1;
+    if (tiles < 512) S = std::min<int64_t>({(512 + tiles - 1) / tiles, ktiles / 8, 16});
+    S = std::max<int64_t>(S, 1);
+    at::Tensor ws;
+    if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
+    const int rc2 = xdot_gemm2_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
+                                      a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
+    if (rc2 == 0) {
+      check_launch(hipGetLastError(), "gemm2");
+      return;
+    }
+  }
   const int rc = xdot_gemm_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()),
                                   dt_code(C.scalar_type()), a_mc, b_mc, vec, cur_stream(A));
   TORCH_CHECK(rc == 0, "xdot.gemm: unsupported dtype combination ", A.scalar_type(), " -> ", C.scalar_type());
@@ -533,7 +571,7 @@ at::Tensor flash_bwd_rows_sum(const at::Tensor& dpart, int64_t H, const at::Tens
 TORCH_LIBRARY(xdot, m) {
   m.def("gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int nseg, int nb1, int nb2, "
         "int lda, int ldb, int ldc, int sA1, int sA2, int sB1, int sB2, int sC1, int sC2, "
-        "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha) -> ()");
+        "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha, float beta=0.0) -> ()");
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");

@@ -261,13 +261,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int v = 0; v < 16 / EO; ++v) {
           union { u32x4 u; TO e[EO]; } o;
+          if (p.beta != 0.f) {
+            o.u = *reinterpret_cast<const u32x4*>(dst + v * EO);
 #pragma unroll
-          for (int e = 0; e < EO; ++e) o.e[e] = (TO)src[v * EO + e];
+            for (int e = 0; e < EO; ++e) o.e[e] = (TO)(src[v * EO + e] + p.beta * (float)o.e[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < EO; ++e) o.e[e] = (TO)src[v * EO + e];
+          }
           *reinterpret_cast<u32x4*>(dst + v * EO) = o.u;
         }
       } else {
         for (int e = 0; e < 16; ++e)
-          if (gn + e < p.N) dst[e] = (TO)src[e];
+          if (gn + e < p.N) dst[e] = (TO)(p.beta != 0.f ? src[e] + p.beta * (float)dst[e] : src[e]);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);

@@ -20,6 +20,7 @@ struct GemmArgs {
   int64_t sA1, sA2, sB1, sB2, sC1, sC2;  // batch strides (elements)
   int64_t sAseg, sBseg;                  // segment strides (elements)
   float alpha;
+  float beta;      // C = alpha * A.B + beta * C (beta = 0: C is not read)
 };
 
 namespace smx {
@@ -99,6 +100,9 @@ struct AdamArgs {
 extern "C" {
 int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc,
                      int b_mc, int vec, hipStream_t st);
+// 256x256 LDS-DMA 16-bit GEMM (csrc/gemm2.hip); splits > 1 needs ws: splits*batches*M*N fp32
+int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
+                      int splits, float* ws, hipStream_t st);
 int xdot_softmax_fwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 int xdot_softmax_bwd_launch(const xdot::smx::Args* a, int dt, int vec, hipStream_t st);
 // bool mask (B, R, T) -> row-major bits (B, R, NKT), column-major bits (B, ceil(R/64),

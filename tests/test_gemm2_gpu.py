@@ -1,0 +1,71 @@
+"""Numerics of the 256x256 LDS-DMA GEMM (csrc/gemm2.hip) against fp32 PyTorch (GPU only).
+
+Shapes are chosen so xdot.gemm's dispatcher takes the v2 path (16-bit operands, M, N >= 192,
+aligned layouts): every operand layout, M/N/K tails, K segments, split-K, alpha/beta.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HALF = [torch.bfloat16, torch.float16]
+
+
+def _tol(dt, k):
+    return (2e-2 if dt == torch.bfloat16 else 4e-3) * math.sqrt(max(k, 1) / 64)
+
+
+def _run(gpu, dt, a_mc, b_mc, M, N, K, nseg=1, batches=2, alpha=1.0, beta=0.0, out_dt=torch.float32, seed=0):
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(seed + M * 7 + N + K)
+    A = torch.randn(batches, nseg, *((K, M) if a_mc else (M, K)), generator=g).to(gpu, dt)
+    B = torch.randn(batches, nseg, *((K, N) if b_mc else (N, K)), generator=g).to(gpu, dt)
+    C0 = torch.randn(batches, M, N, generator=g).to(gpu, out_dt)
+    C = C0.clone()
+    strided_gemm(A, B, C, M=M, N=N, K=K, nseg=nseg, nb2=batches, lda=(M if a_mc else K),
+                 ldb=(N if b_mc else K), ldc=N, sA2=nseg * M * K, sB2=nseg * N * K, sC2=M * N,
+                 sAseg=M * K, sBseg=N * K, a_mc=a_mc, b_mc=b_mc, alpha=alpha, beta=beta)
+    Af, Bf = A.float(), B.float()
+    opA = Af.transpose(-1, -2) if a_mc else Af        # (b, s, M, K)
+    opB = Bf if b_mc else Bf.transpose(-1, -2)        # (b, s, K, N)
+    ref = alpha * torch.matmul(opA, opB).sum(1) + beta * C0.float()
+    err = (C.float() - ref).abs().max().item()
+    tol = _tol(dt, K * nseg) * max(1.0, ref.abs().max().item() / 4)
+    if out_dt != torch.float32:
+        tol += ref.abs().max().item() * (2 ** -7 if out_dt == torch.bfloat16 else 2 ** -10)
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("dt", HALF)
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 32), (520, 264, 96), (776, 1000, 40), (264, 520, 200)])
+def test_gemm2_layouts_tails(gpu, dt, a_mc, b_mc, M, N, K):
+    _run(gpu, dt, a_mc, b_mc, M, N, K, alpha=0.5)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm2_segments_beta_bf16_out(gpu, a_mc, b_mc):
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 512, 264, 104, nseg=3, alpha=0.25, beta=1.0, out_dt=torch.bfloat16)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (True, True), (False, True)])
+@pytest.mark.parametrize("K", [4096, 4104])
+def test_gemm2_split_k(gpu, a_mc, b_mc, K):
+    """one 256x256 tile per batch and a long K: the dispatcher splits K (fp32 partials)"""
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 256, 256, K, batches=1, alpha=2.0, beta=0.5)
+
+
+def test_gemm2_nt_distributed_product(gpu):
+    """the nt product at a v2 size through the op-level helper (final (P, R, T) layout)"""
+    from xdot.ops.gemm import nt_chunk_into
+
+    N, Pn, R, D = 3, 2, 320, 96
+    left = torch.randn(Pn, R, D, device=gpu).bfloat16()
+    chunk = torch.randn(N, Pn, R, D, device=gpu).bfloat16()
+    out = torch.empty(Pn, R, N * R, device=gpu, dtype=torch.bfloat16)
+    nt_chunk_into(out, left, chunk, 0, alpha=0.125)
+    ref = 0.125 * torch.cat([left.float() @ chunk.float()[j].transpose(-1, -2) for j in range(N)], -1)
+    assert torch.allclose(out.float(), ref, atol=0.05, rtol=2e-2)
