@@ -14,8 +14,11 @@
 //     LDS fragment reads drop to 96 B/clk/CU at peak (37 % of the 256 B/clk array);
 //   * operands travel HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging, no
 //     ds_write), through a ring of BK = 64 tiles (64 KiB per stage, 2 stages: every
-//     k-contiguous row segment is one whole 128-byte line) or BK = 32 x 4 stages
-//     (XDOT_GEMM2_BK=32), one counted `s_waitcnt vmcnt` + barrier per tile;
+//     k-contiguous row segment is one whole 128-byte line; BK = 32 x 4 stages measured
+//     7-8 % slower), one `s_waitcnt vmcnt` + barrier per tile, the next tile's DMAs
+//     interleaved with the first two k-steps' MFMAs;
+//   * persistent grid (one workgroup per CU) walking (split, batch, tile) items: the ring
+//     continues across items, so each item's epilogue overlaps the next item's first DMAs;
 //   * k-contiguous images [256 rows][2 BK bytes], 16-byte chunks XOR-swizzled by row bits:
 //     ds_read_b128 fragment reads conflict-free; mn-contiguous images [BK k][512 B], chunks
 //     XOR-swizzled by 4 (k & 3): ds_read_b64_tr_b16 (hardware transpose) conflict-free.  The
@@ -114,6 +117,13 @@ __device__ __forceinline__ u32x4 frag_mc(const char* img, int lane_off, int base
   return c.u;
 }
 
+// wave-uniform pointer forced into SGPRs (the DMA's base operand must be scalar)
+template <typename T> __device__ __forceinline__ const T* sgpr_ptr(const T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+}
+
 template <int DT> __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
   if constexpr (DT == DT_BF16)
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -123,62 +133,128 @@ template <int DT> __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x1
 
 }  // namespace g2
 
-// ws != nullptr: split-K slice blockIdx.z writes fp32 partials ws[(z_split * batches + z) * M * N]
-template <int DTI, int DTO, bool A_MC, bool B_MC, class CF>
-__global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restrict__ ws) {
+// Persistent: gridDim.x workgroups (<= one per CU) walk the work items L = slot, slot + G, ...
+// (item = (split, batch, output tile)); the LDS-DMA ring runs straight across item
+// boundaries, so the next item's first k-tile streams in during this item's last k-tile and
+// epilogue.  ws != nullptr: split-K partials ws[((split * batches) + batch) * M * N + m * N + n].
+// ISS: where the next k-tile's 8 DMAs are issued -- 0: all before k-step 0's fragment reads,
+// 1: 4 after k-step 0's and 4 after k-step 1's fragment reads (before their MFMAs)
+// PST: persistent grid (epilogue strips beside the ring, overlapping the next item's DMAs);
+// !PST: one item per workgroup, the epilogue reuses the drained ring (128 KiB LDS)
+template <int DTI, int DTO, bool A_MC, bool B_MC, int ISS, bool PST>
+__global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restrict__ ws, int W, int batches, int nsplit) {
   using namespace g2;
+  using CF = Cfg<64, 2>;
   using fa::glds16;
   using fa::wait_vm;
   using fa::raw_barrier;
   using TI = typename dt_traits<DTI>::T;
   using TO = typename dt_traits<DTO>::T;
-  constexpr int BK = CF::BK, NBUF = CF::NBUF, PF = CF::PF, NG = CF::NG, IMG = CF::IMG, STAGE = CF::STAGE;
+  constexpr int BK = CF::BK, NG = CF::NG, IMG = CF::IMG, STAGE = CF::STAGE;
   constexpr int PPW = CF::PPW, KCH = CF::KCH, KS = BK / 16;
+  constexpr int EPI_OFF = PST ? 2 * STAGE : 0;  // 32 KiB of wave-private epilogue strips
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-
-  // tile order: XCD remap, then groups of 8 M-tiles swept N-major inside the group
-  const int ntile = p.tiles_m * p.tiles_n;
-  const int t_lin = xcd_remap(blockIdx.x, gridDim.x);
-  if (t_lin >= ntile) return;
-  constexpr int GM = 8;
-  const int gsz = GM * p.tiles_n;
-  const int g = t_lin / gsz, first_m = g * GM;
-  const int gm_n = min(GM, p.tiles_m - first_m);
-  const int tile_m = first_m + (t_lin % gsz) % gm_n, tile_n = (t_lin % gsz) / gm_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int z = blockIdx.y, z1 = z / p.nb2, z2 = z % p.nb2;
-
-  const TI* A = reinterpret_cast<const TI*>(p.A) + z1 * p.sA1 + z2 * p.sA2 + (A_MC ? (int64_t)m0 : (int64_t)m0 * p.lda);
-  const TI* B = reinterpret_cast<const TI*>(p.B) + z1 * p.sB1 + z2 * p.sB2 + (B_MC ? (int64_t)n0 : (int64_t)n0 * p.ldb);
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);  // XCD x runs a contiguous slot range
+  if (slot >= W) return;
 
   const int ktiles = (p.K + BK - 1) / BK;
   const int ntot = ktiles * p.nseg;
-  const int nsplit = gridDim.z;
-  const int tb = (int)((int64_t)blockIdx.z * ntot / nsplit), te = (int)((int64_t)(blockIdx.z + 1) * ntot / nsplit);
+  const int ntile = p.tiles_m * p.tiles_n;
+  constexpr int GM = 8;
+  const int gsz = GM * p.tiles_n;
 
+  struct Item {
+    int m0, n0, z, zs, tb, te;
+    const TI* A;  // batch + mn base
+    const TI* B;
+  };
+  auto item_of = [&](int L) {
+    Item it;
+    const int zz = L / ntile, tl = L % ntile;
+    it.zs = zz / batches;
+    it.z = zz % batches;
+    const int g = tl / gsz, first_m = g * GM;
+    const int gm_n = min(GM, p.tiles_m - first_m);
+    it.m0 = (first_m + (tl % gsz) % gm_n) * BM;
+    it.n0 = ((tl % gsz) / gm_n) * BN;
+    it.tb = (int)((int64_t)it.zs * ntot / nsplit);
+    it.te = (int)((int64_t)(it.zs + 1) * ntot / nsplit);
+    const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
+    it.te = __builtin_amdgcn_readfirstlane(it.te);
+    it.tb = __builtin_amdgcn_readfirstlane(it.tb);
+    it.A = reinterpret_cast<const TI*>(p.A) + z1 * p.sA1 + z2 * p.sA2 + (A_MC ? (int64_t)it.m0 : (int64_t)it.m0 * p.lda);
+    it.B = reinterpret_cast<const TI*>(p.B) + z1 * p.sB1 + z2 * p.sB2 + (B_MC ? (int64_t)it.n0 : (int64_t)it.n0 * p.ldb);
+    return it;
+  };
+
+  // ---- issue side: the k-tile whose DMAs go out next (item ii, flattened k index ik) ----
+  int iL = slot;
+  Item ii = item_of(iL);
   OpDma<CF, A_MC> da;
   OpDma<CF, B_MC> db;
-  da.init(wave, lane, p.lda, p.M - m0);
-  db.init(wave, lane, p.ldb, p.N - n0);
-
-  // DMA pieces [d0, d1) of tile t (piece d < PPW: A piece d, else B piece d - PPW)
-  auto issue_part = [&](int t, int d0, int d1) {
-    char* st = smem + ((t - tb) % NBUF) * STAGE;
-    const int seg = t / ktiles, k0 = (t % ktiles) * BK;
-    const TI* a = A + seg * p.sAseg + (A_MC ? (int64_t)k0 * p.lda : (int64_t)k0);
-    const TI* b = B + seg * p.sBseg + (B_MC ? (int64_t)k0 * p.ldb : (int64_t)k0);
-    const bool full = k0 + BK <= p.K;
-    const int kl = p.K - k0;
+  da.init(wave, lane, p.lda, p.M - ii.m0);
+  db.init(wave, lane, p.ldb, p.N - ii.n0);
+  int ik = ii.tb, iseg = ik / ktiles, ikt = ik % ktiles, istage = 0;
+  bool ivalid = true;
+  const TI* ia = ii.A + iseg * p.sAseg + (A_MC ? (int64_t)ikt * BK * p.lda : (int64_t)ikt * BK);
+  const TI* ib = ii.B + iseg * p.sBseg + (B_MC ? (int64_t)ikt * BK * p.ldb : (int64_t)ikt * BK);
+  auto reset_ptrs = [&]() {
+    ia = ii.A + iseg * p.sAseg + (A_MC ? (int64_t)ikt * BK * p.lda : (int64_t)ikt * BK);
+    ib = ii.B + iseg * p.sBseg + (B_MC ? (int64_t)ikt * BK * p.ldb : (int64_t)ikt * BK);
+  };
+  auto issue_part = [&](int d0, int d1) {
+    char* st = smem + istage * STAGE;
+    const TI* sa = sgpr_ptr(ia);
+    const TI* sb = sgpr_ptr(ib);
+    if ((ikt + 1) * BK <= p.K) {
 #pragma unroll
-    for (int d = 0; d < NG; ++d) {
-      if (d < d0 || d >= d1) continue;
-      if (d < PPW) glds16(a, full ? da.off[d] : da.tail_off(d, p.lda, kl), st + (wave * PPW + d) * 1024);
-      else glds16(b, full ? db.off[d - PPW] : db.tail_off(d - PPW, p.ldb, kl), st + IMG + (wave * PPW + d - PPW) * 1024);
+      for (int d = 0; d < NG; ++d) {
+        if (d < d0 || d >= d1) continue;
+        if (d < PPW) glds16(sa, da.off[d], st + (wave * PPW + d) * 1024);
+        else glds16(sb, db.off[d - PPW], st + IMG + (wave * PPW + d - PPW) * 1024);
+      }
+    } else {  // K-tail tile (once per segment at most)
+      const int kl = p.K - ikt * BK;
+#pragma unroll
+      for (int d = 0; d < NG; ++d) {
+        if (d < d0 || d >= d1) continue;
+        if (d < PPW) glds16(sa, da.tail_off(d, p.lda, kl), st + (wave * PPW + d) * 1024);
+        else glds16(sb, db.tail_off(d - PPW, p.ldb, kl), st + IMG + (wave * PPW + d - PPW) * 1024);
+      }
     }
+  };
+  auto advance_issue = [&]() {
+    istage ^= 1;
+    ik = __builtin_amdgcn_readfirstlane(ik + 1);
+    if (ik < ii.te) {
+      ikt = __builtin_amdgcn_readfirstlane(ikt + 1);
+      if (ikt == ktiles) {
+        ikt = 0;
+        ++iseg;
+        reset_ptrs();
+      } else {
+        ia += A_MC ? (int64_t)BK * p.lda : (int64_t)BK;
+        ib += B_MC ? (int64_t)BK * p.ldb : (int64_t)BK;
+      }
+      return;
+    }
+    iL += G;
+    if (iL >= W) {
+      ivalid = false;
+      return;
+    }
+    ii = item_of(iL);
+    da.init(wave, lane, p.lda, p.M - ii.m0);
+    db.init(wave, lane, p.ldb, p.N - ii.n0);
+    ik = __builtin_amdgcn_readfirstlane(ii.tb);
+    iseg = __builtin_amdgcn_readfirstlane(ik / ktiles);
+    ikt = __builtin_amdgcn_readfirstlane(ik % ktiles);
+    reset_ptrs();
   };
 
   // zero the k >= K part of a tail tile's images (after its DMAs landed, before any read)
@@ -209,9 +285,9 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
   for (int ks = 0; ks < KS; ++ks) kc_off[ks] = l31 * (KCH * 16) + (((2 * ks + hf) ^ kc_swz<KCH>(l31)) << 4);
   int mc_off[4];
   {
-    const int G = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int Gq = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) mc_off[v] = (8 * (G >> 1) + q) * 512 + 64 * (v ^ q) + 32 * (G & 1) + 8 * pp;
+    for (int v = 0; v < 4; ++v) mc_off[v] = (8 * (Gq >> 1) + q) * 512 + 64 * (v ^ q) + 32 * (Gq & 1) + 8 * pp;
   }
 
   f32x16 acc[4][2];
@@ -222,34 +298,85 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nt = te - tb;
+  // ---- epilogue of one item: 8 passes of a 16 x 64 fp32 strip through the wave's LDS strip
+  // (64-float rows, 16-byte chunks XOR-swizzled by row & 3: conflict-free both ways) ----
+  float* ep = reinterpret_cast<float*>(smem + EPI_OFF) + wave * 16 * 64;
+  auto epilogue = [&](const Item& it) {
+    const int rrow = lane >> 2, rq = lane & 3;
+    const int gn = it.n0 + wn * 64 + rq * 16;
+    const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
 #pragma unroll
-  for (int t = 0; t < PF; ++t)
-    if (t < nt) issue_part(tb + t, 0, NG);
-  // tile tb landed: tiles tb+1 .. tb+min(nt,PF)-1 may stay in flight
-  if constexpr (PF >= 3) {
-    if (nt >= PF) wait_vm<NG * (PF - 1)>();
-    else if (nt == 2) wait_vm<NG>();
-    else wait_vm<0>();
-  } else if constexpr (PF == 2) {
-    if (nt >= 2) wait_vm<NG>();
-    else wait_vm<0>();
-  } else {
-    wait_vm<0>();
-  }
-  raw_barrier();
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 8 * h; r < 8 * h + 8; ++r) {
+            const int row = (r & 3) + 8 * ((r >> 2) - 2 * h) + 4 * hf;
+            const int col = 32 * j + l31;
+            ep[row * 64 + ((((col >> 2) ^ (row & 3))) << 2) + (col & 3)] = acc[i][j][r];
+          }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private strip
+        __builtin_amdgcn_wave_barrier();
+        f32x4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const f32x4*>(ep + rrow * 64 + (((4 * rq + c) ^ (rrow & 3)) << 2));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int gm = it.m0 + wm * 128 + 32 * i + 16 * h + rrow;
+        if (gm >= p.M) continue;
+        if (ws) {
+          float* dst = ws + ((int64_t)it.zs * batches + it.z) * (int64_t)p.M * p.N + (int64_t)gm * p.N + gn;
+          if (gn + 16 <= p.N && (p.N & 3) == 0) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) *reinterpret_cast<f32x4*>(dst + 4 * c) = v[c];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              if (gn + e < p.N) dst[e] = v[e >> 2][e & 3];
+          }
+        } else {
+          TO* dst = reinterpret_cast<TO*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)gm * p.ldc + gn;
+          constexpr int EO = 16 / sizeof(TO);
+          if (gn + 16 <= p.N && (p.ldc % EO) == 0) {
+#pragma unroll
+            for (int c = 0; c < 16 / EO; ++c) {
+              union { u32x4 u; TO e[EO]; } o;
+              if (p.beta != 0.f) o.u = *reinterpret_cast<const u32x4*>(dst + c * EO);
+#pragma unroll
+              for (int e = 0; e < EO; ++e) {
+                const float x = v[(c * EO + e) >> 2][(c * EO + e) & 3] * p.alpha;
+                o.e[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)o.e[e] : x);
+              }
+              *reinterpret_cast<u32x4*>(dst + c * EO) = o.u;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              if (gn + e < p.N) {
+                const float x = v[e >> 2][e & 3] * p.alpha;
+                dst[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)dst[e] : x);
+              }
+          }
+        }
+      }
+    }
+  };
 
-  // the next tile's DMAs are spread over the first KSI k-steps, after each step's fragment
-  // reads and before its MFMAs (a DMA issue costs ~60 cycles: in a burst it starves the MFMA
-  // pipe; interleaved, the other wave of the SIMD issues MFMAs meanwhile)
-  constexpr int KSI = (NBUF == 2) ? (KS > 1 ? KS / 2 : 1) : KS;
-  constexpr int DPK = NG / KSI;
-  static_assert(DPK * KSI == NG, "dma split");
-  for (int t = tb; t < te; ++t) {
-    char* st = smem + ((t - tb) % NBUF) * STAGE;
-    const bool pre = t + PF < te;
+  // ---- main loop over this workgroup's k-tiles, item after item ----
+  int cL = slot;
+  Item ci = ii;
+  int ck = ci.tb, ckt = ck % ktiles, cstage = 0;
+  issue_part(0, NG);
+  advance_issue();
+  wait_vm<0>();
+  raw_barrier();
+  while (true) {
+    char* st = smem + cstage * STAGE;
+    const bool pre = ivalid;
     {
-      const int kl = p.K - (t % ktiles) * BK;
+      const int kl = p.K - ckt * BK;
       if (kl < BK) {  // uniform across the workgroup
         patch_tail(st, kl);
         __syncthreads();
@@ -257,6 +384,9 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
     }
     const char* sa = st;
     const char* sb = st + IMG;
+    if (ISS == 0 && pre) issue_part(0, NG);
+    // ISS 1: the next k-tile's DMAs go out after k-steps 0 and 1's fragment reads, before
+    // their MFMAs (a DMA issue costs ~60 cycles; interleaved, the SIMD's other wave issues MFMAs)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       u32x4 fa[4], fb[2];
@@ -270,7 +400,7 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
         const int nb = wn * 64 + 32 * j;
         fb[j] = B_MC ? g2::frag_mc(sb, mc_off[(nb >> 5) & 3], nb, ks) : g2::frag_kc<KCH>(sb, kc_off[ks], nb);
       }
-      if (ks < KSI && pre) issue_part(t + PF, ks * DPK, (ks + 1) * DPK);
+      if (ISS == 1 && ks < 2 && pre) issue_part(ks * (NG / 2), (ks + 1) * (NG / 2));
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -278,67 +408,34 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
         for (int j = 0; j < 2; ++j) acc[i][j] = g2::mfma<DTI>(fa[i], fb[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
-    if (pre) wait_vm<NG * (PF - 1)>();
-    else wait_vm<0>();
-    raw_barrier();
-  }
-
-  // ---- epilogue: per wave, 4 passes of a 32 x 64 strip through LDS (fp32), 16-byte stores ----
-  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * EPI_ROWF;
-  const int rrow = lane >> 1, rcol = (lane & 1) * 32;
-  const int gn = n0 + wn * 64 + rcol;
+    if (pre) advance_issue();
+    ck = __builtin_amdgcn_readfirstlane(ck + 1);
+    const bool last = ck == ci.te;
+    if (PST && last) {  // epilogue while the next item's first k-tile is in flight
+      epilogue(ci);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        ep[((r & 3) + 8 * (r >> 2) + 4 * hf) * EPI_ROWF + 32 * j + l31] = acc[i][j][r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private strip
-    __builtin_amdgcn_wave_barrier();
-    f32x4 v[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = *reinterpret_cast<const f32x4*>(ep + rrow * EPI_ROWF + rcol + 4 * c);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    const int gm = m0 + wm * 128 + 32 * i + rrow;
-    if (gm < p.M) {
-      if (ws) {  // split-K partial: dense fp32 (M, N) slab per (slice, batch)
-        float* dst = ws + ((int64_t)blockIdx.z * gridDim.y + z) * (int64_t)p.M * p.N + (int64_t)gm * p.N + gn;
-        if (gn + 32 <= p.N && (p.N & 3) == 0) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) *reinterpret_cast<f32x4*>(dst + 4 * c) = v[c];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 32; ++e)
-            if (gn + e < p.N) dst[e] = v[e >> 2][e & 3];
-        }
-      } else {
-        TO* dst = reinterpret_cast<TO*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)gm * p.ldc + gn;
-        constexpr int EO = 16 / sizeof(TO);
-        const bool vec = gn + 32 <= p.N && (p.ldc % EO) == 0;
-        if (vec) {
-#pragma unroll
-          for (int c = 0; c < 32 / EO; ++c) {
-            union { u32x4 u; TO e[EO]; } o;
-            if (p.beta != 0.f) o.u = *reinterpret_cast<const u32x4*>(dst + c * EO);
-#pragma unroll
-            for (int e = 0; e < EO; ++e) {
-              const float x = v[(c * EO + e) >> 2][(c * EO + e) & 3] * p.alpha;
-              o.e[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)o.e[e] : x);
-            }
-            *reinterpret_cast<u32x4*>(dst + c * EO) = o.u;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 32; ++e)
-            if (gn + e < p.N) {
-              const float x = v[e >> 2][e & 3] * p.alpha;
-              dst[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)dst[e] : x);
-            }
-        }
-      }
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     }
+    wait_vm<0>();
+    raw_barrier();
+    if (!PST && last) {
+      epilogue(ci);
+      break;
+    }
+    if (last) {
+      cL += G;
+      if (cL >= W) break;
+      ci = item_of(cL);
+      ck = ci.tb;
+      ckt = ck % ktiles;
+    } else if (++ckt == ktiles) {
+      ckt = 0;
+    }
+    cstage ^= 1;
   }
 }
 
@@ -359,25 +456,53 @@ __global__ __launch_bounds__(256) void gemm2_reduce(GemmArgs p, const float* __r
   *c = (TO)(p.beta != 0.f ? x + p.beta * (float)*c : x);
 }
 
-// ring configuration: XDOT_GEMM2_BK=32 -> BK 32 x 4 stages; default BK 64 x 2 stages
-inline int gemm2_bk() {
+inline int num_cus() {
   static const int v = [] {
-    const char* e = std::getenv("XDOT_GEMM2_BK");
-    return (e && e[0] == '3') ? 32 : 64;
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return v;
+}
+
+inline int gemm2_iss() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM2_ISS");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+// XDOT_GEMM2_PERSIST_KT: largest k-tile count per item that still runs persistent (default 32)
+inline int gemm2_persist_kt() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM2_PERSIST_KT");
+    return e ? std::atoi(e) : 32;
   }();
   return v;
 }
 
 template <int DTI, int DTO, bool AMC, bool BMC>
 static void launch2_t(const GemmArgs& a, int batches, int splits, float* ws, hipStream_t st) {
-  dim3 grid(a.tiles_m * a.tiles_n, batches, splits);
-  if (gemm2_bk() == 32) {
-    using CF = g2::Cfg<32, 4>;
-    hipLaunchKernelGGL((gemm2_kernel<DTI, DTO, AMC, BMC, CF>), grid, dim3(g2::NT), CF::LDS, st, a, splits > 1 ? ws : nullptr);
+  const int W = a.tiles_m * a.tiles_n * batches * splits;
+  // persistent (one workgroup per CU) when items are short (the per-item prologue/epilogue is
+  // then a large share that the ring overlaps); one workgroup per item for long K
+  const int kt_item = ((a.K + 63) / 64) * a.nseg / splits;
+  const int G = (W > num_cus() && kt_item <= gemm2_persist_kt()) ? num_cus() : W;
+  constexpr int LDS = g2::Cfg<64, 2>::LDS + 32768;  // ring + epilogue strips = 160 KiB
+  const bool pst = G < W;
+#define XDOT_G2L(ISS, PST, LDSB)                                                                                   \
+  hipLaunchKernelGGL((gemm2_kernel<DTI, DTO, AMC, BMC, ISS, PST>), dim3(G), dim3(g2::NT), LDSB, st, a,          \
+                     splits > 1 ? ws : nullptr, W, batches, splits)
+  if (gemm2_iss() == 1) {
+    if (pst) XDOT_G2L(1, true, LDS);
+    else XDOT_G2L(1, false, LDS - 32768);
   } else {
-    using CF = g2::Cfg<64, 2>;
-    hipLaunchKernelGGL((gemm2_kernel<DTI, DTO, AMC, BMC, CF>), grid, dim3(g2::NT), CF::LDS, st, a, splits > 1 ? ws : nullptr);
+    if (pst) XDOT_G2L(0, true, LDS);
+    else XDOT_G2L(0, false, LDS - 32768);
   }
+#undef XDOT_G2L
   if (splits > 1) {
     const int64_t n = (int64_t)a.M * a.N * batches;
     hipLaunchKernelGGL((gemm2_reduce<DTO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches);

@@ -69,3 +69,15 @@ def test_gemm2_nt_distributed_product(gpu):
     nt_chunk_into(out, left, chunk, 0, alpha=0.125)
     ref = 0.125 * torch.cat([left.float() @ chunk.float()[j].transpose(-1, -2) for j in range(N)], -1)
     assert torch.allclose(out.float(), ref, atol=0.05, rtol=2e-2)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (True, True), (False, True), (True, False)])
+def test_gemm2_persistent_many_items(gpu, a_mc, b_mc):
+    """more work items than CUs: each persistent workgroup crosses item boundaries (edge tiles,
+    K tails, segments) with the DMA ring running on"""
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 1288, 1800, 200, nseg=2, batches=5, alpha=0.5, beta=0.25,
+         out_dt=torch.bfloat16)
+
+
+def test_gemm2_split_k_many_items(gpu):
+    _run(gpu, torch.float16, False, True, 264, 512, 6000, batches=6, alpha=1.0)
