@@ -226,21 +226,21 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
 // exactly NG DMAs (its share of the two images + one 256 B/1 KiB row-constant piece), so a
 // counted `s_waitcnt vmcnt(NG)` retires tile rt+1 while tile rt+2 stays in flight across the
 // raw barrier (3-deep ring; 2-deep when three stages do not fit twice in 160 KiB).
-template <int D> struct ColsCfg {
+template <int D, int NB = 0> struct ColsCfg {
   static constexpr int IMG = Img<D>::BYTES;
   static constexpr int IPW = IMG / 4096;  // 1 KiB DMA pieces per wave per image
   static constexpr int OFF_L = 2 * IMG, OFF_D = OFF_L + 256, OFF_W = OFF_D + 256, OFF_X = OFF_W + 1024;
   static constexpr int OFF_F = OFF_X + 256;  // tile flags of the two 32-row halves (glds_flags)
   static constexpr int STAGE = OFF_F + 256;
-  static constexpr int NBUF = (2 * 3 * STAGE <= 160 * 1024) ? 3 : 2;
+  static constexpr int NBUF = NB ? NB : ((2 * 3 * STAGE <= 160 * 1024) ? 3 : 2);
   static constexpr int PF = NBUF - 1;     // tiles in flight ahead of the one being computed
   static constexpr int NG = 2 * IPW + 2;  // DMAs per wave per tile
 };
 
-template <int DT, int D, int WPS = 2>
+template <int DT, int D, int WPS = 2, int NB = 0>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
-  using CF = ColsCfg<D>;
+  using CF = ColsCfg<D, NB>;
   constexpr int ROW = Img<D>::ROW, IMG = CF::IMG, IPW = CF::IPW, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
   constexpr int KS = D / 16, DB = D / 32;
 
@@ -452,11 +452,26 @@ static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hi
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
 }
 
+// Ring depth of the column kernel: 2 stages (default) keeps it under the 256-register budget
+// of 2 waves/SIMD at D = 96 (the 3-stage ring spilled 9 VGPRs to scratch inside the tile
+// loop, and every scratch reload's vmcnt drained the DMA prefetch): 4.36 vs 4.62 ms at
+// T = R = 25000, 0.60 vs 0.64 ms at R = 3125 on MI355X.  XDOT_COLS_NBUF=3 restores 3 stages.
+inline int cols_nbuf() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_COLS_NBUF");
+    return (e && e[0] == '3') ? 3 : 2;
+  }();
+  return v;
+}
+
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
   constexpr int LDS = ColsCfg<D>::NBUF * ColsCfg<D>::STAGE;
+  constexpr int LDS2 = 2 * ColsCfg<D, 2>::STAGE;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
+  else if (cols_nbuf() == 2)
+    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS2, st, a);
   else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
 }
 
