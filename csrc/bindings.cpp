@@ -83,7 +83,8 @@ void check_launch(hipError_t e, const char* what) {
 void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N,
           int64_t K, int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb,
           int64_t ldc, int64_t sA1, int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1,
-          int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha, double beta) {
+          int64_t sC2, int64_t sAseg, int64_t sBseg, bool a_mc, bool b_mc, double alpha, double beta,
+          int64_t path) {
   Range rr_("xdot.gemm");
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "xdot.gemm: tensors must be on GPU");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "xdot.gemm: A/B dtype mismatch");
@@ -122,13 +123,20 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   // v2 (256x256 tiles, LDS-DMA, csrc/gemm2.hip) for 16-bit operands whose layout meets its
   // alignment rules and whose output fills 256-wide tiles; split-K when the tiles alone would
   // leave CUs idle.  XDOT_GEMM=v1|v2 forces a path (v2 still needs the layout rules).
-  const int mode = gemm_mode();
+  // path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call; XDOT_GEMM overrides auto)
+  const int mode = path ? (int)path : gemm_mode();
   const bool half = A.element_size() == 2;
   bool v2 = half && vec && mode != 1;
   if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;
   if (v2 && a_mc) v2 = M % 8 == 0;
   if (v2 && b_mc) v2 = N % 8 == 0;
-  if (v2 && mode != 2) v2 = M >= 192 && N >= 192;
+  if (v2 && mode != 2) {
+    // auto: outputs that fill 256-wide tiles, and enough of them (>= 32 per batch entry or
+    // >= 512 overall) -- small outputs batched over K slabs (the split-K weight gradients of
+    // xdot.ops.linear) keep the 128x128 kernel, which fills the GPU without a second split
+    const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
+    v2 = M >= 192 && N >= 192 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
+  }
   if (v2 && K > 0) {
     const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb1 * nb2;
     const int64_t ktiles = nseg * ((K + 31) / 32);
@@ -571,7 +579,7 @@ at::Tensor flash_bwd_rows_sum(const at::Tensor& dpart, int64_t H, const at::Tens
 TORCH_LIBRARY(xdot, m) {
   m.def("gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int nseg, int nb1, int nb2, "
         "int lda, int ldb, int ldc, int sA1, int sA2, int sB1, int sB2, int sC1, int sC2, "
-        "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha, float beta=0.0) -> ()");
+        "int sAseg, int sBseg, bool a_mc, bool b_mc, float alpha, float beta=0.0, int path=0) -> ()");
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");

@@ -1,7 +1,6 @@
 """Numerics of the 256x256 LDS-DMA GEMM (csrc/gemm2.hip) against fp32 PyTorch (GPU only).
 
-Shapes are chosen so xdot.gemm's dispatcher takes the v2 path (16-bit operands, M, N >= 192,
-aligned layouts): every operand layout, M/N/K tails, K segments, split-K, alpha/beta.
+Every call forces the v2 path (``path=2``; 16-bit operands, aligned layouts): every operand layout, M/N/K tails, K segments, split-K, alpha/beta.
 """
 import math
 
@@ -27,7 +26,7 @@ def _run(gpu, dt, a_mc, b_mc, M, N, K, nseg=1, batches=2, alpha=1.0, beta=0.0, o
     C = C0.clone()
     strided_gemm(A, B, C, M=M, N=N, K=K, nseg=nseg, nb2=batches, lda=(M if a_mc else K),
                  ldb=(N if b_mc else K), ldc=N, sA2=nseg * M * K, sB2=nseg * N * K, sC2=M * N,
-                 sAseg=M * K, sBseg=N * K, a_mc=a_mc, b_mc=b_mc, alpha=alpha, beta=beta)
+                 sAseg=M * K, sBseg=N * K, a_mc=a_mc, b_mc=b_mc, alpha=alpha, beta=beta, path=2)
     Af, Bf = A.float(), B.float()
     opA = Af.transpose(-1, -2) if a_mc else Af        # (b, s, M, K)
     opB = Bf if b_mc else Bf.transpose(-1, -2)        # (b, s, K, N)
@@ -59,7 +58,7 @@ def test_gemm2_split_k(gpu, a_mc, b_mc, K):
 
 
 def test_gemm2_nt_distributed_product(gpu):
-    """the nt product at a v2 size through the op-level helper (final (P, R, T) layout)"""
+    """the nt product through the op-level helper (final (P, R, T) layout, automatic kernel choice)"""
     from xdot.ops.gemm import nt_chunk_into
 
     N, Pn, R, D = 3, 2, 320, 96

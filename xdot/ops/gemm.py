@@ -22,13 +22,16 @@ def hip_dtype_ok(*ts: torch.Tensor) -> bool:
 
 def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0, sA2=0,
                  sB1=0, sB2=0, sC1=0, sC2=0, sAseg=0, sBseg=0, a_mc=False, b_mc=False,
-                 alpha=1.0, beta=0.0) -> None:
+                 alpha=1.0, beta=0.0, path=0) -> None:
     """C[z1, z2](m, n) = alpha * sum_s sum_k opA(m, k) * opB(k, n) + beta * C[z1, z2](m, n)
-    (csrc/gemm.hip; 16-bit operands with large outputs run the 256x256 csrc/gemm2.hip)."""
+    (csrc/gemm.hip; 16-bit operands with large outputs run the 256x256 csrc/gemm2.hip).
+
+    ``path``: 0 = automatic kernel choice, 1 = the 128x128 kernel, 2 = the 256x256 kernel
+    whenever its layout rules hold."""
     _ext.ops().gemm(A, B, C, int(M), int(N), int(K), int(nseg), int(nb1), int(nb2), int(lda),
                     int(ldb), int(ldc), int(sA1), int(sA2), int(sB1), int(sB2), int(sC1), int(sC2),
                     int(sAseg), int(sBseg), bool(a_mc), bool(b_mc), float(alpha),
-                    float(beta))
+                    float(beta), int(path))
 
 
 def _flat(t: torch.Tensor, lead: int) -> torch.Tensor:
