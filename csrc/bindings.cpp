@@ -213,7 +213,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> mask_pack(const at::Tensor& mask)
   auto m = mask.contiguous();
   const int64_t B = m.size(0), R = m.size(1), T = m.size(2);
   const int64_t NKT = (T + 63) / 64, NRT = (R + 63) / 64, Tpad = (T + 127) / 128 * 128;
-  auto bits = at::empty({B, R, NKT}, m.options().dtype(at::kLong));
+  auto bits = at::empty({B, NKT, R}, m.options().dtype(at::kLong));
   auto flags = at::empty({B, (R + 31) / 32, (NKT + 3) & ~3}, m.options().dtype(at::kByte));
   auto bitsT = at::empty({B, NRT, Tpad}, m.options().dtype(at::kLong));
   TORCH_CHECK(B * R * NKT < (1LL << 40) && T < (1LL << 31), "xdot.mask_pack: too large");
@@ -231,7 +231,7 @@ struct FlashGeom {
 
 // rows: contiguous (B, R, C).  kc / vc: (B, T, C) views with unit inner stride and a common
 // row stride `ld` (C for separate tensors, 2C for the two halves of a packed [q | v]).
-// `bits`: the row-major (B, R, NKT) words, or with colmajor the (B, NRT, Tpad) words of the
+// `bits`: the kt-major (B, NKT, R) words, or with colmajor the (B, NRT, Tpad) words of the
 // backward column kernel (mask_pack's third output)
 FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc, int64_t H,
                       const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,

@@ -107,8 +107,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   dma.init(wave, lane, ldb);
   const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
-  const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
-  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
+  const uint64_t* mwg = a.mbits ? a.mbits + (int64_t)b * NKT * a.R + rb * 128 : nullptr;  // + kt * R per tile
+  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * 8 + (wave >> 1) * 4);
   const int NKT4 = (NKT + 3) & ~3;
   const int NRB32 = (a.R + 31) / 32;
   const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
     dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
     if (mwg) {
-      glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      glds4(mwg + (int64_t)kt * a.R, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
       glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
     } else {  // keeps NG DMAs per wave per tile
       glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);

@@ -75,8 +75,8 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   dma.init(wave, lane, ldb);
   const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
-  const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 128) * NKT : nullptr;
-  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * NKT * 8 + (wave >> 1) * 4);
+  const uint64_t* mwg = a.mbits ? a.mbits + (int64_t)b * NKT * a.R + rb * 128 : nullptr;  // + kt * R per tile
+  const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * 8 + (wave >> 1) * 4);
   // two rings over the same 3 stages: Q(t) + mask words(t) and V(t) go to stage (t - kt_beg) % 3,
   // but Q/mask are DMA'd one tile earlier than V (Q(kt+1) is read in iteration kt)
   constexpr int NQ = ImgDma<D>::IPW + 2, NV = ImgDma<D>::IPW;  // DMAs per wave
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     const int64_t t0 = (int64_t)kt * 64;
     dma.issue(kcb + t0 * ldb, ldb, a.T - 1 - (int)t0, st, wave);  // columns past T re-read T-1 (masked)
     if (mwg) {
-      glds4(mwg + kt, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      glds4(mwg + (int64_t)kt * a.R, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
       glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
     } else {  // same DMA count with or without a mask
       glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
@@ -357,11 +357,11 @@ __global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
   const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
   const int NKT4 = (NKT + 3) & ~3;
   const int NRB32 = (a.R + 31) / 32;
-  const uint64_t* mwg = a.mbits ? a.mbits + ((int64_t)b * a.R + rb * 256) * NKT : nullptr;
+  const uint64_t* mwg = a.mbits ? a.mbits + (int64_t)b * NKT * a.R + rb * 256 : nullptr;  // + kt * R per tile
   const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 8) * NKT4 : nullptr;
   const int nfr = min(8, NRB32 - rb * 8);
   // words: [dword][256 rows]; wave w moves rows 64w + lane, both dwords (2 DMAs)
-  const uint32_t moff = (uint32_t)(min(wave * 64 + lane, a.R - 1 - rb * 256) * NKT * 8);
+  const uint32_t moff = (uint32_t)(min(wave * 64 + lane, a.R - 1 - rb * 256) * 8);
   auto issue = [&](int kt) {
     char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
     const int64_t t0 = (int64_t)kt * 64;
@@ -369,8 +369,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
     dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
     dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
     if (mwg) {
-      glds4(mwg + kt, moff, st + CF::OFF_W + wave * 256);
-      glds4(mwg + kt, moff + 4, st + CF::OFF_W + 1024 + wave * 256);
+      glds4(mwg + (int64_t)kt * a.R, moff, st + CF::OFF_W + wave * 256);
+      glds4(mwg + (int64_t)kt * a.R, moff + 4, st + CF::OFF_W + 1024 + wave * 256);
       glds_flags(fwg, NKT4, nfr, kt >> 2, st + CF::OFF_F);
     } else {  // same DMA count with or without a mask
       glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);

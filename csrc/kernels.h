@@ -42,7 +42,7 @@ struct FwdArgs {
   const void* vc;          // gathered value side (B, T, ldkv)
   void* out;               // (B, R, H*D)
   float* lse;              // (B, H, R) natural-log LSE
-  const uint64_t* mbits;   // (B, R, NKT) bit k = col kt*64+k masked, or null
+  const uint64_t* mbits;   // (B, NKT, R) bit k = col kt*64+k masked, or null
   const uint8_t* mflags;   // (B, ceil(R/32), NKT) 0 none / 1 all / 2 partial, or null
   int B, H, R, T;
   int64_t ldkv;            // element stride between gathered rows (H*D, or 2*H*D when packed [q|v])

@@ -114,12 +114,12 @@ def test_mask_pack_flags(gpu):
     mask[0, :, :64] = True
     mask[1, 3, 100] = True
     mk = flash.prepare_mask(mask, B, R, T)
-    assert mk.bits.shape == (B, R, 3) and mk.flags.shape == (B, 3, 4)
+    assert mk.bits.shape == (B, 3, R) and mk.flags.shape == (B, 3, 4)
     f = mk.flags.cpu()[..., :3]
     assert f[0, :, 0].tolist() == [1, 1, 1] and f[0, :, 1:].eq(0).all()
     assert f[1, 0, 1] == 2 and f[1, 1:, :].eq(0).all()
     bits = mk.bits.cpu().view(torch.int64)
-    assert bits[1, 3, 1].item() == (1 << (100 - 64))
+    assert bits[1, 1, 3].item() == (1 << (100 - 64))
 
 
 @pytest.mark.parametrize("shape", [(2, 70, 150), (1, 200, 1000), (1, 64, 128)])

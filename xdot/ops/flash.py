@@ -17,7 +17,7 @@ from .. import _ext
 
 
 class PackedMask:
-    """Boolean (B, R, T) mask compressed to per-row bit words ``bits`` (B, R, ceil(T/64)),
+    """Boolean (B, R, T) mask compressed to per-row bit words ``bits`` (B, ceil(T/64), R),
     the same bits column-major per 64-row tile ``bits_t`` (B, ceil(R/64), Tpad) for the
     backward column kernel, and per (32-row, 64-col) tile ``flags`` (0 none / 1 all / 2 some
     masked)."""
