@@ -138,11 +138,17 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     v2 = M >= 192 && N >= 192 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
   }
   if (v2 && K > 0) {
+    // split-K: fewest k-slices S minimising ceil(items / CUs) / S (idle CUs of the last round),
+    // each slice >= 4 k-tiles of 64, with a 3 % charge per slice for the fp32 partial round trip
     const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb1 * nb2;
-    const int64_t ktiles = nseg * ((K + 31) / 32);
+    const int64_t kt64 = nseg * ((K + 63) / 64);
+    const int64_t ncu = 256;
     int64_t S = 1;
-    if (tiles < 512) S = std::min<int64_t>({(512 + tiles - 1) / tiles, ktiles / 8, 16});
-    S = std::max<int64_t>(S, 1);
+    double best = 1e300;
+    for (int64_t s = 1; s <= 64 && (s == 1 || kt64 / s >= 4); ++s) {
+      const double cost = (double)((tiles * s + ncu - 1) / ncu) / (double)s * (1.0 + 0.03 * (s - 1));
+      if (cost < best * 0.98) { best = cost; S = s; }
+    }
     at::Tensor ws;
     if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
     const int rc2 = xdot_gemm2_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),

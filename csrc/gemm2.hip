@@ -483,6 +483,26 @@ inline int gemm2_persist_kt() {
   return v;
 }
 
+// 4 consecutive columns per thread (N % 4 == 0, ldc % 4 == 0, C 16-byte aligned)
+template <int DTO>
+__global__ __launch_bounds__(256) void gemm2_reduce4(GemmArgs p, const float* __restrict__ ws, int S, int batches) {
+  using TO = typename dt_traits<DTO>::T;
+  const int64_t MN = (int64_t)p.M * p.N, MN4 = MN / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= MN4 * batches) return;
+  const int z = (int)(idx / MN4);
+  const int64_t mn = (idx % MN4) * 4;
+  const int m = (int)(mn / p.N), n = (int)(mn % p.N);
+  f32x4 acc = *reinterpret_cast<const f32x4*>(ws + (int64_t)z * MN + mn);
+  for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(ws + ((int64_t)s * batches + z) * MN + mn);
+  TO* c = reinterpret_cast<TO*>(p.C) + (z / p.nb2) * p.sC1 + (z % p.nb2) * p.sC2 + (int64_t)m * p.ldc + n;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = acc[e] * p.alpha;
+    c[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)c[e] : x);
+  }
+}
+
 template <int DTI, int DTO, bool AMC, bool BMC>
 static void launch2_t(const GemmArgs& a, int batches, int splits, float* ws, hipStream_t st) {
   const int W = a.tiles_m * a.tiles_n * batches * splits;
@@ -505,7 +525,12 @@ static void launch2_t(const GemmArgs& a, int batches, int splits, float* ws, hip
 #undef XDOT_G2L
   if (splits > 1) {
     const int64_t n = (int64_t)a.M * a.N * batches;
-    hipLaunchKernelGGL((gemm2_reduce<DTO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches);
+    const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && a.sC1 % 4 == 0 && a.sC2 % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
+    if (v4)
+      hipLaunchKernelGGL((gemm2_reduce4<DTO>), dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches);
+    else
+      hipLaunchKernelGGL((gemm2_reduce<DTO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches);
   }
 }
 

@@ -4,9 +4,10 @@ The four projections of the module (reference: ``distributed_dot_product/module.
 applied at ``:43-45`` and ``:75``) are ordinary ``nn.Linear`` layers; their forward and the
 input gradient ``dX = dY·W`` are well served by hipBLASLt.  The weight gradient
 ``dW = dYᵀ·X`` is not: its reduction runs over the sequence (K = T/N rows: 25000 at N = 1)
-while the output is only 768 x 768 (36 MFMA tiles of 128²) — hipBLASLt runs it at
-≈170-330 TF/s with most CUs idle.  Here K is split into S slabs that fill the 256 CUs, each
-slab writes an fp32 partial (bf16 inputs, fp32 accumulation), and one reduction sums them in
+while the output is only 768 x 768 (9 tiles of 256²) — hipBLASLt runs it at ≈170-330 TF/s
+with most CUs idle.  Here K is split into slices that fill the 256 CUs (the 256x256 kernel of
+``csrc/gemm2.hip`` chooses the split; other shapes use S slabs of the 128x128 kernel), each
+slice writes an fp32 partial (bf16 inputs, fp32 accumulation), and one reduction sums them in
 fp32 before the cast to the parameter dtype.
 
 ``linear(x, weight, bias)`` is a drop-in for ``torch.nn.functional.linear``; parameters stay
@@ -48,6 +49,12 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
         return (dy.float().t() @ x.float()).to(out_dtype)
     dy = dy.contiguous()
     x = x.contiguous()
+    if M % 8 == 0 and N % 8 == 0 and min(M, N) >= 128:
+        # 256x256 LDS-DMA kernel: it picks the K split itself (fp32 slices, one vectorised
+        # in-order reduction that also casts to the parameter dtype)
+        out = torch.empty(M, N, dtype=out_dtype, device=dy.device)
+        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True, path=2)
+        return out
     S = _splits(M, N, K)
     slab = K // S
     part = torch.empty(S + (1 if K % S else 0), M, N, dtype=torch.float32, device=dy.device)
