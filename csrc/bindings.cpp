@@ -372,11 +372,14 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   a.dkc = dkv.data_ptr(); a.dvc = static_cast<char*>(dkv.data_ptr()) + g.C * dkv.element_size(); a.ldg = 2 * g.C;
   a.dkv16 = fp32_out ? 0 : 1;
   a.delta = delta.data_ptr<float>();
+  auto lse2 = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  a.lse2 = lse2.data_ptr<float>();
   c10::DeviceGuard guard(rows.device());
   const int dt = dt_code(rows.scalar_type());
-  if (!have_delta)
-    TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt, (int)g.D, cur_stream(rows)) == 0,
-                "xdot.flash_bwd_cols: config");
+  // prep: lse2 (+ δ unless given)
+  TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), have_delta ? nullptr : delta.data_ptr<float>(), dt,
+                                          (int)g.D, cur_stream(rows)) == 0,
+              "xdot.flash_bwd_cols: config");
   TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, dt, (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
   check_launch(hipGetLastError(), "flash_bwd_cols");
   return {dkv, delta};

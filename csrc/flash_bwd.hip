@@ -31,6 +31,7 @@ namespace fa {
 
 // ---------------------------------------------------------------------------------------
 // δ = rowsum(dO ⊙ O) per (b, h, row); one thread per (b, row, h)
+// (and lse2 = lse * log2 e when a.lse2 is set; delta == nullptr: lse2 only)
 template <int DT, int D>
 __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const void* out_, float* delta) {
   using T16 = typename dt_traits<DT>::T;
@@ -40,6 +41,9 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
   const int h = (int)(idx % a.H);
   const int64_t br = idx / a.H;
   const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int64_t li = ((int64_t)b * a.H + h) * a.R + row;
+  if (a.lse2) a.lse2[li] = a.lse[li] * LOG2E;
+  if (!delta) return;
   const int64_t off = br * (a.H * D) + h * D;
   const T16* o = reinterpret_cast<const T16*>(out_) + off;
   const T16* d = reinterpret_cast<const T16*>(a.dout) + off;
@@ -52,7 +56,7 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc += (float)x.e[e] * (float)y.e[e];
   }
-  delta[((int64_t)b * a.H + h) * a.R + row] = acc;
+  delta[li] = acc;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -275,6 +279,10 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     // before the first DMA instead of waiting vmcnt(0) (all DMAs in flight) inside the loop
 #pragma unroll
     for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(qf[s]), "+v"(vf[s]));
+    // -V: the dP accumulator then starts at δ and ends at δ - dP, so dS' = P ⊙ acc = -dS with
+    // no per-element subtraction; the sign comes back in the dq epilogue (scale -> -scale)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) vf[s] ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
   }
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   dma.init(wave, lane, C * 2);
   const char* rows_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.rows) + (int64_t)b * a.R * C + h * D);
   const char* dout_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.dout) + (int64_t)b * a.R * C + h * D);
-  const float* lse = a.lse + ((int64_t)b * a.H + h) * a.R;
+  const float* lse = a.lse2 + ((int64_t)b * a.H + h) * a.R;  // log2-domain LSE
   const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
   // column-major mask words (mask_pack's bits_t): one u64 per (64-row tile, column)
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
@@ -321,15 +329,14 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   // P and dS of one 32-row half tile in place (s <- P, dp <- dS); rows of register r:
   // tt*32 + (r&3) + 8*(r>>2) + 4*hf.  Rows past R carry lse = +inf (patched below), so the
   // unmasked path has no per-element test at all.
-  auto softmax_grad = [&](f32x16& s, f32x16& dp, const float* ls, const float* dls, const uint64_t* ws, int tt,
-                          bool masked) {
+  // (dp holds δ - dP on entry: see the -V fragments above; leaves -dS)
+  auto softmax_grad = [&](f32x16& s, f32x16& dp, const float* ls, const uint64_t* ws, int tt, bool masked) {
     // masked: this lane's column word over the tile's 64 rows, shifted to its row half
     const uint32_t hw = masked ? (uint32_t)(ws[wave * 32 + (lane & 31)] >> (tt * 32)) >> (4 * hf) : 0u;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int rbase = tt * 32 + 8 * g + 4 * hf;
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase) * LOG2E;
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + rbase);
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase);  // lse * log2 e
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
@@ -337,9 +344,20 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
         if (masked && ((hw >> (8 * g + e)) & 1u)) x = NEG_INF;
         const float p = fast_exp2(x);
         s[r] = p;
-        dp[r] = p * (dp[r] - d4[e]);
+        dp[r] = p * dp[r];
       }
     }
+  };
+  // dP accumulator seed: δ of the half tile's rows in the accumulator's row order
+  auto delta_seed = [&](const float* dls, int tt) {
+    f32x16 d;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + tt * 32 + 8 * g + 4 * hf);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[4 * g + e] = d4[e];
+    }
+    return d;
   };
 
   // one row tile from ring stage BUF (a compile-time constant: every LDS address is a lane
@@ -366,14 +384,14 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], f32x16{});
-        f32x16 dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, 0, L), vf[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, 0, L), vf[0], delta_seed(dls, tt));
 #pragma unroll
         for (int kk = 1; kk < KS; ++kk) {
           s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, kk, L), qf[kk], s);
           dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, kk, L), vf[kk], dp);
         }
-        if (flag == 2) softmax_grad(s, dp, ls, dls, ws, tt, true);
-        else softmax_grad(s, dp, ls, dls, ws, tt, false);
+        if (flag == 2) softmax_grad(s, dp, ls, ws, tt, true);
+        else softmax_grad(s, dp, ls, ws, tt, false);
         // one 16-row k-step at a time: only 2 packed operand fragments live
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
@@ -398,6 +416,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       if (rt + 2 < NRT) tile(std::integral_constant<int, 2>{}, rt + 2);
     }
   }
+  const float nscale = -a.scale;  // dq was accumulated from -dS
   if (col_ok && a.dkv16) {  // input dtype: half the store (and reduce-scatter) bytes
     const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
     T16* pq = reinterpret_cast<T16*>(a.dkc) + off;
@@ -407,8 +426,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         u32x2 q2, v2;
-        q2[0] = pack2<DT>(dq[db][4 * g] * a.scale, dq[db][4 * g + 1] * a.scale);
-        q2[1] = pack2<DT>(dq[db][4 * g + 2] * a.scale, dq[db][4 * g + 3] * a.scale);
+        q2[0] = pack2<DT>(dq[db][4 * g] * nscale, dq[db][4 * g + 1] * nscale);
+        q2[1] = pack2<DT>(dq[db][4 * g + 2] * nscale, dq[db][4 * g + 3] * nscale);
         v2[0] = pack2<DT>(dv[db][4 * g], dv[db][4 * g + 1]);
         v2[1] = pack2<DT>(dv[db][4 * g + 2], dv[db][4 * g + 3]);
         *reinterpret_cast<u32x2*>(pq + db * 32 + 8 * g + 4 * hf) = q2;
@@ -422,7 +441,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        f32x4 q4 = {dq[db][4 * g] * a.scale, dq[db][4 * g + 1] * a.scale, dq[db][4 * g + 2] * a.scale, dq[db][4 * g + 3] * a.scale};
+        f32x4 q4 = {dq[db][4 * g] * nscale, dq[db][4 * g + 1] * nscale, dq[db][4 * g + 2] * nscale, dq[db][4 * g + 3] * nscale};
         f32x4 v4 = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
         *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) = q4;
         *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) = v4;

@@ -61,6 +61,7 @@ struct BwdArgs {
   const void* dout;        // (B, R, H*D)   upstream grad of out
   const float* lse;        // (B, H, R)
   const float* delta;      // (B, H, R) rowsum(dO * O)
+  float* lse2;             // (B, H, R) lse * log2(e) for the column kernel (written by the prep kernel), or null
   void* drows;             // (B, R, H*D)   grad of row side (out dtype)
   void* dkc;               // (B, T, ldg) partial grads of the gathered key side (fp32 or the input dtype)
   void* dvc;               // (B, T, ldg) partial grads of the gathered value side

@@ -65,7 +65,11 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
     """Compile and link ``xdot/_C.so``; returns its path."""
     os.makedirs(BUILD, exist_ok=True)
     inc, lib, abi = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", CSRC,
+    # -fno-slp-vectorize: no v_pk_mul/add_f32 beside the MFMAs (packed f32 VALU costs ~13
+    # issue cycles per instruction in an MFMA gap vs 4 for each scalar v_fma/v_mul: the
+    # softmax / softmax-grad epilogues of the flash kernels are VALU-issue bound)
+    extra = os.environ.get("XDOT_HIPCC_FLAGS", "-fno-slp-vectorize").split()
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", CSRC] + extra + [
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
               "-Wno-unused-result", "-Wno-unused-variable"]
     hdrs = _headers()
