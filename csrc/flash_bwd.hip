@@ -105,6 +105,13 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   asm volatile("" : "+v"(lse2), "+v"(dlt));
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
+  // -dO fragments + a δ-filled seed (loop-invariant): the dPᵀ accumulator ends at δ - dP, so
+  // dSᵀ' = Pᵀ ⊙ acc = -dSᵀ with no per-element subtract; the dk epilogue scales by -scale
+#pragma unroll
+  for (int s = 0; s < KS; ++s) df[s] ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+  f32x16 dseed;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dseed[r] = dlt;
 
   const int ldb = a.ldkv * 2;
   ImgDma<D> dma;
@@ -153,7 +160,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         f32x16 s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, 0, L), kf[0], f32x16{});
-        f32x16 dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, 0, L), df[0], f32x16{});
+        f32x16 dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, 0, L), df[0], dseed);
 #pragma unroll
         for (int ks = 1; ks < KS; ++ks) {
           s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s);
@@ -164,11 +171,11 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
           for (int r = 0; r < 16; ++r) {
             float x = __builtin_fmaf(s[r], c2, -lse2);
             if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
-            s[r] = fast_exp2(x) * (dp[r] - dlt);  // dSᵀ (unscaled)
+            s[r] = fast_exp2(x) * dp[r];  // -dSᵀ (unscaled)
           }
         } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(__builtin_fmaf(s[r], c2, -lse2)) * (dp[r] - dlt);
+          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(__builtin_fmaf(s[r], c2, -lse2)) * dp[r];
         }
         const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
 #pragma unroll
@@ -196,13 +203,14 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
       if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
     }
   }
+  const float nscale = -a.scale;  // dk was accumulated from -dS
   if (row_ok && (a.nsplit > 1 || a.force_partial)) {
     float* op = a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        f32x4 v = {dk[db][4 * g] * a.scale, dk[db][4 * g + 1] * a.scale, dk[db][4 * g + 2] * a.scale, dk[db][4 * g + 3] * a.scale};
+        f32x4 v = {dk[db][4 * g] * nscale, dk[db][4 * g + 1] * nscale, dk[db][4 * g + 2] * nscale, dk[db][4 * g + 3] * nscale};
         *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
       }
   } else if (row_ok) {
@@ -212,8 +220,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         u32x2 wv;
-        wv[0] = pack2<DT>(dk[db][4 * g + 0] * a.scale, dk[db][4 * g + 1] * a.scale);
-        wv[1] = pack2<DT>(dk[db][4 * g + 2] * a.scale, dk[db][4 * g + 3] * a.scale);
+        wv[0] = pack2<DT>(dk[db][4 * g + 0] * nscale, dk[db][4 * g + 1] * nscale);
+        wv[1] = pack2<DT>(dk[db][4 * g + 2] * nscale, dk[db][4 * g + 3] * nscale);
         *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = wv;
       }
   }
