@@ -143,3 +143,22 @@ def test_fused_adamw_kernel(gpu, dtype):
     for p, q in zip(ours, ref):
         tol = 1e-6 if dtype == torch.float32 else 2e-2
         torch.testing.assert_close(p.float(), q.detach(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("offset", [24, 100, None])
+def test_all_row_chunking_gpu(gpu, dt, offset):
+    """distributed_matmul_all with an offset: row-block plan (fp32 K-accumulation through the
+    GEMM's beta) and the reference's feature-column plan agree with torch (world size 1)."""
+    import xdot.parallel.functional as F
+    from xdot.utils.comm import LocalComm
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    left = torch.randn(2, 300, 300, generator=g).to(gpu, dt)
+    right = torch.randn(2, 300, 256, generator=g).to(gpu, dt)
+    ref = left.float() @ right.float()
+    for chunking in ("rows", "columns"):
+        out = F.distributed_matmul_all(left, right, offset, comm=LocalComm(), chunking=chunking)
+        assert out.dtype == dt
+        tol = 1e-3 if dt == torch.float32 else 0.15
+        assert (out.float() - ref).abs().max().item() < tol * ref.abs().max().item() ** 0.5, chunking

@@ -43,13 +43,13 @@ def cases(ws):
     }
 
 
-def run_case(op, left, right, offset):
+def run_case(op, left, right, offset, chunking="rows"):
     import xdot.parallel.functional as F
 
     if op == "nt":
         return F.distributed_matmul_nt(left, right, offset)
     if op == "all":
-        return F.distributed_matmul_all(left, right, offset)
+        return F.distributed_matmul_all(left, right, offset, chunking=chunking)
     return F.distributed_matmul_tn(left, right)
 
 
@@ -59,10 +59,13 @@ def check_all_modes(rank, ws, offsets):
     for name, (gl, gr, gt_fn, op) in cases(ws).items():
         gt = gt_fn(gl, gr)
         for off in offsets:
-            res = run_case(op, shard(gl, rank, ws), shard(gr, rank, ws), off)
-            full = F.gather_sequence(res, -2)
-            assert full.shape == gt.shape, (name, off, full.shape, gt.shape)
-            assert torch.equal(full, gt), f"{name} offset={off} rank={rank}"
+            # distributed_matmul_all: the default row-block plan and the reference's literal
+            # feature-column plan (same per-step gather budget)
+            for chunking in (("rows", "columns") if op == "all" else ("rows",)):
+                res = run_case(op, shard(gl, rank, ws), shard(gr, rank, ws), off, chunking)
+                full = F.gather_sequence(res, -2)
+                assert full.shape == gt.shape, (name, off, full.shape, gt.shape)
+                assert torch.equal(full, gt), f"{name} offset={off} chunking={chunking} rank={rank}"
 
 
 @pytest.mark.parametrize("ws", [1, 2, 3])

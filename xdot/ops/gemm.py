@@ -87,6 +87,30 @@ def all_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, d
 
 
 # ---------------------------------------------------------------------------------------
+# all, row-block chunks: acc[p] (+)= sum_j left[p, :, j*R + r0 : j*R + r0 + c] @ chunk[j, p]
+# ---------------------------------------------------------------------------------------
+def all_rows_chunk_into(acc: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, r0: int, accumulate: bool) -> None:
+    """``acc``: (Pn, R, D); ``left``: (Pn, R, T); ``chunk``: (N, Pn, c, D) = rows r0..r0+c of every
+    rank's ``right``.  ``accumulate``: add to ``acc`` (beta = 1) instead of overwriting it."""
+    N, Pn, c, D = chunk.shape
+    R, T = left.shape[-2], left.shape[-1]
+    Rr = T // N
+    if _ext.use_hip(acc, left, chunk) and hip_dtype_ok(left, chunk) and acc.dtype in _HIP_IN:
+        left = left.contiguous()
+        chunk = chunk.contiguous()
+        strided_gemm(left[..., r0:], chunk, acc, M=R, N=D, K=c, nseg=N, nb1=1, nb2=Pn,
+                     lda=T, ldb=D, ldc=D, sA2=R * T, sB2=c * D, sC2=R * D,
+                     sAseg=Rr, sBseg=Pn * c * D, a_mc=False, b_mc=True, beta=1.0 if accumulate else 0.0)
+        return
+    ct = acc.dtype if acc.dtype in (torch.float32, torch.float64) else torch.float32
+    part = sum(torch.matmul(left[..., j * Rr + r0:j * Rr + r0 + c].to(ct), chunk[j].to(ct)) for j in range(N))
+    if accumulate:
+        acc += part.to(acc.dtype)
+    else:
+        acc.copy_(part)
+
+
+# ---------------------------------------------------------------------------------------
 # tn: send[j, p] = left[p, :, j*R:(j+1)*R]^T @ right[p]   (reduce-scatter send buffer)
 # ---------------------------------------------------------------------------------------
 def tn_partials_into(send: torch.Tensor, left: torch.Tensor, right: torch.Tensor) -> None:

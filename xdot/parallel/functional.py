@@ -20,10 +20,12 @@ MI355X design, per op:
   (source rank, P) that writes straight into the final (P, R, T) layout — no ``(N,P,R,R)``
   staging buffer and no permute copy (reference K3/K4).  Optional ``alpha`` fuses the
   attention scale into the epilogue.
-* ``all`` (reference :161-212): all-gather ``right`` (feature-column chunks if ``offset``),
-  then one GEMM whose K loop walks the N source-rank column blocks of ``left`` in place — the
-  reference's full ``torch.stack`` copy of ``left`` (7.5 GB at T=75000) and the trailing
-  ``sum(dim=0)`` are gone; ``left`` is read once per chunk.
+* ``all`` (reference :161-212): all-gather ``right``, then one GEMM whose K loop walks the N
+  source-rank column blocks of ``left`` in place — the reference's full ``torch.stack`` copy
+  of ``left`` (7.5 GB at T=75000) and the trailing ``sum(dim=0)`` are gone.  With an
+  ``offset`` the gather buffer keeps the reference's size (N·R·offset elements) but holds
+  whole rows of ``right``, accumulated over K steps, so ``left`` is read exactly once
+  (the reference's feature-column chunks re-read it D/offset times: ``chunking='columns'``).
 * ``tn`` (reference :103-148): one batched GEMM producing all N partial blocks
   ``left[:, jR:(j+1)R]ᵀ·right`` into a contiguous send buffer (``left`` read transposed in
   place by the kernel's LDS transpose read), then ONE ``reduce_scatter`` — half the bytes and
@@ -103,10 +105,16 @@ def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offse
 @measure
 def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offset = None, *,
                            comm: Optional[_comm.Communicator] = None,
-                           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+                           out_dtype: Optional[torch.dtype] = None, chunking: str = "rows") -> torch.Tensor:
     """Row block ``r`` of ``L·R``: (P, R, T) x (P, R, D) -> (P, R, D).
 
-    ``offset``: feature columns of ``right`` gathered per step.  Reference: ``functions.py:161-212``.
+    ``offset`` bounds the per-step gather buffer exactly as in the reference, where a step
+    gathers ``offset`` feature columns of every rank's ``right`` (N·R·offset elements;
+    ``functions.py:161-212``).  ``chunking='columns'`` does literally that; each step then
+    re-reads the whole (R, T) ``left`` block (D/offset passes: 32 at offset 24, D 768).  The
+    default ``chunking='rows'`` spends the same buffer on ceil(R·offset/D) whole rows (all D
+    features) of every rank per step and accumulates the K-partial products in fp32, so
+    ``left`` is streamed exactly once whatever the offset.
     """
     _prep(left, right, "distributed_matmul_all")
     comm = comm or _comm.get_comm()
@@ -119,8 +127,14 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
     Pn = 1
     for d in P:
         Pn *= d
+    if chunking not in ("rows", "columns"):
+        raise ValueError(f"chunking must be 'rows' or 'columns', got {chunking!r}")
     off = resolve_offset(offset, D, n * Pn * Rr * right.element_size(), right.device)
-    chunks = plan_chunks(D, off)
+    by_rows = chunking == "rows" and off is not None and off < D and Rr > 0
+    if by_rows:  # same gather-buffer budget, whole rows: ceil(Rr * off / D) rows per step
+        chunks = plan_chunks(Rr, max(1, -(-Rr * off // D)))
+    else:
+        chunks = plan_chunks(D, off)
     check_consistent(comm, "all", left, right, tuple(chunks))
     out = torch.empty((Pn, R, D), dtype=_result_dtype(left, right, out_dtype), device=left.device)
     if R == 0 or D == 0:
@@ -129,6 +143,18 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
         return out.zero_().view(*P, R, D)
     l3 = left.reshape(Pn, R, T)
     r3 = right.reshape(Pn, Rr, D)
+
+    if by_rows:
+        acc = out if out.dtype in (torch.float32, torch.float64) else torch.empty_like(out, dtype=torch.float32)
+
+        def consume_rows(s, e, gathered):  # (N, Pn, c, D)
+            G.all_rows_chunk_into(acc, l3, gathered, s, accumulate=s > 0)
+
+        gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
+                        right.device, consume_rows)
+        if acc is not out:
+            out.copy_(acc)
+        return out.view(*P, R, D)
 
     def consume(s, e, gathered):  # (N, Pn, Rr, c)
         G.all_chunk_into(out, l3, gathered, s)
