@@ -35,6 +35,7 @@ from ..ops.linear import linear
 from ..ops.softmax import scale_mask_softmax
 from ..parallel.autograd import FullMultiplication, RightTransposeMultiplication
 from ..utils import comm as _comm
+from ..utils.env import FLAGS
 
 __all__ = ["DistributedDotProductAttn"]
 
@@ -79,6 +80,12 @@ class DistributedDotProductAttn(nn.Module):
             from ..parallel.attention import seq_parallel_attention_packed, start_gather
 
             comm = (self.comm or _comm.get_comm()) if self.distributed else _comm.LocalComm()
+            if attn_mask is not None and attn_mask.is_cuda and attn_mask.dim() == 3 and FLAGS.mask_async:
+                # pack the mask on a side stream while the projection GEMMs run
+                from ..ops import flash
+
+                attn_mask = flash.prepare_mask_async(attn_mask.to(torch.bool), attn_mask.shape[0],
+                                                     attn_mask.shape[1], attn_mask.shape[2])
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
             pending = start_gather(qv, comm)

@@ -41,6 +41,43 @@ def prepare_mask(mask: Optional[torch.Tensor], B: int, R: int, T: int) -> Option
     return PackedMask(bits, flags, bits_t, mask.shape)
 
 
+class PendingMask:
+    """A mask being packed on a side stream (:func:`prepare_mask_async`): the packing overlaps
+    whatever the current stream does meanwhile (the projection GEMMs); :meth:`get` orders the
+    calling stream after it."""
+
+    __slots__ = ("raw", "shape", "_packed", "_event")
+
+    def __init__(self, raw: torch.Tensor, packed: PackedMask, event):
+        self.raw, self.shape, self._packed, self._event = raw, tuple(raw.shape), packed, event
+
+    def get(self) -> PackedMask:
+        cur = torch.cuda.current_stream(self.raw.device)
+        cur.wait_event(self._event)
+        for t in (self._packed.bits, self._packed.flags, self._packed.bits_t):
+            t.record_stream(cur)
+        return self._packed
+
+
+_AUX = {}
+
+
+def prepare_mask_async(mask: torch.Tensor, B: int, R: int, T: int) -> PendingMask:
+    """:func:`prepare_mask` on a per-device side stream, ordered after the current stream."""
+    dev = mask.device
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _AUX:
+        _AUX[i] = torch.cuda.Stream(device=i)
+    side = _AUX[i]
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        packed = prepare_mask(mask, B, R, T)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    mask.record_stream(side)
+    return PendingMask(mask, packed, ev)
+
+
 def gathered_to_btc(g: torch.Tensor) -> torch.Tensor:
     """(N, B, Rc, C) rank-major all-gather output -> (B, N*Rc, C)."""
     N, B, Rc, C = g.shape

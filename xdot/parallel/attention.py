@@ -205,9 +205,16 @@ class SeqParallelAttention(torch.autograd.Function):
         if use_hip:
             from ..ops import flash
 
-            # masks are packed per chunk while the gathers are in flight
+            # masks are packed per chunk while the gathers are in flight (or were packed on a
+            # side stream before the projections: flash.PendingMask)
             mks = []
+            if isinstance(mask, flash.PendingMask):
+                if len(chunks) == 1:
+                    mks.append(mask.get())
+                mask = mask.raw
             for r0, rc in chunks:
+                if mks and len(chunks) == 1:
+                    break
                 if mask is None:
                     mks.append(None)
                     continue
@@ -231,6 +238,7 @@ class SeqParallelAttention(torch.autograd.Function):
                                           float(scale), opart, lpart, c * ns, ns)
                 o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
         else:
+            mask = getattr(mask, "raw", mask)
             mks = [mask]
             qvg = torch.cat(pending.wait_all(), dim=2) if len(chunks) > 1 else pending.wait(0)  # (N, B, R, 2C)
             o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
@@ -341,7 +349,8 @@ def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor],
         T = qv.shape[1] * comm.world_size
         if tuple(mask.shape) != (k.shape[0], k.shape[1], T):
             raise ValueError(f"mask must be (B, R, T)=({k.shape[0]}, {k.shape[1]}, {T}), got {tuple(mask.shape)}")
-        mask = mask.to(torch.bool)
+        if isinstance(mask, torch.Tensor):
+            mask = mask.to(torch.bool)
     return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm, pending)
 
 

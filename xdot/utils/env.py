@@ -18,6 +18,10 @@
                                pipeline with several ranks (default 1 = one collective each; 2+
                                overlaps them with the kernels at ~0.2 ms extra compute per
                                8-rank step: worth it only on a slow interconnect)
+``XDOT_MASK_ASYNC``            ``1``: pack the attention mask on a side stream, overlapping the
+                               projection GEMMs (default off: no gain measured at N=1, 9.23-9.29
+                               vs 9.23-9.25 ms; with several ranks packing already overlaps the
+                               all-gather)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
@@ -46,6 +50,7 @@ class _Flags:
         self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
         self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
+        self.mask_async = _flag("XDOT_MASK_ASYNC")
 
 
 FLAGS = _Flags()
