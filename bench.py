@@ -166,7 +166,7 @@ def main(argv=None, comm=None):
             "loss": lossv,
         }
         if emulated:
-            rec["metric"] = "EMULATED per-rank step (no transport; diagnostics only): " + METRIC
+            rec["metric"] = "EMULATED per-rank step (no transport; diagnostics only): " + metric
             rec["config"]["parallelism"] += "-emulated"
         print(json.dumps(rec), flush=True)
     if not emulated:
