@@ -131,11 +131,14 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   if (v2 && a_mc) v2 = M % 8 == 0;
   if (v2 && b_mc) v2 = N % 8 == 0;
   if (v2 && mode != 2) {
-    // auto: outputs that fill 256-wide tiles, and enough of them (>= 32 per batch entry or
-    // >= 512 overall) -- small outputs batched over K slabs (the split-K weight gradients of
-    // xdot.ops.linear) keep the 128x128 kernel, which fills the GPU without a second split
+    // auto: enough 256x256 tiles (>= 32 per batch entry or >= 512 overall) -- small outputs
+    // batched over K slabs (the split-K weight gradients of xdot.ops.linear) keep the 128x128
+    // kernel, which fills the GPU without a second split.  Skinny outputs (one side 64..191,
+    // e.g. N = head dim 96 in the materialised path) still go to v2: streaming the long operand
+    // through its deeper LDS-DMA ring beats v1's register staging even with 62 % of the tile
+    // idle (materialised step 39.3 -> 34.2 ms at T = 25000)
     const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
-    v2 = M >= 192 && N >= 192 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
+    v2 = M >= 64 && N >= 64 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
   }
   if (v2 && K > 0) {
     // split-K: fewest k-slices S minimising ceil(items / CUs) / S (idle CUs of the last round),
