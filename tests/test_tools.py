@@ -1,0 +1,117 @@
+"""Entry points and tooling on the CPU: ``bench.py`` (the driver's JSON-line contract),
+``benchmarks/bench_ops.py`` (reference ``benchmark.py`` CLI + 8-key records, run over gloo
+with 2 ranks — BASELINE.json config 1), ``example.py`` (reference ``example.py:1-33``) and
+the ``distributed_dot_product`` import shim (reference import lines unchanged)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from _dist import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# the 8 record keys of the reference's benchmark.py:241-253
+REF_KEYS = ("input_memory", "total_time", "peak_memory", "output_memory", "distributed_input_memory",
+            "distributed_time", "distributed_peak_memory", "distributed_output_memory")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "2"
+    env["HIP_VISIBLE_DEVICES"] = ""      # CPU path even on a GPU box
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
+def _run(args, timeout=240):
+    p = subprocess.run([sys.executable] + args, cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=timeout)
+    assert p.returncode == 0, f"exit {p.returncode}\nstdout:\n{p.stdout[-3000:]}\nstderr:\n{p.stderr[-3000:]}"
+    return p.stdout
+
+
+def _json_lines(out):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def _torchrun(n):
+    return ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+            "--master-port", str(free_port())]
+
+
+def test_bench_contract_cpu():
+    out = _run(["bench.py", "--device", "cpu", "--dtype", "fp32", "--seq-len", "128", "--dim", "64",
+                "--heads", "4", "--steps", "2", "--warmup", "1"])
+    recs = _json_lines(out)
+    assert len(recs) == 1, out
+    r = recs[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["value"] > 0 and r["value"] == r["ms_per_step"] and r["higher_is_better"] is False
+    assert r["config"]["seq_len"] == 128 and "T=128" in r["metric"]
+    assert "synthetic" in r["data"]
+
+
+def test_bench_two_ranks_gloo():
+    """The driver's N>1 launch line, on the CPU over gloo: ONE JSON line, from rank 0."""
+    out = _run(_torchrun(2) + ["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--dtype", "fp32",
+                               "--seq-len", "128", "--dim", "64", "--heads", "4", "--steps", "2", "--warmup", "1"])
+    recs = _json_lines(out)
+    assert len(recs) == 1, out
+    assert recs[0]["n_gpus"] == 2 and recs[0]["config"]["parallelism"] == "sp2"
+
+
+@pytest.mark.parametrize("mode", ["nt", "all", "tn"])
+def test_bench_ops_records_gloo(tmp_path, mode):
+    """BASELINE.json config 1 (nt, gloo world size 2, T=256, d=64, offset=32) and the other two
+    reference modes: a JSON list of records with the reference's 8 keys plus the extras."""
+    f = tmp_path / f"{mode}.json"
+    out = _run(_torchrun(2) + ["benchmarks/bench_ops.py", "--mode", mode, "--T", "256", "--dim", "64", "--offset",
+                               "32", "--iters", "2", "--warmup", "1", "--file", str(f)])
+    assert len(_json_lines(out)) == 1
+    data = json.loads(f.read_text())
+    assert isinstance(data, list) and len(data) == 1
+    rec = data[0]
+    for k in REF_KEYS:
+        assert k in rec, k
+    assert rec["world_size"] == 2 and rec["T"] == 256 and rec["D"] == 64 and rec["offset"] == 32
+    assert rec["ms_p50"] > 0 and rec["distributed_time"] > 0
+
+
+def test_bench_ops_fwd_bwd_mode_emulated():
+    out = _run(["benchmarks/bench_ops.py", "--mode", "leftT_fb", "--T", "96", "--dim", "16", "--emulate", "3",
+                "--iters", "1", "--warmup", "0"])
+    rec = _json_lines(out)[0]
+    assert rec["world_size"] == 3 and rec["emulated"] is True and rec["mode"] == "leftT_fb"
+
+
+def test_example_runs():
+    out = _run(["example.py"], timeout=300)
+    assert "rank 0/1" in out and "loss" in out
+
+
+def test_reference_import_lines():
+    """Reference import paths (example.py:10, tests/test_multiplication.py, tests/test_gradient.py)."""
+    code = "\n".join([
+        "from distributed_dot_product.module import DistributedDotProductAttn",
+        "from distributed_dot_product.multiplication.functions import (distributed_matmul_nt,",
+        "    distributed_matmul_tn, distributed_matmul_all, distributed_matmul_block)",
+        "from distributed_dot_product.multiplication.ops import (RightTransposeMultiplication,",
+        "    FullMultiplication, LeftTransposeMultiplication)",
+        "from distributed_dot_product.utils.comm import get_world_size, get_rank, is_main_process, synchronize",
+        "import distributed_dot_product as d",
+        "m = DistributedDotProductAttn(32, num_heads=4)",
+        "assert {k.split('.')[0] for k in m.state_dict()} == {'keys', 'queries', 'values', 'composition'}",
+        "assert get_world_size() == 1 and get_rank() == 0 and is_main_process()",
+        "print('ok', d.__version__)",
+    ])
+    out = _run(["-c", code])
+    assert out.startswith("ok")
