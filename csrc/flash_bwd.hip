@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 // ---------------------------------------------------------------------------------------
 // grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols arrive by
 // LDS-DMA into the same ring as the forward's (RowsCfg).
-template <int DT, int D, int WPS = 2>
+template <int DT, int D, int WPS = 2, bool PS = false>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
@@ -112,6 +112,15 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   f32x16 dseed;
 #pragma unroll
   for (int r = 0; r < 16; ++r) dseed[r] = dlt;
+  // PS: K rows pre-scaled by scale*log2 e (one bf16 rounding, like the projection's own) and
+  // the Sᵀ accumulator seeded with -lse2, so P = 2^acc: no per-element FMA
+  f32x16 sseed;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sseed[r] = PS ? -lse2 : 0.f;
+  if constexpr (PS) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) kf[s] = scale_frag<DT>(kf[s], c2);
+  }
 
   const int ldb = a.ldkv * 2;
   ImgDma<D> dma;
@@ -159,7 +168,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
       // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        f32x16 s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, 0, L), kf[0], f32x16{});
+        f32x16 s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, 0, L), kf[0], sseed);
         f32x16 dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, 0, L), df[0], dseed);
 #pragma unroll
         for (int ks = 1; ks < KS; ++ks) {
@@ -169,13 +178,13 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         if (chk) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            float x = __builtin_fmaf(s[r], c2, -lse2);
+            float x = PS ? s[r] : __builtin_fmaf(s[r], c2, -lse2);
             if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
             s[r] = fast_exp2(x) * dp[r];  // -dSᵀ (unscaled)
           }
         } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(__builtin_fmaf(s[r], c2, -lse2)) * dp[r];
+          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(PS ? s[r] : __builtin_fmaf(s[r], c2, -lse2)) * dp[r];
         }
         const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
 #pragma unroll
@@ -249,7 +258,7 @@ template <int D, int NB = 0> struct ColsCfg {
   static constexpr int NG = 2 * IPW + 2;  // DMAs per wave per tile
 };
 
-template <int DT, int D, int WPS = 2, int NB = 0>
+template <int DT, int D, int WPS = 2, int NB = 0, bool PS = false>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = ColsCfg<D, NB>;
@@ -293,6 +302,12 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     for (int s = 0; s < KS; ++s) vf[s] ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
   }
   const float c2 = a.scale * LOG2E;
+  // PS: Q columns pre-scaled by scale*log2 e and the S accumulator seeded with -lse2 of its
+  // rows, so P = 2^acc (no per-element FMA in softmax_grad)
+  if constexpr (PS) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = scale_frag<DT>(qf[s], c2);
+  }
   const float NEG_INF = -__builtin_inff();
   const int NRT = (a.R + 63) / 64;
 
@@ -344,11 +359,12 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int rbase = tt * 32 + 8 * g + 4 * hf;
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + rbase);  // lse * log2 e
+      f32x4 l4 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (!PS) l4 = *reinterpret_cast<const f32x4*>(ls + rbase);  // lse * log2 e
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
-        float x = __builtin_fmaf(s[r], c2, -l4[e]);
+        float x = PS ? s[r] : __builtin_fmaf(s[r], c2, -l4[e]);
         if (masked && ((hw >> (8 * g + e)) & 1u)) x = NEG_INF;
         const float p = fast_exp2(x);
         s[r] = p;
@@ -364,6 +380,18 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + tt * 32 + 8 * g + 4 * hf);
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[4 * g + e] = d4[e];
+    }
+    return d;
+  };
+
+  // S accumulator seed (PS): -lse2 of the half tile's rows in the accumulator's row order
+  auto lse_seed = [&](const float* ls, int tt) {
+    f32x16 d;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + tt * 32 + 8 * g + 4 * hf);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[4 * g + e] = -l4[e];
     }
     return d;
   };
@@ -391,7 +419,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     if (flag != 1 && c0 < a.T) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], f32x16{});
+        f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], PS ? lse_seed(ls, tt) : f32x16{});
         f32x16 dp = mfma32<DT>::run(row_frag<D>(ds, tt * 32, 0, L), vf[0], delta_seed(dls, tt));
 #pragma unroll
         for (int kk = 1; kk < KS; ++kk) {
@@ -491,12 +519,25 @@ inline int cols_nbuf() {
   return v;
 }
 
+// Backward with pre-scaled operands (XDOT_BWD_PRESCALE=1, read once): the row-side K (rows
+// kernel) / the gathered Q (cols kernel) are multiplied by scale*log2 e in registers and the
+// S accumulators are seeded with -lse*log2 e, removing one FMA per score element.
+inline bool bwd_prescale() {
+  static const bool v = [] {
+    const char* e = std::getenv("XDOT_BWD_PRESCALE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
   constexpr int LDS = ColsCfg<D>::NBUF * ColsCfg<D>::STAGE;
   constexpr int LDS2 = 2 * ColsCfg<D, 2>::STAGE;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
+  else if (cols_nbuf() == 2 && bwd_prescale())
+    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2, true>), dim3(ncb * a.B * a.H), dim3(256), LDS2, st, a);
   else if (cols_nbuf() == 2)
     hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS2, st, a);
   else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
@@ -513,6 +554,8 @@ static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
   constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+  else if (bwd_prescale())
+    hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   if (a.nsplit > 1 && !a.force_partial) launch_rows_sum<DT, D>(a, st);
 }

@@ -22,6 +22,12 @@
                                projection GEMMs (default off: no gain measured at N=1, 9.23-9.29
                                vs 9.23-9.25 ms; with several ranks packing already overlaps the
                                all-gather)
+``XDOT_BWD_PRESCALE``          ``1``: flash backward kernels multiply the register-resident score
+                               operand by scale*log2 e once and seed the score accumulator
+                               with -LSE (one FMA less per score element; one extra bf16
+                               rounding of that operand).  Off: measured +1-1.5 % per kernel
+                               (cols 4.07->4.03 ms, rows 2.79->2.75 ms at T=R=25000), within
+                               box noise on the step
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
