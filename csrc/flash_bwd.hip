@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 // ---------------------------------------------------------------------------------------
 // grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols arrive by
 // LDS-DMA into the same ring as the forward's (RowsCfg).
-template <int DT, int D, int WPS = 2, bool PS = false>
+template <int DT, int D, int WPS = 2, bool PS = false, bool PIPE = false>
 __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
@@ -153,6 +153,82 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   for (int i = 0; i < DB; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
+  // PIPE: software-pipelined tile body.  Per 64-column tile the wave runs
+  //   A0: Sᵀ/dPᵀ chains of sub-tile 0 (12 MFMAs, operand reads two ahead)
+  //   A1 ∥ V0: the chains of sub-tile 1, each MFMA followed by its share of sub-tile 0's
+  //            softmax gradient (FMA, v_exp, multiply)
+  //   K0 ∥ V1: dk += Q·dSᵀ of sub-tile 0, each MFMA followed by a share of sub-tile 1's VALU
+  //   K1:      dk of sub-tile 1
+  // so nearly all the VALU work issues between this wave's own MFMAs (the plain body runs
+  // S/dP -> VALU -> dk back to back and leaves the matrix pipe to the partner wave during
+  // the VALU block).  Costs 32 more live accumulator registers.
+  auto pipe_body = [&](auto chkc, const char* qs, const char* vs, uint64_t w) {
+    constexpr bool CHK = decltype(chkc)::value;
+    constexpr int NA = 2 * KS, NK = 2 * DB;
+    auto elem = [&](f32x16& sc, const f32x16& dc, int tt, int r) {
+      float x = PS ? sc[r] : __builtin_fmaf(sc[r], c2, -lse2);
+      if constexpr (CHK) {
+        if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
+      }
+      float y = fast_exp2(x) * dc[r];  // -dSᵀ (unscaled)
+      asm volatile("" : "+v"(y));      // keeps it in this MFMA gap (LLVM would sink it to its use)
+      sc[r] = y;
+    };
+    // operand i of a sub-tile's interleaved S (even i) / dP (odd i) chains
+    auto opnd = [&](int tt, int i) { return (i & 1) ? row_frag<D>(vs, tt * 32, i >> 1, L) : row_frag<D>(qs, tt * 32, i >> 1, L); };
+    f32x16 s0, d0, s1, d1;
+    {
+      u32x4 o0 = opnd(0, 0), o1 = opnd(0, 1);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        u32x4 o2 = o1;
+        if (i + 2 < NA) o2 = opnd(0, i + 2);
+        const int ks = i >> 1;
+        if (i & 1) d0 = mfma32<DT>::run(o0, df[ks], ks == 0 ? dseed : d0);
+        else s0 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sseed : s0);
+        o0 = o1;
+        o1 = o2;
+      }
+    }
+    {
+      u32x4 o0 = opnd(1, 0), o1 = opnd(1, 1);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        u32x4 o2 = o1;
+        if (i + 2 < NA) o2 = opnd(1, i + 2);
+        const int ks = i >> 1;
+        if (i & 1) d1 = mfma32<DT>::run(o0, df[ks], ks == 0 ? dseed : d1);
+        else s1 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sseed : s1);
+#pragma unroll
+        for (int j = (i * 16) / NA; j < ((i + 1) * 16) / NA; ++j) elem(s0, d0, 0, j);
+        __builtin_amdgcn_sched_barrier(0);
+        o0 = o1;
+        o1 = o2;
+      }
+    }
+    const u32x4 p00 = acc_to_frag<DT>(s0, 0), p01 = acc_to_frag<DT>(s0, 1);
+    {
+      u32x4 t0 = tr_frag<D>(qs, 0, 0, L), t1 = tr_frag<D>(qs, 16, 0, L);
+#pragma unroll
+      for (int i = 0; i < NK; ++i) {
+        u32x4 t2 = t1;
+        if (i + 2 < NK) t2 = tr_frag<D>(qs, ((i + 2) & 1) * 16, ((i + 2) >> 1) * 32, L);
+        dk[i >> 1] = mfma32<DT>::run(t0, (i & 1) ? p01 : p00, dk[i >> 1]);
+#pragma unroll
+        for (int j = (i * 16) / NK; j < ((i + 1) * 16) / NK; ++j) elem(s1, d1, 1, j);
+        __builtin_amdgcn_sched_barrier(0);
+        t0 = t1;
+        t1 = t2;
+      }
+    }
+    const u32x4 p10 = acc_to_frag<DT>(s1, 0), p11 = acc_to_frag<DT>(s1, 1);
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+      dk[db] = mfma32<DT>::run(tr_frag<D>(qs, 32, db * 32, L), p10, dk[db]);
+      dk[db] = mfma32<DT>::run(tr_frag<D>(qs, 48, db * 32, L), p11, dk[db]);
+    }
+  };
+
   auto tile = [&](auto bufc, int kt) {
     constexpr int BUF = decltype(bufc)::value;
     if (kt + PF < kt_end) issue(kt + PF);
@@ -160,7 +236,15 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     const char* vs = qs + IMG;
     const int flag = r0 >= a.R ? 1 : (fwg ? staged_flag(qs + CF::OFF_F, wave, kt & 3) : 0);
     const bool tail = (kt + 1) * 64 > a.T;
-    if (flag != 1 && r0 < a.R) {
+    if (PIPE && flag != 1 && r0 < a.R) {
+      if (flag == 2 || tail) {
+        const uint64_t w = tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
+                                     a.T - kt * 64, hf);
+        pipe_body(std::true_type{}, qs, vs, w);
+      } else {
+        pipe_body(std::false_type{}, qs, vs, 0ull);
+      }
+    } else if (flag != 1 && r0 < a.R) {
       const bool chk = flag == 2 || tail;
       const uint64_t w = chk ? tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
                                          a.T - kt * 64, hf)
@@ -530,6 +614,17 @@ inline bool bwd_prescale() {
   return v;
 }
 
+// Software-pipelined row kernel body (default; XDOT_ROWS_PIPE=0 selects the plain body, read
+// once); see pipe_body.  MI355X, T = R = 25000, D = 96: 2.63 -> 2.59 ms (1.10 PFLOP/s), headline
+// step 8.70 -> 8.63 ms, emulated N=8 rank step 1.460 -> 1.449 ms (3 alternating runs each).
+inline bool rows_pipe() {
+  static const bool v = [] {
+    const char* e = std::getenv("XDOT_ROWS_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
@@ -554,6 +649,8 @@ static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
   constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
   if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+  else if (rows_pipe())
+    hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, false, true>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   else if (bwd_prescale())
     hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);

@@ -28,6 +28,9 @@
                                rounding of that operand).  Off: measured +1-1.5 % per kernel
                                (cols 4.07->4.03 ms, rows 2.79->2.75 ms at T=R=25000), within
                                box noise on the step
+``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
+                               row kernel (default 1: VALU of one sub-tile issues between the
+                               next sub-tile's MFMAs; 1.5 % faster kernel)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
