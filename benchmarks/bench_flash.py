@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--only", default="all", choices=["all", "fwd", "bwd_cols", "bwd_rows", "mask"])
     ap.add_argument("--mask", action="store_true", help="pass an all-False (B, R, T) mask")
     ap.add_argument("--nsplit", type=int, default=0)
+    ap.add_argument("--no-prescale", action="store_true",
+                    help="kernels scale every score (default: pre-scaled rows + seeded accumulators, the module's path)")
     ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
     ap.add_argument("--concurrent", action="store_true",
                     help="also time bwd_cols and bwd_rows launched together on two streams (cols on a normal "
@@ -64,21 +66,23 @@ def main():
     mask = torch.zeros(B, R, T, dtype=torch.bool, device=dev) if a.mask else None
     mk = flash.prepare_mask(mask, B, R, T)
     scale = 1.0 / math.sqrt(D)
-    out, lse = flash.fwd(rows, kc, vc, mk, H, scale, a.nsplit)
-    dkv, delta = flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale)
+    ps = not a.no_prescale
+    rk = flash.prescale(rows, scale) if ps else rows
+    out, lse = flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps)
+    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps)
     gemm = 2.0 * B * R * T * H * D
     res = []
     if a.only in ("all", "mask") and mask is not None:
         ms, mn = timeit(lambda: flash.prepare_mask(mask, B, R, T), a.iters)
         res.append({"kernel": "mask_pack", "ms": ms, "min_ms": mn, "GB_s": B * R * T / ms / 1e6})
     if a.only in ("all", "fwd"):
-        ms, mn = timeit(lambda: flash.fwd(rows, kc, vc, mk, H, scale, a.nsplit), a.iters)
+        ms, mn = timeit(lambda: flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps), a.iters)
         res.append({"kernel": "flash_fwd", "ms": ms, "min_ms": mn, "TFLOPs": 2 * gemm / ms / 1e9})
     if a.only in ("all", "bwd_cols"):
-        ms, mn = timeit(lambda: flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale), a.iters)
+        ms, mn = timeit(lambda: flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps), a.iters)
         res.append({"kernel": "flash_bwd_cols", "ms": ms, "min_ms": mn, "TFLOPs": 4 * gemm / ms / 1e9})
     if a.only in ("all", "bwd_rows"):
-        ms, mn = timeit(lambda: flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale, a.nsplit), a.iters)
+        ms, mn = timeit(lambda: flash.bwd_rows(do, rk, kc, vc, lse, delta, mk, H, scale, a.nsplit, prescaled=ps), a.iters)
         res.append({"kernel": "flash_bwd_rows", "ms": ms, "min_ms": mn, "TFLOPs": 3 * gemm / ms / 1e9})
     if a.concurrent:
         for prio in (0, -1):
@@ -90,9 +94,9 @@ def main():
                 e0.record()
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
-                    flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale, delta)
+                    flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, delta, prescaled=ps)
                     ec.record()
-                flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale, a.nsplit)
+                flash.bwd_rows(do, rk, kc, vc, lse, delta, mk, H, scale, a.nsplit, prescaled=ps)
                 cur.wait_stream(side)
                 e1.record()
                 e1.synchronize()

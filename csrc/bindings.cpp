@@ -301,7 +301,7 @@ int pick_split(int64_t blocks, int64_t T, int64_t slots, int64_t req) {
 
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
-                                             int64_t H, double scale, int64_t nsplit) {
+                                             int64_t H, double scale, int64_t nsplit, bool prescaled) {
   Range rr_("xdot.flash_fwd");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   auto out = at::empty_like(rows);
@@ -324,6 +324,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   a.nsplit = ns;
   a.opart = ns > 1 ? opart.data_ptr<float>() : nullptr;
   a.lpart = ns > 1 ? lpart.data_ptr<float>() : nullptr;
+  a.prescaled = prescaled ? 1 : 0;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0, "xdot.flash_fwd: config");
   check_launch(hipGetLastError(), "flash_fwd");
@@ -356,12 +357,13 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
                                                               double scale, const c10::optional<at::Tensor>& delta_in,
-                                                              bool fp32_out) {
+                                                              bool fp32_out, bool prescaled) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
+  a.prescaled = prescaled ? 1 : 0;
   auto dkv = at::empty({g.B, g.T, 2 * g.C}, fp32_out ? kc.options().dtype(at::kFloat) : kc.options());
   const bool have_delta = delta_in.has_value() && delta_in->defined();
   at::Tensor delta;
@@ -401,6 +403,20 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
   TORCH_CHECK(xdot_sum_partials_launch(part.data_ptr<float>(), out.data_ptr(), (int)part.size(0), n, dt_code(out_dtype),
                                        cur_stream(part)) == 0, "xdot.sum_partials: unsupported dtype");
   check_launch(hipGetLastError(), "sum_partials");
+  return out;
+}
+
+// row side of the flash kernels pre-multiplied by scale * log2(e), in the input dtype
+at::Tensor flash_prescale(const at::Tensor& x, double scale) {
+  Range rr_("xdot.flash_prescale");
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) &&
+                  x.numel() % 8 == 0 && aligned16(x.data_ptr()),
+              "xdot.flash_prescale: contiguous 16-byte aligned bf16/fp16 device tensor, numel % 8 == 0");
+  auto out = at::empty_like(x);
+  c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(xdot_prescale_rows_launch(x.data_ptr(), out.data_ptr(), x.numel(), (float)scale, dt_code(x.scalar_type()),
+                                        cur_stream(x)) == 0, "xdot.flash_prescale: dtype");
+  check_launch(hipGetLastError(), "flash_prescale");
   return out;
 }
 
@@ -469,7 +485,8 @@ at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_
 // row-side grad (this rank's rows), column-split when the row count is small
 at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                           const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
-                          const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit) {
+                          const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit,
+                          bool prescaled) {
   Range rr_("xdot.flash_bwd_rows");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
@@ -481,6 +498,7 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   if (ns > 1) dpart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
   a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
   a.nsplit = ns; a.dpart = ns > 1 ? dpart.data_ptr<float>() : nullptr;
+  a.prescaled = prescaled ? 1 : 0;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows: config");
@@ -505,7 +523,8 @@ void check_part(const at::Tensor& t, int64_t slots_needed, int64_t per_slot, con
 // forward over this column chunk into partial slots [sp0, sp0 + nsplit) of opart / lpart
 void flash_fwd_partial(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                        const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags, int64_t H,
-                       double scale, at::Tensor& opart, at::Tensor& lpart, int64_t sp0, int64_t nsplit) {
+                       double scale, at::Tensor& opart, at::Tensor& lpart, int64_t sp0, int64_t nsplit,
+                       bool prescaled) {
   Range rr_("xdot.flash_fwd_partial");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(sp0 >= 0 && nsplit >= 1, "xdot.flash_fwd_partial: slots");
@@ -521,6 +540,7 @@ void flash_fwd_partial(const at::Tensor& rows, const at::Tensor& kc, const at::T
   a.ldkv = g.ld;
   a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1;
   a.opart = opart.data_ptr<float>(); a.lpart = lpart.data_ptr<float>();
+  a.prescaled = prescaled ? 1 : 0;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_fwd_partial: config");
@@ -553,7 +573,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd_combine(const at::Tensor& opart, co
 void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                             const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                             const c10::optional<at::Tensor>& flags, int64_t H, double scale, at::Tensor& dpart,
-                            int64_t sp0, int64_t nsplit) {
+                            int64_t sp0, int64_t nsplit, bool prescaled) {
   Range rr_("xdot.flash_bwd_rows_partial");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
@@ -564,6 +584,7 @@ void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, cons
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   a.delta = delta.data_ptr<float>();
   a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1; a.dpart = dpart.data_ptr<float>();
+  a.prescaled = prescaled ? 1 : 0;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows_partial: config");
@@ -595,22 +616,23 @@ TORCH_LIBRARY(xdot, m) {
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
-  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0) -> (Tensor, Tensor)");
+  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
-        "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True) -> (Tensor, Tensor)");
+        "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
   m.def("flash_splits(int B, int R, int T, int H, bool rows_kernel) -> int");
   m.def("flash_fwd_partial(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, "
-        "Tensor(a!) opart, Tensor(b!) lpart, int sp0, int nsplit) -> ()");
+        "Tensor(a!) opart, Tensor(b!) lpart, int sp0, int nsplit, bool prescaled=False) -> ()");
   m.def("flash_fwd_combine(Tensor opart, Tensor lpart, int H, Tensor like) -> (Tensor, Tensor)");
   m.def("flash_bwd_rows_partial(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit) -> ()");
+        "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit, bool prescaled=False) -> ()");
   m.def("flash_bwd_rows_sum(Tensor dpart, int H, Tensor like) -> Tensor");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, int nsplit=0) -> Tensor");
+        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
+  m.def("flash_prescale(Tensor x, float scale) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
@@ -627,6 +649,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);
   m.impl("sum_partials", &sum_partials);
+  m.impl("flash_prescale", &flash_prescale);
   m.impl("flash_fwd_partial", &flash_fwd_partial);
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);

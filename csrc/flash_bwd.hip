@@ -112,15 +112,11 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   f32x16 dseed;
 #pragma unroll
   for (int r = 0; r < 16; ++r) dseed[r] = dlt;
-  // PS: K rows pre-scaled by scale*log2 e (one bf16 rounding, like the projection's own) and
-  // the Sᵀ accumulator seeded with -lse2, so P = 2^acc: no per-element FMA
+  // PS: K rows pre-multiplied by scale*log2 e on the host (the forward's buffer) and the Sᵀ
+  // accumulator seeded with -lse2, so P = 2^acc: no per-element FMA
   f32x16 sseed;
 #pragma unroll
   for (int r = 0; r < 16; ++r) sseed[r] = PS ? -lse2 : 0.f;
-  if constexpr (PS) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) kf[s] = scale_frag<DT>(kf[s], c2);
-  }
 
   const int ldb = a.ldkv * 2;
   ImgDma<D> dma;
@@ -386,12 +382,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
     for (int s = 0; s < KS; ++s) vf[s] ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
   }
   const float c2 = a.scale * LOG2E;
-  // PS: Q columns pre-scaled by scale*log2 e and the S accumulator seeded with -lse2 of its
-  // rows, so P = 2^acc (no per-element FMA in softmax_grad)
-  if constexpr (PS) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = scale_frag<DT>(qf[s], c2);
-  }
+  // PS: the K-row images hold K * scale * log2 e (host pre-scaled, the forward's buffer) and the
+  // S accumulator is seeded with -lse2 of its rows, so P = 2^acc (no per-element FMA in
+  // softmax_grad); dq = Σ dS'·K' then carries the factor -ln 2 instead of -scale
   const float NEG_INF = -__builtin_inff();
   const int NRT = (a.R + 63) / 64;
 
@@ -536,7 +529,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       if (rt + 2 < NRT) tile(std::integral_constant<int, 2>{}, rt + 2);
     }
   }
-  const float nscale = -a.scale;  // dq was accumulated from -dS
+  const float nscale = PS ? -LN2 : -a.scale;  // dq was accumulated from -dS (and K' = K * scale * log2 e)
   if (col_ok && a.dkv16) {  // input dtype: half the store (and reduce-scatter) bytes
     const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
     T16* pq = reinterpret_cast<T16*>(a.dkc) + off;
@@ -603,17 +596,6 @@ inline int cols_nbuf() {
   return v;
 }
 
-// Backward with pre-scaled operands (XDOT_BWD_PRESCALE=1, read once): the row-side K (rows
-// kernel) / the gathered Q (cols kernel) are multiplied by scale*log2 e in registers and the
-// S accumulators are seeded with -lse*log2 e, removing one FMA per score element.
-inline bool bwd_prescale() {
-  static const bool v = [] {
-    const char* e = std::getenv("XDOT_BWD_PRESCALE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 // Software-pipelined row kernel body (default; XDOT_ROWS_PIPE=0 selects the plain body, read
 // once); see pipe_body.  MI355X, T = R = 25000, D = 96: 2.63 -> 2.59 ms (1.10 PFLOP/s), headline
 // step 8.70 -> 8.63 ms, emulated N=8 rank step 1.460 -> 1.449 ms (3 alternating runs each).
@@ -630,12 +612,17 @@ static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
   const int ncb = (a.T + 127) / 128;
   constexpr int LDS = ColsCfg<D>::NBUF * ColsCfg<D>::STAGE;
   constexpr int LDS2 = 2 * ColsCfg<D, 2>::STAGE;
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
-  else if (cols_nbuf() == 2 && bwd_prescale())
-    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2, true>), dim3(ncb * a.B * a.H), dim3(256), LDS2, st, a);
+  const dim3 grid(ncb * a.B * a.H);
+  if (a.prescaled) {
+    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1, 0, true>), grid, dim3(256), LDS, st, a);
+    else if (cols_nbuf() == 2) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2, true>), grid, dim3(256), LDS2, st, a);
+    else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 0, true>), grid, dim3(256), LDS, st, a);
+    return;
+  }
+  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
   else if (cols_nbuf() == 2)
-    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS2, st, a);
-  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), dim3(ncb * a.B * a.H), dim3(256), LDS, st, a);
+    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), grid, dim3(256), LDS2, st, a);
+  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
 }
 
 template <int DT, int D>
@@ -648,12 +635,16 @@ template <int DT, int D>
 static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
   constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-  else if (rows_pipe())
-    hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, false, true>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-  else if (bwd_prescale())
-    hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-  else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+  const dim3 grid(nrb * a.B * a.H * a.nsplit);
+  if (a.prescaled) {
+    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1, true>), grid, dim3(256), LDS, st, a);
+    else if (rows_pipe()) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true, true>), grid, dim3(256), LDS, st, a);
+    else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true>), grid, dim3(256), LDS, st, a);
+  } else {
+    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
+    else if (rows_pipe()) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, false, true>), grid, dim3(256), LDS, st, a);
+    else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
+  }
   if (a.nsplit > 1 && !a.force_partial) launch_rows_sum<DT, D>(a, st);
 }
 

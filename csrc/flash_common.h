@@ -70,28 +70,6 @@ __device__ __forceinline__ u32x4 acc_to_frag(const f32x16& x, int s) {
   return r;
 }
 
-// every 16-bit element of an operand fragment times c (fp32 math, one rounding)
-template <int DT>
-__device__ __forceinline__ u32x4 scale_frag(u32x4 x, float c) {
-  u32x4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t w = x[i];
-    float lo, hi;
-    if constexpr (DT == DT_BF16) {
-      lo = __builtin_bit_cast(float, w << 16);
-      hi = __builtin_bit_cast(float, w & 0xffff0000u);
-    } else {
-      typedef __attribute__((ext_vector_type(2))) _Float16 h2;
-      const h2 v = __builtin_bit_cast(h2, w);
-      lo = (float)v[0];
-      hi = (float)v[1];
-    }
-    r[i] = pack2<DT>(lo * c, hi * c);
-  }
-  return r;
-}
-
 // ---- LDS tile images -------------------------------------------------------------------
 // One layout serves both ways a tile is read: rows of IMG_ROW bytes (D = 32/64/96/128 ->
 // 64/192/192/320) whose 16-byte chunks are XOR-swizzled by (row >> 2) & 3.  Checked against

@@ -31,7 +31,7 @@
 namespace xdot {
 namespace fa {
 
-template <int DT, int D, int WPS = 2>
+template <int DT, int D, int WPS = 2, bool PS = false>
 __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
@@ -105,6 +105,15 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const float c2 = a.scale * LOG2E;
   const float NEG_INF = -__builtin_inff();
   float m_run = NEG_INF, l_run = 0.f;
+  // PS: K rows pre-multiplied by scale*log2 e on the host (FwdArgs::prescaled; one bf16
+  // rounding, the same buffer the backward reads) and every score chain seeded
+  // with -m (the running max it will be exponentiated against), so P = 2^acc with no per-score
+  // FMA.  m_seed is the m encoded in mseed; a (rare, deferred) max update corrects the pending
+  // tile by m_seed - m_new and re-seeds.
+  f32x16 mseed;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) mseed[r] = 0.f;
+  float m_seed = 0.f;
   f32x16 o[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i)
@@ -134,7 +143,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       const int tt = i / KS, ks = i % KS;
       u32x4 qn = qa;
       if (i + 1 < 2 * KS) qn = row_frag<D>(qs, ((i + 1) / KS) * 32, (i + 1) % KS, L);
-      s[tt] = mfma32<DT>::run(qa, kf[ks], ks == 0 ? f32x16{} : s[tt]);
+      s[tt] = mfma32<DT>::run(qa, kf[ks], ks == 0 ? (PS ? mseed : f32x16{}) : s[tt]);
       qa = qn;
     }
   };
@@ -161,9 +170,10 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
-    return pair_max(mx) * c2;
+    return PS ? pair_max(mx) + m_seed : pair_max(mx) * c2;
   };
-  auto rescale_to = [&](float mx) {
+  // s: the tile whose max is mx (exponentiated next; PS: corrected to the new m)
+  auto rescale_to = [&](float mx, f32x16 (&s)[2]) {
     const float m_new = fmaxf(m_run, mx);
     if (__any(m_new > m_run + RESCALE_LOG2)) {
       const float alpha = fast_exp2(m_run - ((m_new == NEG_INF) ? 0.f : m_new));
@@ -173,6 +183,17 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
       m_run = m_new;
+      if constexpr (PS) {
+        const float mu = (m_run == NEG_INF) ? 0.f : m_run;
+        const float corr = m_seed - mu;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[tt][r] += corr;
+        m_seed = mu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mseed[r] = -mu;
+      }
     }
   };
 
@@ -203,10 +224,10 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
           const int tt = i / KS, ks = i % KS;
           u32x4 q2 = q1;
           if (i + 2 < NA) q2 = row_frag<D>(nxt, ((i + 2) / KS) * 32, (i + 2) % KS, L);
-          sn[tt] = mfma32<DT>::run(q0, kf[ks], ks == 0 ? f32x16{} : sn[tt]);
+          sn[tt] = mfma32<DT>::run(q0, kf[ks], ks == 0 ? (PS ? mseed : f32x16{}) : sn[tt]);
 #pragma unroll
           for (int j = (i * 32) / NA; j < ((i + 1) * 32) / NA; ++j) {
-            sc[j >> 4][j & 15] = fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
+            sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
             if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -234,7 +255,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       }
       l_run += ls;
       if (flag_n != 0 || (kt + 2) * 64 > a.T) mask_tile(sn, kt + 1, flag_n, nxt);
-      rescale_to(row_max(sn));
+      rescale_to(row_max(sn), sn);
     } else {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
@@ -261,7 +282,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     flag_cur = f0;
     if (f0 != 1) s_tile(sv[0], smem);
     if (f0 != 0 || (kt_beg + 1) * 64 > a.T) mask_tile(sv[0], kt_beg, f0, smem);
-    rescale_to(row_max(sv[0]));
+    rescale_to(row_max(sv[0]), sv[0]);
   }
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -580,15 +601,21 @@ inline int fwd_rows_per_wave() {
 
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  if (fwd_rows_per_wave() == 64) {
+  if (fwd_rows_per_wave() == 64 && !a.prescaled) {  // the 64-row kernel has no pre-scaled form
     constexpr int LDS = 3 * Fwd64Cfg<D>::STAGE;
     const int nrb = (a.R + 255) / 256;
     hipLaunchKernelGGL((flash_fwd64_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
   } else {
     constexpr int LDS = 3 * RowsCfg<D>::STAGE;
     const int nrb = (a.R + 127) / 128;
-    if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-    else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
+    const dim3 grid(nrb * a.B * a.H * a.nsplit);
+    if (a.prescaled) {
+      if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1, true>), grid, dim3(256), LDS, st, a);
+      else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2, true>), grid, dim3(256), LDS, st, a);
+    } else {
+      if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
+      else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
+    }
   }
   if (a.nsplit > 1 && !a.force_partial) launch_combine<DT, D>(a, st);
 }

@@ -52,6 +52,7 @@ struct FwdArgs {
   float* lpart;            // (slots, B, H, R) partial LSE
   int sp0;                 // first partial slot of this launch (chunked launches)
   int force_partial;       // 1: write partials even with nsplit == 1 (no combine here)
+  int prescaled;           // 1: rows hold K * scale * log2(e) (xdot_prescale_rows_launch)
 };
 
 struct BwdArgs {
@@ -76,6 +77,7 @@ struct BwdArgs {
   float* dpart;            // (slots, B, R, H*D) fp32 partial row-side grads (nsplit > 1)
   int sp0;                 // first partial slot of this launch (chunked launches)
   int force_partial;       // 1: write partials even with nsplit == 1 (summed separately)
+  int prescaled;           // 1: rows hold K * scale * log2(e) (same buffer as the forward's)
 };
 
 }  // namespace fa
@@ -118,6 +120,9 @@ int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStr
 int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 // out (n elements, dtype dto) = Σ_s part[s] (fp32 partials, n % 4 == 0)
 int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int dto, hipStream_t st);
+// out = (16-bit) (x * (scale * log2 e)) elementwise, n % 8 == 0: the pre-scaled row side of the
+// flash kernels (the factor is formed in fp32 exactly as the kernels form it)
+int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, int dt, hipStream_t st);
 // rows per workgroup of the forward kernel (depends on XDOT_FWD_ROWS)
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments

@@ -48,7 +48,10 @@ CASES = [
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
-def test_flash_fwd_bwd(gpu, dt, case, mask_kind):
+@pytest.mark.parametrize("prescaled", [False, True])
+def test_flash_fwd_bwd(gpu, dt, case, mask_kind, prescaled):
+    """``prescaled``: the kernels read rows * scale * log2 e (flash.prescale, the module's
+    default) and seed their score accumulators; gradients are still those of the unscaled rows."""
     from xdot.ops import flash
 
     B, R, N, Rc, H, D = case
@@ -70,14 +73,16 @@ def test_flash_fwd_bwd(gpu, dt, case, mask_kind):
         mask = mask.to(gpu)
     scale = 1.0 / math.sqrt(D)
     mk = flash.prepare_mask(mask, B, R, T)
-    out, lse = flash.fwd(rows, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), mk, H, scale)
+    rk = flash.prescale(rows, scale) if prescaled else rows
+    out, lse = flash.fwd(rk, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), mk, H, scale, prescaled=prescaled)
     k, q, v, ref_o, ref_lse = _ref(rows, kc, vc, mask, H, scale)
     tol = 2e-2 if dt == torch.bfloat16 else 4e-3
     assert (out.float() - ref_o).abs().max().item() < tol * 4, "fwd out"
     assert (lse - ref_lse).abs().max().item() < 1e-2, "lse"
 
     do = torch.randn(B, R, C, generator=g).to(gpu, dt)
-    drows, dkc, dvc = flash.bwd(do, rows, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), out, lse, mk, H, scale)
+    drows, dkc, dvc = flash.bwd(do, rk, flash.gathered_to_btc(kc), flash.gathered_to_btc(vc), out, lse, mk, H, scale,
+                                prescaled=prescaled)
     dkc, dvc = flash.btc_to_rank_major(dkc, N), flash.btc_to_rank_major(dvc, N)
     ref_o.backward(do.float())
     dk_ref = k.grad.transpose(1, 2).reshape(B, R, C)
@@ -92,7 +97,8 @@ def test_flash_fwd_bwd(gpu, dt, case, mask_kind):
     assert rel(dvc, dv_ref) < 3e-2, "d cols (v)"
 
 
-def test_flash_fully_masked_row_nan(gpu):
+@pytest.mark.parametrize("prescaled", [False, True])
+def test_flash_fully_masked_row_nan(gpu, prescaled):
     from xdot.ops import flash
 
     B, R, N, Rc, H, D = 1, 64, 1, 64, 2, 64
@@ -101,7 +107,8 @@ def test_flash_fully_masked_row_nan(gpu):
     mask = torch.zeros(B, R, N * Rc, dtype=torch.bool, device=gpu)
     mask[0, 5] = True
     kb = flash.gathered_to_btc(kc)
-    out, lse = flash.fwd(rows, kb, kb, flash.prepare_mask(mask, B, R, N * Rc), H, 0.125)
+    rk = flash.prescale(rows, 0.125) if prescaled else rows
+    out, lse = flash.fwd(rk, kb, kb, flash.prepare_mask(mask, B, R, N * Rc), H, 0.125, prescaled=prescaled)
     assert torch.isnan(out[0, 5]).all()
     assert not torch.isnan(out[0, 4]).any()
 

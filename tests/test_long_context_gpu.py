@@ -28,9 +28,10 @@ def test_flash_long_context_sampled(gpu, R, T, masked):
         mask = (torch.arange(T, device=gpu).view(1, T) > 8 * ri).unsqueeze(0)
         mask[..., 0] = False
     mk = flash.prepare_mask(mask, 1, R, T)
-    out, lse = flash.fwd(rows, kc, vc, mk, H, scale)
-    dkv, delta = flash.bwd_cols(do, rows, kc, vc, out, lse, mk, H, scale)
-    drows = flash.bwd_rows(do, rows, kc, vc, lse, delta, mk, H, scale)
+    rk = flash.prescale(rows, scale)  # the module's default path (XDOT_PRESCALE)
+    out, lse = flash.fwd(rk, kc, vc, mk, H, scale, prescaled=True)
+    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=True)
+    drows = flash.bwd_rows(do, rk, kc, vc, lse, delta, mk, H, scale, prescaled=True)
 
     K, V, Q, dO = kc[0].float(), vc[0].float(), rows[0].float(), do[0].float()
     ri = torch.randint(0, R, (32,), device=gpu, generator=g)

@@ -105,13 +105,23 @@ def _mask_args(mk: Optional[PackedMask]):
     return (mk.bits, mk.flags) if mk is not None else (None, None)
 
 
+def prescale(rows: torch.Tensor, scale: float) -> torch.Tensor:
+    """``rows * (scale * log2 e)`` in the input dtype (one rounding), the form the kernels take with
+    ``prescaled=True``: their score accumulators are then seeded with the row max / LSE and the
+    probabilities are ``2^acc`` with no per-score FMA.  Forward and backward must see the SAME
+    pre-scaled buffer."""
+    return _ext.ops().flash_prescale(rows.contiguous(), float(scale))
+
+
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
-        scale: float, nsplit: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        scale: float, nsplit: int = 0, prescaled: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """-> (out (B, R, H*D) in rows.dtype, lse (B, H, R) fp32 natural log).
 
-    ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU)."""
+    ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU).
+    ``prescaled``: ``rows`` is :func:`prescale` output."""
     bits, flags = _mask_args(mk)
-    return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit))
+    return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit),
+                                bool(prescaled))
 
 
 def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
@@ -120,7 +130,7 @@ def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
 
 
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
-             delta: Optional[torch.Tensor] = None, fp32_out: bool = True):
+             delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False):
     """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
     ``delta`` (from :func:`bwd_delta`) is computed here when not given.  The grads are fp32
@@ -128,21 +138,25 @@ def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, sca
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
-                                     bool(fp32_out))
+                                     bool(fp32_out), bool(prescaled))
 
 
-def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0):
+def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0,
+             prescaled: bool = False):
     """Row-side grad (B, R, H*D) in rows.dtype."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
-                                     int(nsplit))
+                                     int(nsplit), bool(prescaled))
 
 
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,
-        lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float):
-    """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads)."""
-    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale)
-    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale)
+        lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float, prescaled: bool = False):
+    """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads).
+
+    ``prescaled``: ``rows`` is :func:`prescale` output (the buffer the forward read); d_rows is
+    still the gradient of the unscaled rows."""
+    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale, prescaled=prescaled)
+    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale, prescaled=prescaled)
     C = rows.shape[-1]
     return drows, dkv[..., :C], dkv[..., C:]

@@ -202,9 +202,16 @@ class SeqParallelAttention(torch.autograd.Function):
         if pending is None:
             pending = _PendingGather(comm, qv, _row_chunks(n, qv.shape[1], use_hip))
         chunks = pending.chunks
+        prescaled = False
         if use_hip:
             from ..ops import flash
 
+            # the row side pre-multiplied by scale*log2 e once (XDOT_PRESCALE, default on): the
+            # forward and both backward kernels read this same buffer and seed their score
+            # accumulators instead of scaling every score (saved in place of k for backward)
+            prescaled = FLAGS.prescale and (k.numel() % 8 == 0)
+            if prescaled:
+                k = flash.prescale(k, scale)
             # masks are packed per chunk while the gathers are in flight (or were packed on a
             # side stream before the projections: flash.PendingMask)
             mks = []
@@ -222,7 +229,7 @@ class SeqParallelAttention(torch.autograd.Function):
                 mks.append(flash.prepare_mask(mc, B, R, n * rc))
             if len(chunks) == 1:
                 qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
-                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mks[0], H, scale)
+                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mks[0], H, scale, prescaled=prescaled)
                 bufs = [qvg]
             else:
                 ops = _ext.ops()
@@ -235,7 +242,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     bufs.append(g)
                     bits, flags = (mks[c].bits, mks[c].flags) if mks[c] is not None else (None, None)
                     ops.flash_fwd_partial(k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                          float(scale), opart, lpart, c * ns, ns)
+                                          float(scale), opart, lpart, c * ns, ns, prescaled)
                 o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
         else:
             mask = getattr(mask, "raw", mask)
@@ -245,6 +252,7 @@ class SeqParallelAttention(torch.autograd.Function):
             bufs = [qvg]
         ctx.save_for_backward(k, o, lse, *bufs)
         ctx.mks, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, chunks, H, scale, comm, use_hip
+        ctx.prescaled = prescaled
         return o
 
     @staticmethod
@@ -289,7 +297,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
                     # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
                     dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[c], H, scale, delta,
-                                            fp32_out=FLAGS.grad_fp32)
+                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
                     h, oc = reduce_async(flash.btc_to_rank_major(dkv, n), None if dqv is None else dqv[:, r0:r0 + rc])
                     handles.append(h)
                     outs.append(oc)
@@ -297,7 +305,8 @@ class SeqParallelAttention(torch.autograd.Function):
             delta.record_stream(cur)
             if len(chunks) == 1:
                 g = bufs[0]
-                dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, ctx.mks[0], H, scale)
+                dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, ctx.mks[0], H, scale,
+                                    prescaled=ctx.prescaled)
             else:
                 ops = _ext.ops()
                 ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))
@@ -307,7 +316,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     mk = ctx.mks[c]
                     bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                     ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                               flags, int(H), float(scale), dpart, c * ns, ns)
+                                               flags, int(H), float(scale), dpart, c * ns, ns, ctx.prescaled)
                 dk = ops.flash_bwd_rows_sum(dpart, int(H), k)
             cur.wait_stream(hi)
             for oc in outs:

@@ -22,12 +22,11 @@
                                projection GEMMs (default off: no gain measured at N=1, 9.23-9.29
                                vs 9.23-9.25 ms; with several ranks packing already overlaps the
                                all-gather)
-``XDOT_BWD_PRESCALE``          ``1``: flash backward kernels multiply the register-resident score
-                               operand by scale*log2 e once and seed the score accumulator
-                               with -LSE (one FMA less per score element; one extra bf16
-                               rounding of that operand).  Off: measured +1-1.5 % per kernel
-                               (cols 4.07->4.03 ms, rows 2.79->2.75 ms at T=R=25000), within
-                               box noise on the step
+``XDOT_PRESCALE``              ``0``: flash kernels scale every score by scale*log2 e (default 1:
+                               the row side is pre-multiplied once per forward — one bf16
+                               rounding, the same buffer for forward and backward — and the
+                               score accumulators are seeded with the row max / LSE; forward
+                               2.11 -> 1.98 ms at T=R=25000)
 ``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
                                row kernel (default 1: VALU of one sub-tile issues between the
                                next sub-tile's MFMAs; 1.5 % faster kernel)
@@ -60,6 +59,7 @@ class _Flags:
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
         self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
         self.mask_async = _flag("XDOT_MASK_ASYNC")
+        self.prescale = _flag("XDOT_PRESCALE", default="1")
 
 
 FLAGS = _Flags()
