@@ -19,8 +19,8 @@
 namespace xdot {
 
 // One wave per 64-row x 128-column block of one batch.  The wave reads the block with
-// coalesced 8-byte loads (8 lanes cover 64 contiguous bytes of a row; rows only need 8-byte
-// alignment, e.g. T = 25000), packs every 8 bool bytes to one byte (4 bytes -> 4 bits with one
+// coalesced 8-byte lane pieces (8 lanes cover 64 contiguous bytes of a row; 8-byte loads when
+// rows are 8-byte aligned, e.g. T = 25000, 4-byte or byte loads otherwise), packs every 8 bool bytes to one byte (4 bytes -> 4 bits with one
 // 32-bit multiply), regroups the bytes per row through 1 KiB of LDS so lane i holds row i's
 // two 64-bit words (a row-per-lane read of the mask was TA-bound: 64 cache lines per load
 // instruction), stores them (bits), turns each set
@@ -37,7 +37,7 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x) { return (x * 0x10204080u)
 __global__ __launch_bounds__(256) void mask_pack_kernel(const uint8_t* __restrict__ m, uint64_t* __restrict__ bits,
                                                          uint64_t* __restrict__ bt, uint8_t* __restrict__ flags,
                                                          int B, int R, int T, int NKT, int NKT4, int NRT, int Tpad,
-                                                         int KT_ALL, bool vec8) {
+                                                         int KT_ALL, int va) {
   const int lane = threadIdx.x & 63;
   const int KT2 = (KT_ALL + 1) / 2;
   const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void mask_pack_kernel(const uint8_t* __restric
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][64 * 16];  // per wave: 64 rows x 128 bits
   uint8_t* sw = stage[threadIdx.x >> 6];
   const int c0 = kt0 * 64;
-  if (vec8 && kt0 < NKT && c0 + 128 <= T) {
+  if (kt0 < NKT && c0 + 128 <= T) {
     // coalesced: instruction (i, j) reads rows 8i..8i+7, bytes 64j..64j+63 of the block
     // (8 lanes x 8 B contiguous per row); each lane packs its 8 bytes to one byte in LDS
     uint64_t x[16];
@@ -61,7 +61,20 @@ __global__ __launch_bounds__(256) void mask_pack_kernel(const uint8_t* __restric
       const int rr = rt * 64 + 8 * i + lr;
       const uint8_t* p = m + ((int64_t)b * R + min(rr, R - 1)) * T + c0 + lc;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) x[2 * i + j] = rr < R ? *reinterpret_cast<const uint64_t*>(p + 64 * j) : 0ull;
+      for (int j = 0; j < 2; ++j) {
+        const uint8_t* q = p + 64 * j;
+        uint64_t v;
+        if (va == 8) {
+          v = *reinterpret_cast<const uint64_t*>(q);
+        } else if (va == 4) {  // rows 4-byte aligned (T % 8 == 4, e.g. T = 12500)
+          v = (uint64_t)*reinterpret_cast<const uint32_t*>(q) | ((uint64_t)*reinterpret_cast<const uint32_t*>(q + 4) << 32);
+        } else {               // odd row strides: byte loads, still 64 contiguous bytes per 8 lanes
+          v = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v |= (uint64_t)q[e] << (8 * e);
+        }
+        x[2 * i + j] = rr < R ? v : 0ull;
+      }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -125,10 +138,13 @@ extern "C" int xdot_mask_pack_launch(const uint8_t* mask, uint64_t* bits, uint64
   using namespace xdot;
   const int NKT = (T + 63) / 64, NKT4 = (NKT + 3) & ~3, NRT = (R + 63) / 64, Tpad = (T + 127) / 128 * 128;
   const int KT_ALL = max(NKT4, Tpad / 64);
-  const bool vec8 = (T % 8 == 0) && ((reinterpret_cast<uintptr_t>(mask) & 7) == 0);
+  // widest load every row start satisfies (the kernel reads each row's 128-column block as
+  // 8-byte lane pieces; narrower alignment splits them, the access pattern stays coalesced)
+  const uintptr_t base = reinterpret_cast<uintptr_t>(mask);
+  const int va = (T % 8 == 0 && (base & 7) == 0) ? 8 : (T % 4 == 0 && (base & 3) == 0) ? 4 : 1;
   const int64_t nblk = (int64_t)B * NRT * ((KT_ALL + 1) / 2);
   if (nblk == 0) return 0;
   hipLaunchKernelGGL(mask_pack_kernel, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, mask, bits, bt, flags, B, R, T,
-                     NKT, NKT4, NRT, Tpad, KT_ALL, vec8);
+                     NKT, NKT4, NRT, Tpad, KT_ALL, va);
   return 0;
 }

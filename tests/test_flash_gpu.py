@@ -129,9 +129,11 @@ def test_mask_pack_flags(gpu):
     assert bits[1, 1, 3].item() == (1 << (100 - 64))
 
 
-@pytest.mark.parametrize("shape", [(2, 70, 150), (1, 200, 1000), (1, 64, 128)])
+@pytest.mark.parametrize("shape", [(2, 70, 150), (1, 200, 1000), (1, 64, 128), (1, 100, 300), (2, 70, 1501),
+                                   (1, 130, 12500)])
 def test_mask_pack_column_major(gpu, shape):
-    """bits_t (B, ceil(R/64), Tpad): bit i of word (b, rt, t) == mask[b, 64*rt + i, t]."""
+    """bits_t (B, ceil(R/64), Tpad): bit i of word (b, rt, t) == mask[b, 64*rt + i, t]; and the
+    row-major bits (B, NKT, R).  Row strides 8-, 4- and 1-byte aligned (T = 1000 / 300 / 1501)."""
     from xdot.ops import flash
 
     B, R, T = shape
@@ -146,6 +148,12 @@ def test_mask_pack_column_major(gpu, shape):
     ref = ref.view(B, NRT, 64, Tpad)
     got = torch.stack([(bt >> i) & 1 for i in range(64)], dim=2).bool()   # (B, NRT, 64, Tpad)
     assert torch.equal(got, ref)
+    NKT = (T + 63) // 64
+    bits = mk.bits.cpu().view(torch.int64)                                # (B, NKT, R)
+    rowbits = torch.stack([(bits >> i) & 1 for i in range(64)], dim=-1).bool()  # (B, NKT, R, 64)
+    refr = torch.zeros(B, R, NKT * 64, dtype=torch.bool)
+    refr[..., :T] = mask
+    assert torch.equal(rowbits.permute(0, 2, 1, 3).reshape(B, R, NKT * 64), refr)
 
 
 @pytest.mark.parametrize("nsplit", [2, 5])

@@ -105,12 +105,6 @@ class _PendingGather:
         return [self.wait(c) for c in range(len(self.chunks))]
 
 
-def _chunk_columns(n: int, R: int, r0: int, rc: int, device) -> Tensor:
-    """global columns of a gathered chunk, in its rank-major order: j*R + r0 + i"""
-    j = torch.arange(n, device=device).view(n, 1) * R
-    return (j + r0 + torch.arange(rc, device=device).view(1, rc)).reshape(-1)
-
-
 def _as_global(g: Tensor) -> Tensor:
     """(N, B, R, C) -> (B, T, C) view/copy for the torch reference path."""
     n, B, R, C = g.shape
@@ -225,7 +219,9 @@ class SeqParallelAttention(torch.autograd.Function):
                 if mask is None:
                     mks.append(None)
                     continue
-                mc = mask if len(chunks) == 1 else mask.index_select(2, _chunk_columns(n, R, r0, rc, mask.device))
+                # chunk columns j*R + r0 + i: a strided slice per source rank (index_select on the
+                # last dim of a (B, R, T) bool tensor is a slow gather)
+                mc = mask if len(chunks) == 1 else mask.view(B, R, n, R)[..., r0:r0 + rc].reshape(B, R, n * rc)
                 mks.append(flash.prepare_mask(mc, B, R, n * rc))
             if len(chunks) == 1:
                 qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
