@@ -15,9 +15,10 @@
                                the bf16/fp16 compute dtype in the kernel, half the bytes)
 ``XDOT_ROCTX``                 ``1``: roctx ranges around every native op (rocprofv3 markers)
 ``XDOT_GATHER_CHUNKS``         row chunks of the fused attention's all-gather / reduce-scatter
-                               pipeline with several ranks (default 1 = one collective each; 2+
-                               overlaps them with the kernels at ~0.2 ms extra compute per
-                               8-rank step: worth it only on a slow interconnect)
+                               pipeline with several ranks (default 1 = one collective each; 2
+                               overlaps half the gather with the kernels at +0.32 / +0.23 /
+                               +0.10 ms of compute per step at N = 2 / 4 / 8 (emulated, T=25000),
+                               about what it hides over xGMI: worth it on a slower interconnect)
 ``XDOT_MASK_ASYNC``            ``1``: pack the attention mask on a side stream, overlapping the
                                projection GEMMs (default off: no gain measured at N=1, 9.23-9.29
                                vs 9.23-9.25 ms; with several ranks packing already overlaps the
