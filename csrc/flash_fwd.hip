@@ -84,22 +84,27 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const int NRB32 = (a.R + 31) / 32;
   const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
   const int fn = min(4, NRB32 - rb * 4);
-  auto issue_q = [&](int kt) {
-    char* st = smem + ((kt - kt_beg) % 3) * CF::STAGE;
-    const int64_t t0 = (int64_t)kt * 64;
-    dma.issue(kcb + t0 * ldb, ldb, a.T - 1 - (int)t0, st, wave);  // columns past T re-read T-1 (masked)
+  // Q and V tiles are issued strictly in order: running byte offsets (no per-tile 64-bit
+  // products) and ring stages that are compile-time constants at every call site
+  int64_t q_off = (int64_t)kt_beg * 64 * ldb, v_off = q_off;
+  const uint64_t* mw_next = mwg ? mwg + (int64_t)kt_beg * a.R : nullptr;
+  auto issue_q = [&](int kt, auto stc) {
+    char* st = smem + decltype(stc)::value * CF::STAGE;
+    dma.issue(kcb + q_off, ldb, a.T - 1 - kt * 64, st, wave);  // columns past T re-read T-1 (masked)
+    q_off += (int64_t)64 * ldb;
     if (mwg) {
-      glds4(mwg + (int64_t)kt * a.R, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      glds4(mw_next, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+      mw_next += a.R;
       glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
     } else {  // same DMA count with or without a mask
       glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
       glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
     }
   };
-  auto issue_v = [&](int kt) {
-    char* st = smem + ((kt - kt_beg) % 3) * CF::STAGE;
-    const int64_t t0 = (int64_t)kt * 64;
-    dma.issue(vcb + t0 * ldb, ldb, a.T - 1 - (int)t0, st + IMG, wave);
+  auto issue_v = [&](int kt, auto stc) {
+    char* st = smem + decltype(stc)::value * CF::STAGE;
+    dma.issue(vcb + v_off, ldb, a.T - 1 - kt * 64, st + IMG, wave);
+    v_off += (int64_t)64 * ldb;
   };
 
   const float c2 = a.scale * LOG2E;
@@ -203,8 +208,8 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     f32x16 (&sc)[2] = sv[PAR];
     f32x16 (&sn)[2] = sv[PAR ^ 1];
     const bool dq = kt + 3 < kt_end, dv = kt + 2 < kt_end;
-    if (dq) issue_q(kt + 3);
-    if (dv) issue_v(kt + 2);
+    if (dq) issue_q(kt + 3, std::integral_constant<int, BUF>{});            // stage (BUF + 3) % 3
+    if (dv) issue_v(kt + 2, std::integral_constant<int, (BUF + 2) % 3>{});
     const char* cur = smem + BUF * CF::STAGE;             // V(kt)
     const char* nxt = smem + ((BUF + 1) % 3) * CF::STAGE; // Q(kt+1), mask words (kt+1)
     // flag(kt) was read one iteration ago (its stage is being refilled with Q(kt+3) now)
@@ -270,11 +275,13 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   };
 
   if (kt_beg < kt_end) {
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      if (kt_beg + t < kt_end) issue_q(kt_beg + t);
-      if (t < 2 && kt_beg + t < kt_end) issue_v(kt_beg + t);
+    issue_q(kt_beg, std::integral_constant<int, 0>{});
+    issue_v(kt_beg, std::integral_constant<int, 0>{});
+    if (kt_beg + 1 < kt_end) {
+      issue_q(kt_beg + 1, std::integral_constant<int, 1>{});
+      issue_v(kt_beg + 1, std::integral_constant<int, 1>{});
     }
+    if (kt_beg + 2 < kt_end) issue_q(kt_beg + 2, std::integral_constant<int, 2>{});
     wait_vm<0>();
     raw_barrier();
     // prologue: S of the first tile, masked, its max sets m
