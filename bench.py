@@ -38,7 +38,7 @@ def parse(argv=None):
     ap.add_argument("--heads", type=int, default=8)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
-    ap.add_argument("--impl", default="auto", choices=["auto", "flash", "materialized"])
+    ap.add_argument("--impl", default="auto", choices=["auto", "flash", "materialized", "ring"])
     ap.add_argument("--offset", type=int, default=None)
     ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random"])
     ap.add_argument("--no-optim", action="store_true", help="(diagnostic) skip the optimizer step")

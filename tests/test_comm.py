@@ -59,6 +59,9 @@ def test_thread_comm_collectives(ws):
         c.broadcast(b, src=1)
         assert b.item() == 11.0
         assert c.all_gather_object(r * 2) == [2 * j for j in range(ws)]
+        got = torch.empty(3)
+        c.sendrecv(torch.full((3,), float(r)), got, (r + 1) % ws, (r - 1) % ws)  # one ring hop
+        assert torch.all(got == (r - 1) % ws)
         return r
 
     assert C.ThreadGroup(ws).run(body) == list(range(ws))
@@ -85,6 +88,9 @@ def _gloo_collectives(rank, ws):
         rs = torch.empty(5, dtype=dt)
         c.reduce_scatter(rs, torch.ones(ws * 5, dtype=dt))
         assert torch.all(rs.float() == ws)
+        got = torch.empty(5, dtype=dt)  # one ring hop (isend/irecv pair)
+        c.sendrecv(torch.full((5,), rank + 1).to(dt), got, (rank + 1) % ws, (rank - 1) % ws, async_op=True).wait()
+        assert torch.all(got.float() == (rank - 1) % ws + 1)
     # the shim's comm functions resolve to the same communicator
     from distributed_dot_product.utils.comm import get_rank, get_world_size, is_main_process, synchronize
 

@@ -58,13 +58,14 @@ def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, t
 
 
 @pytest.mark.parametrize("heads", [1, 4])
-@pytest.mark.parametrize("impl", ["materialized", "flash"])
+@pytest.mark.parametrize("impl", ["materialized", "flash", "ring"])
 def test_module_parity_gloo(heads, impl):
     run_gloo(_module_parity, 2, heads, impl, 32, True)
 
 
 @pytest.mark.parametrize("ws", [1, 3])
-@pytest.mark.parametrize("impl,offset", [("materialized", 5), ("materialized", None), ("flash", None)])
+@pytest.mark.parametrize("impl,offset", [("materialized", 5), ("materialized", None), ("flash", None),
+                                         ("ring", None)])
 def test_module_parity_threads(ws, impl, offset):
     from xdot.utils.comm import ThreadGroup
 
@@ -79,15 +80,16 @@ def test_module_unmasked_float32_reference_config():
                                                 dtype=torch.float32, tol=1e-5))
 
 
-def test_module_bf16_gloo():
-    """bf16 end to end over real gloo collectives (half-precision gathers / reductions)."""
-    run_gloo(_module_parity, 2, 4, "flash", None, True, torch.bfloat16, 0.08)
+@pytest.mark.parametrize("impl", ["flash", "ring"])
+def test_module_bf16_gloo(impl):
+    """bf16 end to end over real gloo collectives (half-precision gathers / reductions / ring hops)."""
+    run_gloo(_module_parity, 2, 4, impl, None, True, torch.bfloat16, 0.08)
 
 
 def test_fully_masked_row_gives_nan():
     from xdot import DistributedDotProductAttn
 
-    for impl in ("materialized", "flash"):
+    for impl in ("materialized", "flash", "ring"):
         m = DistributedDotProductAttn(16, num_heads=2, impl=impl)
         x = torch.randn(1, 4, 16)
         mask = torch.zeros(1, 4, 4, dtype=torch.bool)

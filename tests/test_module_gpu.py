@@ -24,6 +24,8 @@ def _module_case(rank, ws, impl, masked):
     g = torch.Generator(device="cpu").manual_seed(3)
     x_full = torch.randn(1, T, D, generator=g).to(dev, torch.bfloat16)
     mask_full = (torch.rand(1, T, T, generator=g) < 0.3) if masked else torch.zeros(1, T, T, dtype=torch.bool)
+    if masked == "block":  # the first quarter of the rows sees nothing of the second half
+        mask_full[:, :T // 4, T // 2:] = True    # (whole ring blocks fully masked for those rows)
     mask_full[..., torch.arange(T), torch.arange(T)] = False
     mask_full = mask_full.to(dev)
     ref = xdot.DistributedDotProductAttn(D, num_heads=H, distributed=False, impl="materialized").to(dev)
@@ -45,7 +47,7 @@ def _module_case(rank, ws, impl, masked):
     assert (gx.float() - xf.grad).abs().max().item() <= 5e-2 * gs
 
 
-@pytest.mark.parametrize("impl", ["materialized", "flash"])
+@pytest.mark.parametrize("impl", ["materialized", "flash", "ring"])
 @pytest.mark.parametrize("masked", [False, True])
 def test_module_single_rank(gpu, impl, masked):
     from xdot.utils.comm import LocalComm, use_comm
@@ -54,10 +56,16 @@ def test_module_single_rank(gpu, impl, masked):
         _module_case(0, 1, impl, masked)
 
 
-@pytest.mark.parametrize("impl", ["materialized", "flash"])
+@pytest.mark.parametrize("impl", ["materialized", "flash", "ring"])
 @pytest.mark.parametrize("ws", [2, 4])
 def test_module_multi_rank(gpu, impl, ws):
     run_gloo(_module_case, ws, impl, True, timeout=400)
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_module_ring_block_masked(gpu, ws):
+    """Ring path: blocks that are fully masked for some rows (their split partials are empty)."""
+    run_gloo(_module_case, ws, "ring", "block", timeout=400)
 
 
 def test_flash_is_default_on_gpu_bf16(gpu):

@@ -6,7 +6,7 @@ Same constructor, forward signature, math and submodule names as the reference
 **``keys`` is the local/row side and ``queries`` the gathered side**, ``S[mask] = -inf``,
 ``P = softmax(S)``, ``O = P·V``, ``out = composition(merge(O))``.
 
-Two execution paths, chosen by ``impl``:
+Three execution paths, chosen by ``impl``:
 
 ``'materialized'`` — the reference's structure, op for op: ``RightTransposeMultiplication``
     → fused scale+mask+softmax kernel → ``FullMultiplication``.  Scores (B, H, T/N, T) are
@@ -15,6 +15,9 @@ Two execution paths, chosen by ``impl``:
     all-gather once, MFMA flash-attention kernels with online softmax (scores never exist in
     HBM), backward by recomputation with reduce-scatter of the gathered-side gradients.
     Required for long context (T=200000: materialised bf16 scores would be 80 GB per rank).
+``'ring'`` — the same kernels fed by a ring of point-to-point RCCL hops
+    (:mod:`xdot.parallel.ring`): the gathered side travels one rank-block at a time and is
+    never resident in full; its gradient accumulator rides the ring back (no reduce-scatter).
 ``'auto'`` (default) — ``'flash'`` for bf16/fp16 GPU tensors with a supported head dim, else
     ``'materialized'``.
 
@@ -52,8 +55,8 @@ class DistributedDotProductAttn(nn.Module):
         query_dim = query_dim if query_dim is not None else key_dim
         if value_dim % num_heads != 0:
             raise ValueError(f"value_dim {value_dim} not divisible by num_heads {num_heads}")
-        if impl not in ("auto", "flash", "materialized"):
-            raise ValueError(f"impl must be auto|flash|materialized, got {impl!r}")
+        if impl not in ("auto", "flash", "materialized", "ring"):
+            raise ValueError(f"impl must be auto|flash|materialized|ring, got {impl!r}")
         self.num_heads = num_heads
         self.value_dim = value_dim
         self.offset = offset
@@ -91,6 +94,14 @@ class DistributedDotProductAttn(nn.Module):
             pending = start_gather(qv, comm)
             k = self._proj(self.keys, keys)
             o = seq_parallel_attention_packed(k, qv, attn_mask, self.num_heads, scale, comm=comm, pending=pending)
+            return self._proj(self.composition, o)
+        if self._pick_impl(keys) == "ring":
+            from ..parallel.ring import ring_attention_packed
+
+            comm = (self.comm or _comm.get_comm()) if self.distributed else _comm.LocalComm()
+            qv = self._project_qv(queries, values)
+            k = self._proj(self.keys, keys)
+            o = ring_attention_packed(k, qv, attn_mask, self.num_heads, scale, comm=comm)
             return self._proj(self.composition, o)
         k = self.keys(keys)
         q = self.queries(queries)

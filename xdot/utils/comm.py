@@ -53,7 +53,8 @@ class Handle:
 
     def wait(self):
         if self._work is not None:
-            self._work.wait()
+            for w in (self._work if isinstance(self._work, (list, tuple)) else (self._work,)):
+                w.wait()
             self._work = None
         if self._post is not None:
             self._post()
@@ -86,6 +87,12 @@ class Communicator:
         raise NotImplementedError
 
     def barrier(self) -> None:
+        raise NotImplementedError
+
+    def sendrecv(self, send: torch.Tensor, recv: torch.Tensor, dst: int, src: int, async_op: bool = False):
+        """Point-to-point exchange: ``send`` goes to rank ``dst`` while ``recv`` (same shape and
+        dtype on every rank) is filled from rank ``src``.  Every rank of a ring calls it in the
+        same order (one hop of :mod:`xdot.parallel.ring`)."""
         raise NotImplementedError
 
     @property
@@ -131,6 +138,12 @@ class LocalComm(Communicator):
 
     def barrier(self):
         return None
+
+    def sendrecv(self, send, recv, dst, src, async_op=False):
+        # world size 1: the ring hop is to self (EmulatedComm: a device copy stands in for the link)
+        if recv.data_ptr() != send.data_ptr():
+            recv.copy_(send)
+        return Handle(out=recv) if async_op else None
 
 
 class EmulatedComm(LocalComm):
@@ -248,6 +261,30 @@ class TorchDistComm(Communicator):
 
     def barrier(self):
         dist.barrier(group=self.group)
+
+    def _global(self, r: int) -> int:
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def sendrecv(self, send, recv, dst, src, async_op=False):
+        if self._staged(send, recv):
+            c = torch.empty(recv.shape, dtype=recv.dtype)
+            self.sendrecv(send.detach().cpu().contiguous(), c, dst, src)
+            recv.copy_(c)
+            return Handle(out=recv) if async_op else None
+        send = send.contiguous()
+        if self._backend == "nccl":
+            # one RCCL group: the send and the receive of a ring hop progress together on the
+            # collective stream; wait() orders the caller's stream after both
+            works = dist.batch_isend_irecv([dist.P2POp(dist.isend, send, self._global(dst), self.group),
+                                            dist.P2POp(dist.irecv, recv, self._global(src), self.group)])
+        else:
+            works = [dist.isend(send, self._global(dst), group=self.group),
+                     dist.irecv(recv, self._global(src), group=self.group)]
+        h = Handle(list(works), recv)
+        if async_op:
+            return h
+        h.wait()
+        return None
 
 
 # ----------------------------------------------------------------------------------------
@@ -372,6 +409,12 @@ class ThreadComm(Communicator):
 
     def barrier(self):
         self.g._barrier.wait()
+
+    def sendrecv(self, send, recv, dst, src, async_op=False):
+        parts = self._exchange(send.contiguous())
+        recv.copy_(parts[src])
+        self._done(recv)
+        return Handle(out=recv) if async_op else None
 
 
 # ----------------------------------------------------------------------------------------
