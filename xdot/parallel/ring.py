@@ -184,7 +184,13 @@ class RingAttention(torch.autograd.Function):
         if ctx.use_hip:
             from ..ops import flash
 
+            from .attention import _side_stream
+
             ops = _ext.ops()
+            cur = torch.cuda.current_stream(do.device)
+            ov = FLAGS.ring_overlap
+            two = ov not in ("0", "false", "off", "no") and (ov != "auto" or -(-R // 128) * B * H >= 1024)
+            hi = _side_stream(do.device) if two else cur  # XDOT_RING_OVERLAP (utils/env.py)
             delta = flash.bwd_delta(do, o, H)
             nsr = int(ops.flash_splits(B, R, R, H, True))
             dpart = torch.empty(n * nsr, B, R, C, dtype=torch.float32, device=k.device)
@@ -197,11 +203,17 @@ class RingAttention(torch.autograd.Function):
             g = ring.cur
             mk = ctx.mks[s]
             if ctx.use_hip:
+                # one block's gathered-side kernel fills only R/64·H workgroups: it runs on the
+                # high-priority side stream, concurrently with the row-side partial here
+                hi.wait_stream(cur)
+                with torch.cuda.stream(hi):
+                    contrib, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mk, H, scale, delta,
+                                                fp32_out=True, prescaled=ctx.prescaled)
                 bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                 ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
                                            flags, int(H), float(scale), dpart, s * nsr, nsr, ctx.prescaled)
-                contrib, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mk, H, scale, delta,
-                                            fp32_out=True, prescaled=ctx.prescaled)
+                cur.wait_stream(hi)
+                contrib.record_stream(cur)
             else:
                 dkb, contrib = _ref_block_bwd(do, k, g, lse, delta, mk, H, scale)
                 dk += dkb

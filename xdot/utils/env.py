@@ -28,6 +28,11 @@
                                rounding, the same buffer for forward and backward — and the
                                score accumulators are seeded with the row max / LSE; forward
                                2.11 -> 1.98 ms at T=R=25000)
+``XDOT_RING_OVERLAP``          ring attention backward: ``1`` runs each block's gathered-side and
+                               row-side kernels on two streams, ``0`` on one; default ``auto``:
+                               two streams when a block has >= 1024 row tiles of 128 x heads
+                               (measured, 1x MI355X, T=25000: N=1 9.21 -> 8.71 ms with two
+                               streams, emulated N=8 rank 2.46 -> 2.63 ms, i.e. worse)
 ``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
                                row kernel (default 1: VALU of one sub-tile issues between the
                                next sub-tile's MFMAs; 1.5 % faster kernel)
@@ -61,6 +66,7 @@ class _Flags:
         self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.prescale = _flag("XDOT_PRESCALE", default="1")
+        self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
 
 
 FLAGS = _Flags()
