@@ -60,10 +60,12 @@ def test_bench_contract_cpu():
     assert "synthetic" in r["data"]
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("impl", ["auto", "ring"])
+def test_bench_two_ranks_gloo(impl):
     """The driver's N>1 launch line, on the CPU over gloo: ONE JSON line, from rank 0."""
     out = _run(_torchrun(2) + ["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--dtype", "fp32",
-                               "--seq-len", "128", "--dim", "64", "--heads", "4", "--steps", "2", "--warmup", "1"])
+                               "--seq-len", "128", "--dim", "64", "--heads", "4", "--steps", "2", "--warmup", "1",
+                               "--impl", impl])
     recs = _json_lines(out)
     assert len(recs) == 1, out
     assert recs[0]["n_gpus"] == 2 and recs[0]["config"]["parallelism"] == "sp2"
