@@ -203,8 +203,9 @@ class RingAttention(torch.autograd.Function):
             g = ring.cur
             mk = ctx.mks[s]
             if ctx.use_hip:
-                # one block's gathered-side kernel fills only R/64·H workgroups: it runs on the
-                # high-priority side stream, concurrently with the row-side partial here
+                # the gathered-side kernel runs on the high-priority side stream, concurrently
+                # with the row-side partial here, when a block is big enough for that to pay
+                # (``hi is cur`` otherwise)
                 hi.wait_stream(cur)
                 with torch.cuda.stream(hi):
                     contrib, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mk, H, scale, delta,
