@@ -20,9 +20,9 @@
                                +0.10 ms of compute per step at N = 2 / 4 / 8 (emulated, T=25000),
                                about what it hides over xGMI: worth it on a slower interconnect)
 ``XDOT_MASK_ASYNC``            ``1``: pack the attention mask on a side stream, overlapping the
-                               projection GEMMs (default off: no gain measured at N=1, 9.23-9.29
-                               vs 9.23-9.25 ms; with several ranks packing already overlaps the
-                               all-gather)
+                               projection GEMMs (default off: neutral at N=1, 1.7 % slower at the
+                               emulated N=8 rank, profiles/r1_s7_mask_async_ab.md; with several
+                               ranks packing already overlaps the all-gather)
 ``XDOT_PRESCALE``              ``0``: flash kernels scale every score by scale*log2 e (default 1:
                                the row side is pre-multiplied once per forward — one bf16
                                rounding, the same buffer for forward and backward — and the
