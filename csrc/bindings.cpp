@@ -569,6 +569,47 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd_combine(const at::Tensor& opart, co
   return {out, lse};
 }
 
+// merge all slots of opart / lpart into slot 0 in fp32 (the running partial of the ring
+// forward: two slots of memory per block instead of one per ring step).  O is merged in place
+// (each element is read and written by one thread); the merged LSE goes to lrun (lpart slot 0
+// is still read by the other threads of its row) and is copied back by the caller.
+void flash_fwd_merge(at::Tensor& opart, const at::Tensor& lpart, at::Tensor& lrun, int64_t H) {
+  Range rr_("xdot.flash_fwd_merge");
+  TORCH_CHECK(opart.dim() == 4 && opart.is_cuda(), "xdot.flash_fwd_merge: opart (S, B, R, C)");
+  const int64_t S = opart.size(0), B = opart.size(1), R = opart.size(2), C = opart.size(3);
+  TORCH_CHECK(H > 0 && C % H == 0 && (C / H) % 32 == 0, "xdot.flash_fwd_merge: H");
+  check_part(opart, S, B * R * C, "opart");
+  check_part(lpart, S, B * H * R, "lpart");
+  TORCH_CHECK(lrun.is_cuda() && lrun.is_contiguous() && lrun.scalar_type() == at::kFloat && lrun.numel() == B * H * R,
+              "xdot.flash_fwd_merge: lrun (B, H, R) fp32");
+  xdot::fa::FwdArgs a{};
+  a.out32 = opart.data_ptr<float>(); a.lse = lrun.data_ptr<float>();
+  a.B = (int)B; a.H = (int)H; a.R = (int)R; a.nsplit = (int)S;
+  a.opart = opart.data_ptr<float>(); a.lpart = lpart.data_ptr<float>();
+  c10::DeviceGuard guard(opart.device());
+  // dtype only selects the (unused) 16-bit output path
+  TORCH_CHECK(xdot_flash_fwd_combine_launch(&a, xdot::DT_BF16, (int)(C / H), cur_stream(opart)) == 0,
+              "xdot.flash_fwd_merge: config");
+  check_launch(hipGetLastError(), "flash_fwd_merge");
+}
+
+// out = Σ_s part[s] in fp32; out may be part[0] (running sums: each element is read and
+// written by one thread)
+void sum_partials_into(const at::Tensor& part, at::Tensor& out) {
+  Range rr_("xdot.sum_partials_into");
+  TORCH_CHECK(part.is_cuda() && part.is_contiguous() && part.scalar_type() == at::kFloat && part.dim() >= 2,
+              "xdot.sum_partials_into: contiguous fp32 (S, ...) device tensor");
+  const int64_t n = part.numel() / part.size(0);
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kFloat && out.numel() == n,
+              "xdot.sum_partials_into: out must be a contiguous fp32 slot");
+  TORCH_CHECK(n % 4 == 0 && aligned16(part.data_ptr()) && aligned16(out.data_ptr()),
+              "xdot.sum_partials_into: numel % 4 and 16-byte alignment");
+  c10::DeviceGuard guard(part.device());
+  TORCH_CHECK(xdot_sum_partials_launch(part.data_ptr<float>(), out.data_ptr(), (int)part.size(0), n, xdot::DT_F32,
+                                       cur_stream(part)) == 0, "xdot.sum_partials_into");
+  check_launch(hipGetLastError(), "sum_partials_into");
+}
+
 // row-side grads of this column chunk into partial slots [sp0, sp0 + nsplit) of dpart
 void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                             const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
@@ -628,6 +669,8 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_bwd_rows_partial(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit, bool prescaled=False) -> ()");
   m.def("flash_bwd_rows_sum(Tensor dpart, int H, Tensor like) -> Tensor");
+  m.def("flash_fwd_merge(Tensor(a!) opart, Tensor lpart, Tensor(b!) lrun, int H) -> ()");
+  m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
@@ -654,5 +697,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);
   m.impl("flash_bwd_rows_sum", &flash_bwd_rows_sum);
+  m.impl("flash_fwd_merge", &flash_fwd_merge);
+  m.impl("sum_partials_into", &sum_partials_into);
   m.impl("adamw_step", &adamw_step);
 }

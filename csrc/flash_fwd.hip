@@ -579,6 +579,11 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
     acc += wgt * v;
   }
   const float inv = 1.f / sum;  // sum == 0 (fully masked row) -> NaN output, -inf lse
+  if (a.out32) {  // running fp32 merge (ring attention): masked-so-far rows stay 0 / -inf
+    *reinterpret_cast<f32x4*>(a.out32 + br * C + c4 * 4) = sum == 0.f ? f32x4{0.f, 0.f, 0.f, 0.f} : acc * inv;
+    if ((c4 * 4) % D == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = sum == 0.f ? -__builtin_inff() : mx + __logf(sum);
+    return;
+  }
   T16* op = reinterpret_cast<T16*>(a.out) + br * C + c4 * 4;
   u32x2 w;
   w[0] = pack2<DT>(acc[0] * inv, acc[1] * inv);

@@ -53,6 +53,8 @@ struct FwdArgs {
   int sp0;                 // first partial slot of this launch (chunked launches)
   int force_partial;       // 1: write partials even with nsplit == 1 (no combine here)
   int prescaled;           // 1: rows hold K * scale * log2(e) (xdot_prescale_rows_launch)
+  float* out32;            // combine only: non-null -> write the merged O in fp32 here (fully
+                           // masked rows: 0 with lse -inf), a running partial for the ring
 };
 
 struct BwdArgs {

@@ -51,3 +51,90 @@ def test_single_rank_noops():
     sync = GradSync(m)
     sync.wait()
     assert torch.equal(m.weight, w) and torch.equal(m.weight.grad, g)
+
+
+def _gradsync_contract_body(rank, ws):
+    import pytest
+    from xdot.parallel import GradSync
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4))
+    x = torch.full((3, 8), float(rank + 1))
+
+    def summed_grads(xs):
+        ref = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Linear(16, 4))
+        ref.load_state_dict(m.state_dict())
+        for xx in xs:
+            ref(xx).sum().backward()
+        return [p.grad for p in ref.parameters()]
+
+    all_x = [torch.full((3, 8), float(r + 1)) for r in range(ws)]
+    # frozen parameter: excluded from the buckets, no error, no gradient
+    m[0].bias.requires_grad_(False)
+    sync = GradSync(m, bucket_mb=0.0001)
+    m(x).sum().backward()
+    sync.wait()
+    sync.remove()
+    assert m[0].bias.grad is None
+    for p, g in zip(m.parameters(), summed_grads(all_x)):
+        if p.requires_grad:
+            torch.testing.assert_close(p.grad, g)
+    m[0].bias.requires_grad_(True)
+
+    # two backwards before wait(): refused loudly (would reduce partial gradients)
+    m.zero_grad(set_to_none=True)
+    sync = GradSync(m, bucket_mb=64.0)  # one multi-tensor bucket
+    m(x).sum().backward()
+    with pytest.raises(RuntimeError, match="before wait"):
+        m(x).sum().backward()
+    sync.remove()
+
+    # gradient accumulation: earlier micro-batches under no_sync(), the last one outside
+    m.zero_grad(set_to_none=True)
+    sync = GradSync(m, bucket_mb=0.0001)
+    with sync.no_sync():
+        m(x).sum().backward()
+    m(2 * x).sum().backward()
+    sync.wait()
+    sync.remove()
+    ref = summed_grads(all_x + [2 * t for t in all_x])
+    for p, g in zip(m.parameters(), ref):
+        torch.testing.assert_close(p.grad, g)
+
+    # unused parameter: wait() raises by default, reduces zeros with unused='zero'
+    extra = torch.nn.Linear(4, 4)
+    mm = torch.nn.ModuleDict({"a": m, "b": extra})
+    m.zero_grad(set_to_none=True)
+    sync = GradSync(mm, bucket_mb=0.0001)
+    m(x).sum().backward()
+    with pytest.raises(RuntimeError, match="b.weight"):
+        sync.wait()
+    sync.remove()
+    m.zero_grad(set_to_none=True)
+    sync = GradSync(mm, bucket_mb=0.0001, unused="zero")
+    m(x).sum().backward()
+    sync.wait()
+    sync.remove()
+    assert torch.count_nonzero(extra.weight.grad) == 0
+    for p, g in zip(m.parameters(), summed_grads(all_x)):
+        torch.testing.assert_close(p.grad, g)
+
+    # bf16 gradients reduced in fp32: exactly the fp32 sum rounded once
+    mb = torch.nn.Linear(8, 4).to(torch.bfloat16)
+    sync = GradSync(mb, bucket_mb=64.0, reduce_dtype=torch.float32)
+    xb = torch.randn(5, 8, generator=torch.Generator().manual_seed(rank)).to(torch.bfloat16)
+    mb(xb).float().pow(2).sum().backward()
+    local = [p.grad.float().clone() for p in mb.parameters()]
+    sync.wait()
+    sync.remove()
+    from xdot.utils import comm as C
+
+    for p, g in zip(mb.parameters(), local):
+        tot = g.clone()
+        C.get_comm().all_reduce(tot, op="sum")
+        assert p.grad.dtype == torch.bfloat16
+        assert torch.equal(p.grad, tot.to(torch.bfloat16))
+
+
+def test_gradsync_contract_gloo():
+    run_gloo(_gradsync_contract_body, 2)

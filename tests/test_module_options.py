@@ -1,0 +1,78 @@
+"""Constructor knobs of DistributedDotProductAttn beyond the reference signature:
+``fused``, ``backend``, ``dtype`` (compute-dtype policy), ``chunk_plan``; plus the thread-local
+backend override and its pinning into backward."""
+import pytest
+import torch
+
+from xdot import DistributedDotProductAttn
+from xdot import _ext
+
+
+def test_fused_alias_and_validation():
+    assert DistributedDotProductAttn(64, num_heads=2, fused=True).impl == "flash"
+    assert DistributedDotProductAttn(64, num_heads=2, fused=False).impl == "materialized"
+    with pytest.raises(ValueError):
+        DistributedDotProductAttn(64, num_heads=2, fused=True, impl="materialized")
+    with pytest.raises(ValueError):
+        DistributedDotProductAttn(64, backend="cuda")
+    with pytest.raises(ValueError):
+        DistributedDotProductAttn(64, dtype=torch.int32)
+    with pytest.raises(ValueError):
+        DistributedDotProductAttn(64, chunk_plan=0)
+    m = DistributedDotProductAttn(64, num_heads=2, backend="torch", dtype=torch.bfloat16, chunk_plan=2)
+    r = repr(m)
+    assert "backend=torch" in r and "chunk_plan=2" in r and "bfloat16" in r
+
+
+def test_backend_override_scopes_and_pins():
+    assert _ext.current_backend() in ("auto", "hip", "torch")
+    with _ext.backend("torch"):
+        assert _ext.current_backend() == "torch"
+        with _ext.backend(None):  # None / 'auto' keep the enclosing choice
+            assert _ext.current_backend() == "torch"
+    assert _ext.current_backend() != "torch" or _ext.FLAGS.backend == "torch"
+    with pytest.raises(ValueError):
+        _ext.backend("cuda")
+
+    seen = {}
+
+    class F(torch.autograd.Function):
+        @staticmethod
+        @_ext.pinned
+        def forward(ctx, x):
+            return x * 2
+
+        @staticmethod
+        @_ext.pinned
+        def backward(ctx, g):
+            seen["bwd"] = _ext.current_backend()
+            return g * 2
+
+    x = torch.ones(3, requires_grad=True)
+    with _ext.backend("torch"):
+        y = F.apply(x)
+    y.sum().backward()  # outside the context: backward still sees 'torch'
+    assert seen["bwd"] == "torch"
+    torch.testing.assert_close(x.grad, torch.full((3,), 2.0))
+
+
+@pytest.mark.parametrize("impl", ["materialized", "flash", "ring"])
+def test_compute_dtype_policy(impl):
+    """fp32 master params + inputs, bf16 compute: equals running a bf16 copy of the module,
+    output comes back in fp32, gradients land on the fp32 parameters."""
+    torch.manual_seed(0)
+    m = DistributedDotProductAttn(64, num_heads=4, dtype=torch.bfloat16, impl=impl)
+    ref = DistributedDotProductAttn(64, num_heads=4, impl=impl).to(torch.bfloat16)
+    ref.load_state_dict({k: v.to(torch.bfloat16) for k, v in m.state_dict().items()})
+    x = torch.rand(1, 24, 64)
+    mask = torch.rand(1, 24, 24) < 0.2
+    mask[..., 0] = False
+    out = m(x, x, x, mask)
+    assert out.dtype == torch.float32
+    out_ref = ref(x.to(torch.bfloat16), x.to(torch.bfloat16), x.to(torch.bfloat16), mask)
+    torch.testing.assert_close(out, out_ref.float(), atol=0, rtol=0)
+    out.sum().backward()
+    out_ref.float().sum().backward()
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert p.dtype == torch.float32 and p.grad is not None and p.grad.dtype == torch.float32, n
+        torch.testing.assert_close(p.grad, q.grad.float(), atol=2e-2, rtol=2e-2)

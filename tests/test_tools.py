@@ -117,3 +117,22 @@ def test_reference_import_lines():
     ])
     out = _run(["-c", code])
     assert out.startswith("ok")
+
+
+def test_packaging_metadata():
+    """setup.py reads the version from xdot.VERSION_INFO without importing the package and
+    ships the native library as package data (``pip install . --no-build-isolation``)."""
+    import os
+    import subprocess
+    import sys
+
+    import xdot
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "setup.py", "--version"], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, XDOT_SKIP_NATIVE="1"), timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == xdot.__version__
+    src = open(os.path.join(root, "setup.py")).read()
+    assert '"_C.so"' in src and "build_py" in src
+    assert os.path.exists(os.path.join(root, "pyproject.toml"))

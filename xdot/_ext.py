@@ -50,12 +50,60 @@ def available() -> bool:
     return load()
 
 
+_tls = threading.local()
+BACKENDS = ("auto", "hip", "torch")
+
+
+def current_backend() -> str:
+    """Compute backend in effect on this thread: a :func:`backend` override, else
+    ``XDOT_BACKEND`` (``auto`` | ``hip`` | ``torch``)."""
+    return getattr(_tls, "backend", None) or FLAGS.backend
+
+
+class backend:
+    """``with _ext.backend('torch'):`` — override the compute backend on this thread (what the
+    ``backend=`` argument of :class:`xdot.DistributedDotProductAttn` does).  ``None`` / ``'auto'``
+    keep the process default.  Autograd runs backward on its own thread, so the custom
+    Functions record the backend in forward and re-enter it in backward (:func:`pinned`)."""
+
+    def __init__(self, b: str = None):
+        if b is not None and b not in BACKENDS:
+            raise ValueError(f"backend must be one of {BACKENDS}, got {b!r}")
+        self.b = None if b in (None, "auto") else b
+
+    def __enter__(self):
+        self.prev = getattr(_tls, "backend", None)
+        if self.b is not None:
+            _tls.backend = self.b
+        return self
+
+    def __exit__(self, *exc):
+        _tls.backend = self.prev
+        return False
+
+
+def pinned(fn):
+    """Decorator for ``forward(ctx, ...)`` / ``backward(ctx, ...)`` of a custom autograd Function:
+    forward records :func:`current_backend`, backward runs under it."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(ctx, *args):
+        if fn.__name__ == "forward":
+            ctx.xdot_backend = getattr(_tls, "backend", None)
+            return fn(ctx, *args)
+        with backend(getattr(ctx, "xdot_backend", None)):
+            return fn(ctx, *args)
+
+    return wrap
+
+
 def use_hip(*tensors: torch.Tensor) -> bool:
     """Decide whether GPU tensors go to the HIP kernels.  Raises if they should but the
     extension is not loadable (no silent fallback on a GPU box)."""
     if not any(isinstance(t, torch.Tensor) and t.is_cuda for t in tensors):
         return False
-    if FLAGS.backend == "torch":
+    if current_backend() == "torch":
         return False
     if load():
         return True

@@ -24,6 +24,19 @@ Three execution paths, chosen by ``impl``:
 Extensions over the reference (all backward compatible): ``attn_mask=None`` means no mask,
 ``value_dim`` may differ from ``key_dim`` with several heads (the reference raises), any
 float dtype works, and ``distributed=False`` gives the single-device ground truth.
+
+Keyword-only knobs (each mirrors an environment flag, the argument wins):
+
+``impl``        ``'auto'`` | ``'flash'`` | ``'ring'`` | ``'materialized'`` (above);
+``fused``       ``True`` = ``impl='flash'``, ``False`` = ``impl='materialized'`` (SURVEY name);
+``backend``     ``'auto'`` | ``'hip'`` | ``'torch'``: compute backend of this module's ops, forward
+                and backward (``XDOT_BACKEND``); ``'torch'`` runs the torch reference math on GPU;
+``dtype``       compute-dtype policy: e.g. ``torch.bfloat16`` runs projections and attention in
+                bf16 while parameters / inputs stay fp32 (master weights); output in the input
+                dtype.  ``None``: compute in the input dtype;
+``chunk_plan``  row chunks of the fused path's all-gather / reduce-scatter pipeline
+                (``XDOT_GATHER_CHUNKS``); the materialised path's chunking is ``offset``;
+``comm``        communicator (default: the process group of :func:`xdot.init`).
 """
 from __future__ import annotations
 
@@ -34,6 +47,7 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 
+from .. import _ext
 from ..ops.linear import linear
 from ..ops.softmax import scale_mask_softmax
 from ..parallel.autograd import FullMultiplication, RightTransposeMultiplication
@@ -46,9 +60,20 @@ __all__ = ["DistributedDotProductAttn"]
 class DistributedDotProductAttn(nn.Module):
     def __init__(self, key_dim: int, value_dim: Optional[int] = None, query_dim: Optional[int] = None,
                  num_heads: int = 1, add_bias: bool = False, offset: Optional[int] = 32,
-                 distributed: bool = True, *, impl: str = "auto",
+                 distributed: bool = True, *, impl: str = "auto", fused: Optional[bool] = None,
+                 backend: str = "auto", dtype: Optional[torch.dtype] = None, chunk_plan: Optional[int] = None,
                  comm: Optional[_comm.Communicator] = None):
         super().__init__()
+        if fused is not None:
+            if impl not in ("auto", "flash" if fused else "materialized"):
+                raise ValueError(f"fused={fused} contradicts impl={impl!r}")
+            impl = "flash" if fused else "materialized"
+        if backend not in ("auto", "hip", "torch"):
+            raise ValueError(f"backend must be auto|hip|torch, got {backend!r}")
+        if dtype is not None and not (isinstance(dtype, torch.dtype) and dtype.is_floating_point):
+            raise ValueError(f"dtype must be a floating torch.dtype or None, got {dtype!r}")
+        if chunk_plan is not None and int(chunk_plan) < 1:
+            raise ValueError(f"chunk_plan must be a positive number of row chunks, got {chunk_plan!r}")
         if key_dim % num_heads != 0:
             raise ValueError(f"key_dim {key_dim} not divisible by num_heads {num_heads}")
         value_dim = value_dim if value_dim is not None else key_dim
@@ -63,6 +88,9 @@ class DistributedDotProductAttn(nn.Module):
         self.distributed = distributed
         self.dim = key_dim // num_heads
         self.impl = impl
+        self.backend = backend
+        self.compute_dtype = dtype
+        self.chunk_plan = None if chunk_plan is None else int(chunk_plan)
         self.comm = comm
         self.keys = nn.Linear(key_dim, key_dim, bias=add_bias)
         self.queries = nn.Linear(query_dim, key_dim, bias=add_bias)
@@ -75,9 +103,30 @@ class DistributedDotProductAttn(nn.Module):
             return self.impl
         from ..parallel import attention as pa
 
-        return "flash" if pa.flash_supported(x, self.dim, self.value_dim // self.num_heads) else "materialized"
+        with _ext.backend(self.backend):
+            if self.compute_dtype is not None:
+                x = x.to(self.compute_dtype) if x.is_floating_point() else x
+            return "flash" if pa.flash_supported(x, self.dim, self.value_dim // self.num_heads) else "materialized"
 
     def forward(self, keys: Tensor, queries: Tensor, values: Tensor, attn_mask: Optional[Tensor] = None) -> Tensor:
+        with _ext.backend(self.backend):
+            cdt = self.compute_dtype
+            if cdt is None or keys.dtype == cdt:
+                return self._forward(keys, queries, values, attn_mask)
+            out_dt = keys.dtype
+            same_qv = queries is values
+            keys_c = keys.to(cdt)
+            queries_c = keys_c if queries is keys else queries.to(cdt)
+            values_c = queries_c if same_qv else (keys_c if values is keys else values.to(cdt))
+            return self._forward(keys_c, queries_c, values_c, attn_mask).to(out_dt)
+
+    def _w(self, t: Optional[Tensor]) -> Optional[Tensor]:
+        """A parameter in the compute dtype (autograd flows back to the master copy)."""
+        if t is None or self.compute_dtype is None or t.dtype == self.compute_dtype:
+            return t
+        return t.to(self.compute_dtype)
+
+    def _forward(self, keys: Tensor, queries: Tensor, values: Tensor, attn_mask: Optional[Tensor]) -> Tensor:
         scale = 1.0 / math.sqrt(self.dim)
         if self._pick_impl(keys) == "flash":
             from ..parallel.attention import seq_parallel_attention_packed, start_gather
@@ -91,7 +140,7 @@ class DistributedDotProductAttn(nn.Module):
                                                      attn_mask.shape[1], attn_mask.shape[2])
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
-            pending = start_gather(qv, comm)
+            pending = start_gather(qv, comm, chunks=self.chunk_plan)
             k = self._proj(self.keys, keys)
             o = seq_parallel_attention_packed(k, qv, attn_mask, self.num_heads, scale, comm=comm, pending=pending)
             return self._proj(self.composition, o)
@@ -103,24 +152,23 @@ class DistributedDotProductAttn(nn.Module):
             k = self._proj(self.keys, keys)
             o = ring_attention_packed(k, qv, attn_mask, self.num_heads, scale, comm=comm)
             return self._proj(self.composition, o)
-        k = self.keys(keys)
-        q = self.queries(queries)
-        v = self.values(values)
-        return self.composition(self._materialized(k, q, v, attn_mask, scale))
+        k = self._proj(self.keys, keys)
+        q = self._proj(self.queries, queries)
+        v = self._proj(self.values, values)
+        return self._proj(self.composition, self._materialized(k, q, v, attn_mask, scale))
 
-    @staticmethod
-    def _proj(layer: nn.Linear, x: Tensor) -> Tensor:
-        """``layer(x)`` with the split-K MFMA weight gradient (:mod:`xdot.ops.linear`)."""
-        return linear(x, layer.weight, layer.bias)
+    def _proj(self, layer: nn.Linear, x: Tensor) -> Tensor:
+        """``layer(x)`` (compute dtype) with the split-K MFMA weight gradient (:mod:`xdot.ops.linear`)."""
+        return linear(x, self._w(layer.weight), self._w(layer.bias))
 
     def _project_qv(self, queries: Tensor, values: Tensor) -> Tensor:
         """[q | v] packed (B, R, 2C): ONE GEMM when ``queries is values`` (self-attention), so
         the gathered side travels in one all-gather and its grads in one reduce-scatter."""
         if queries is values and self.queries.in_features == self.values.in_features:
-            w = torch.cat([self.queries.weight, self.values.weight], 0)
+            w = self._w(torch.cat([self.queries.weight, self.values.weight], 0))
             b = None
             if self.queries.bias is not None:
-                b = torch.cat([self.queries.bias, self.values.bias], 0)
+                b = self._w(torch.cat([self.queries.bias, self.values.bias], 0))
             return linear(queries, w, b)
         return torch.cat([self._proj(self.queries, queries), self._proj(self.values, values)], dim=-1)
 
@@ -147,4 +195,5 @@ class DistributedDotProductAttn(nn.Module):
 
     def extra_repr(self) -> str:
         return (f"heads={self.num_heads}, head_dim={self.dim}, value_dim={self.value_dim}, "
-                f"offset={self.offset}, distributed={self.distributed}, impl={self.impl}")
+                f"offset={self.offset}, distributed={self.distributed}, impl={self.impl}, backend={self.backend}, "
+                f"dtype={self.compute_dtype}, chunk_plan={self.chunk_plan}")

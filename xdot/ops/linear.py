@@ -72,12 +72,14 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
 
 class LinearFn(torch.autograd.Function):
     @staticmethod
+    @_ext.pinned
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         return F.linear(x, weight, bias)
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dx = dw = db = None

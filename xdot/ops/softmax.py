@@ -67,6 +67,7 @@ class ScaleMaskSoftmax(torch.autograd.Function):
     """y = softmax(scale * x, masked -> -inf); one fused kernel per direction on GPU."""
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx, scores, mask, scale):
         y = scale_mask_softmax_fwd(scores, mask, scale)
         ctx.save_for_backward(y)
@@ -74,6 +75,7 @@ class ScaleMaskSoftmax(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
         return scale_mask_softmax_bwd(y, dy, ctx.scale), None, None

@@ -50,6 +50,15 @@ def flash_supported(x: Tensor, head_dim: int, v_head_dim: int) -> bool:
     return _ext.use_hip(x) and hasattr(_ext.ops(), "flash_fwd")
 
 
+def _hip_ok(k: Tensor, qv: Tensor, H: int) -> bool:
+    """The HIP kernels take this call: a GPU bf16/fp16 row side, a supported head dim and a
+    value width equal to the key width (otherwise the torch path runs, as documented)."""
+    C = k.shape[-1]
+    return (k.is_cuda and k.dtype in (torch.bfloat16, torch.float16) and C % H == 0
+            and C // H in FLASH_HEAD_DIMS and qv.shape[-1] == 2 * C and _ext.use_hip(k)
+            and hasattr(_ext.ops(), "flash_fwd"))
+
+
 # ----------------------------------------------------------------------------------------
 # gather helpers
 # ----------------------------------------------------------------------------------------
@@ -64,7 +73,7 @@ def _gather_rows(comm, x: Tensor, async_op: bool = True):
     return h if async_op else out
 
 
-def _row_chunks(n: int, R: int, hip: bool) -> List[Tuple[int, int]]:
+def _row_chunks(n: int, R: int, hip: bool, nchunks: Optional[int] = None) -> List[Tuple[int, int]]:
     """Row chunks (r0, rc) of every rank's shard for the pipelined gather of the fused path:
     with several ranks the gathered side can travel in ``XDOT_GATHER_CHUNKS`` all-gathers so
     chunk c+1 is in flight while the kernels consume chunk c (and, in backward, chunk c's
@@ -72,7 +81,7 @@ def _row_chunks(n: int, R: int, hip: bool) -> List[Tuple[int, int]]:
     one MI355X with emulated 8-rank shapes, 2 chunks cost ≈0.23 ms more compute per step
     (per-chunk mask copies, split partials, half-occupied last workgroup rounds), about what
     the overlap can save over xGMI."""
-    nc = FLAGS.gather_chunks if (hip and n > 1) else 1
+    nc = (nchunks or FLAGS.gather_chunks) if (hip and n > 1) else 1
     nc = max(1, min(nc, R // 64))
     base, extra = divmod(R, nc)
     out, r0 = [], 0
@@ -187,12 +196,13 @@ class SeqParallelAttention(torch.autograd.Function):
     into split partials (merged by one combine) so communication overlaps compute."""
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx, k, qv, mask, H, scale, comm, pending=None):
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
         B, R = k.shape[0], k.shape[1]
         n = comm.world_size
-        use_hip = _ext.use_hip(k) and k.dtype in (torch.bfloat16, torch.float16)
+        use_hip = _hip_ok(k, qv, H)
         if pending is None:
             pending = _PendingGather(comm, qv, _row_chunks(n, qv.shape[1], use_hip))
         chunks = pending.chunks
@@ -220,9 +230,14 @@ class SeqParallelAttention(torch.autograd.Function):
                     mks.append(None)
                     continue
                 # chunk columns j*R + r0 + i: a strided slice per source rank (index_select on the
-                # last dim of a (B, R, T) bool tensor is a slow gather)
-                mc = mask if len(chunks) == 1 else mask.view(B, R, n, R)[..., r0:r0 + rc].reshape(B, R, n * rc)
-                mks.append(flash.prepare_mask(mc, B, R, n * rc))
+                # last dim of a (B, R, T) bool tensor is a slow gather); packed once per mask
+                # tensor (flash.MASK_CACHE: re-passing the same mask costs nothing)
+                if len(chunks) == 1:
+                    mks.append(flash.prepare_mask_cached(mask, B, R, n * rc))
+                else:
+                    mks.append(flash.prepare_mask_cached(
+                        mask, B, R, n * rc, tag=(r0, rc, n),
+                        view=lambda m, r0=r0, rc=rc: m.view(B, R, n, R)[..., r0:r0 + rc].reshape(B, R, n * rc)))
             if len(chunks) == 1:
                 qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
                 o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mks[0], H, scale, prescaled=prescaled)
@@ -252,6 +267,7 @@ class SeqParallelAttention(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx, do):
         k, o, lse, *bufs = ctx.saved_tensors
         comm, H, scale, chunks = ctx.comm, ctx.H, ctx.scale, ctx.chunks
@@ -332,12 +348,14 @@ class SeqParallelAttention(torch.autograd.Function):
         return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None
 
 
-def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None) -> "_PendingGather":
+def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None,
+                 chunks: Optional[int] = None) -> "_PendingGather":
     """Issue the all-gather(s) of the packed gathered side early (e.g. before the row-side
-    projection GEMM) and hand the result to :func:`seq_parallel_attention_packed`."""
+    projection GEMM) and hand the result to :func:`seq_parallel_attention_packed`.
+    ``chunks``: row chunks of the pipeline (default ``XDOT_GATHER_CHUNKS``)."""
     comm = comm or _comm.get_comm()
     hip = _ext.use_hip(qv) and qv.dtype in (torch.bfloat16, torch.float16)
-    return _PendingGather(comm, qv.detach(), _row_chunks(comm.world_size, qv.shape[1], hip))
+    return _PendingGather(comm, qv.detach(), _row_chunks(comm.world_size, qv.shape[1], hip, chunks))
 
 
 def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,

@@ -19,6 +19,7 @@ from typing import Any, Optional
 import torch
 from torch import Tensor
 
+from .. import _ext
 from ..utils import comm as _comm
 from .functional import distributed_matmul_all, distributed_matmul_nt, distributed_matmul_tn
 
@@ -29,6 +30,7 @@ class RightTransposeMultiplication(torch.autograd.Function):
     """``C = A·Bᵀ`` (local (P,R,D) x (P,R,D) -> (P,R,T)).  Reference ``ops.py:19-37``."""
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx: Any, left: Tensor, right: Tensor, offset: Optional[int] = None,
                 comm: Optional[_comm.Communicator] = None) -> Tensor:
         comm = comm or _comm.get_comm()
@@ -37,6 +39,7 @@ class RightTransposeMultiplication(torch.autograd.Function):
         return distributed_matmul_nt(left, right, offset, comm=comm)
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx: Any, grad: Tensor):
         left, right = ctx.saved_tensors
         gl = gr = None
@@ -51,6 +54,7 @@ class FullMultiplication(torch.autograd.Function):
     """``C = A·B`` (local (P,R,T) x (P,R,D) -> (P,R,D)).  Reference ``ops.py:40-54``."""
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx: Any, left: Tensor, right: Tensor, offset: Optional[int] = None,
                 comm: Optional[_comm.Communicator] = None) -> Tensor:
         comm = comm or _comm.get_comm()
@@ -59,6 +63,7 @@ class FullMultiplication(torch.autograd.Function):
         return distributed_matmul_all(left, right, offset, comm=comm)
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx: Any, grad: Tensor):
         left, right = ctx.saved_tensors
         gl = gr = None
@@ -75,6 +80,7 @@ class LeftTransposeMultiplication(torch.autograd.Function):
     compat_reference_bug = False
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx: Any, left: Tensor, right: Tensor, offset: Optional[int] = None,
                 comm: Optional[_comm.Communicator] = None) -> Tensor:
         comm = comm or _comm.get_comm()
@@ -83,6 +89,7 @@ class LeftTransposeMultiplication(torch.autograd.Function):
         return distributed_matmul_tn(left, right, comm=comm)
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx: Any, grad: Tensor):
         left, right = ctx.saved_tensors
         gl = gr = None

@@ -14,6 +14,7 @@ must be **summed** (not averaged) across ranks.  The reference leaves this to th
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -92,42 +93,94 @@ class GradSync:
         sync = GradSync(model)          # registers hooks
         loss.backward()
         sync.wait()                     # all buckets reduced (stream-ordered)
+
+    Contract (checked, never silently wrong):
+
+    * one ``backward`` per ``wait()``.  A second backward before ``wait()`` would launch the
+      all-reduces on partial gradients, so it raises; accumulate micro-batches under
+      :meth:`no_sync` (hooks are muted there) and let the LAST backward run outside it;
+    * every bucket must have been launched when ``wait()`` runs.  A parameter that requires a
+      gradient but took no part in the backward leaves its bucket incomplete: ``unused="raise"``
+      (default) raises naming it, ``unused="zero"`` reduces it as a zero gradient (every rank
+      must then do the same, as with DDP's ``find_unused_parameters``);
+    * ``reduce_dtype``: dtype of the all-reduce (e.g. ``torch.float32`` for bf16 gradients: one
+      rounding at the end instead of one per ring step).  Default: the gradients' dtype.
     """
 
     def __init__(self, module: nn.Module, comm: Optional[_comm.Communicator] = None,
-                 bucket_mb: float = 16.0, op: str = "sum"):
+                 bucket_mb: float = 16.0, op: str = "sum", reduce_dtype: Optional[torch.dtype] = None,
+                 unused: str = "raise"):
+        if op not in ("sum", "avg"):
+            raise ValueError(f"op must be sum|avg, got {op!r}")
+        if unused not in ("raise", "zero"):
+            raise ValueError(f"unused must be raise|zero, got {unused!r}")
         self.comm = comm or _comm.get_comm()
         self.op = op
+        self.reduce_dtype = reduce_dtype
+        self.unused = unused
         params = [p for p in module.parameters() if p.requires_grad]
+        self._names = {id(p): n for n, p in module.named_parameters()}
         # reverse registration order ~ gradient arrival order
         self.buckets = _buckets(list(reversed(params)), int(bucket_mb * 2**20))
         self._index = {id(p): i for i, b in enumerate(self.buckets) for p in b}
-        self._ready = [0] * len(self.buckets)
+        self._seen = [set() for _ in self.buckets]
+        self._launched = [False] * len(self.buckets)
         self._handles: List = []
         self._hooks = []
+        self._muted = False
         if self.comm.world_size > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (no all-reduce) inside this context."""
+        prev, self._muted = self._muted, True
+        try:
+            yield
+        finally:
+            self._muted = prev
+
     def _on_grad(self, p):
+        if self._muted:
+            return
         i = self._index[id(p)]
-        self._ready[i] += 1
-        if self._ready[i] == len(self.buckets[i]):
+        if self._launched[i] or id(p) in self._seen[i]:
+            raise RuntimeError(
+                f"GradSync: gradient of {self._names.get(id(p), '<param>')} arrived again before wait(): "
+                "run one backward per wait(), or accumulate earlier micro-batches under sync.no_sync()")
+        self._seen[i].add(id(p))
+        if len(self._seen[i]) == len(self.buckets[i]):
             self._launch(i)
 
     def _launch(self, i):
         b = self.buckets[i]
+        self._launched[i] = True
+        for p in b:
+            if p.grad is None:  # unused="zero": reduce a zero gradient
+                p.grad = torch.zeros_like(p)
         g0 = b[0].grad
-        if len(b) == 1 and g0.is_contiguous():
+        rdt = self.reduce_dtype or g0.dtype
+        if len(b) == 1 and g0.is_contiguous() and g0.dtype == rdt:
             flat = g0  # one-tensor bucket: reduce the gradient in place (no flatten / copy back)
         else:
-            flat = torch.cat([p.grad.reshape(-1) for p in b])
+            flat = torch.cat([p.grad.reshape(-1).to(rdt) for p in b])
         h = self.comm.all_reduce(flat, op="sum", async_op=True)
         self._handles.append((i, flat, h))
 
     @torch.no_grad()
     def wait(self) -> None:
         ws = self.comm.world_size
+        if ws > 1:
+            missing = [i for i, done in enumerate(self._launched) if not done]
+            if missing and self.unused == "raise":
+                names = [self._names.get(id(p), "<param>") for i in missing for p in self.buckets[i]
+                         if id(p) not in self._seen[i]]
+                self._reset()
+                raise RuntimeError(f"GradSync.wait(): no gradient arrived for {names} (unused parameter? "
+                                   "freeze it, or pass unused='zero')")
+            for i in missing:  # bucket index order: the same on every rank
+                self._launch(i)
         for i, flat, h in self._handles:
             h.wait()
             if self.op == "avg":
@@ -140,8 +193,12 @@ class GradSync:
                 n = p.numel()
                 p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
+        self._reset()
+
+    def _reset(self):
         self._handles.clear()
-        self._ready = [0] * len(self.buckets)
+        self._seen = [set() for _ in self.buckets]
+        self._launched = [False] * len(self.buckets)
 
     def remove(self):
         for h in self._hooks:

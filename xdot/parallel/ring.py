@@ -11,12 +11,13 @@ This module is the memory-lean alternative for sequences whose gathered side sho
 resident in full: the ``[q | v]`` shards travel around the ring one rank-block at a time
 (``sendrecv`` to rank+1 / from rank-1 on the RCCL stream), and the block that arrived last step
 is consumed by the flash kernels while the next one is in flight.  Resident per rank: two
-``(B, R, 2C)`` blocks (instead of ``(B, T, 2C)``) plus the fp32 split partials.
+``(B, R, 2C)`` blocks (instead of ``(B, T, 2C)``) plus ``1 + splits`` fp32 ``(B, R, C)`` partial
+slots (a running merge: independent of the ring length).
 
 forward   step s (s = 0..N-1) consumes block ``src = (rank - s) mod N``: the flash kernel
-          writes its split partials (O, LSE) into slots of one buffer; ONE combine kernel
-          merges all blocks at the end (blocks whose rows are fully masked contribute nothing,
-          rows masked everywhere come out NaN like the reference);
+          writes its split partials (O, LSE), which are merged at once into a running fp32
+          (O, LSE) slot; the last step's combine writes the output (blocks whose rows are fully
+          masked contribute nothing, rows masked everywhere come out NaN like the reference);
 backward  the blocks circulate again.  Per step: the row-side partial ``dk`` (summed once at
           the end) and the block's ``[dq | dv]`` contribution, added to an fp32 accumulator that
           travels WITH the block one hop behind it; after N steps plus one hop every rank holds
@@ -113,6 +114,7 @@ class RingAttention(torch.autograd.Function):
     """Ring attention on the packed gathered side ``qv = [q | v]`` (B, R, 2C) of this rank."""
 
     @staticmethod
+    @_ext.pinned
     def forward(ctx, k, qv, mask, H, scale, comm):
         check_consistent(comm, "ring_attention", k, qv, H)
         B, R, C = k.shape
@@ -132,17 +134,26 @@ class RingAttention(torch.autograd.Function):
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0)
             kk = flash.prescale(k, scale) if prescaled else k.contiguous()
             ns = int(ops.flash_splits(B, R, R, H, False))
-            opart = torch.empty(n * ns, B, R, C, dtype=torch.float32, device=k.device)
-            lpart = torch.empty(n * ns, B, H, R, dtype=torch.float32, device=k.device)
+            # slot 0: the running (O, LSE) of the blocks seen so far (fp32), slots 1..ns: the
+            # arriving block's split partials, merged into slot 0 after each step — resident
+            # partials stay (1 + ns) slots whatever the ring length
+            opart = torch.empty(1 + ns, B, R, C, dtype=torch.float32, device=k.device)
+            lpart = torch.empty(1 + ns, B, H, R, dtype=torch.float32, device=k.device)
+            lpart[0].fill_(-float("inf"))
+            lrun = torch.empty(B, H, R, dtype=torch.float32, device=k.device)
             for s in range(n):
                 ring.start(s)
                 src = ring.src(s)
-                mk = flash.prepare_mask(_block_mask(mask, src, R), B, R, R)
+                mk = flash.prepare_mask_cached(mask, B, R, R, tag=("ring", src, R),
+                                               view=lambda m, src=src: _block_mask(m, src, R))
                 mks.append(mk)
                 bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                 g = ring.cur
                 ops.flash_fwd_partial(kk, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                      float(scale), opart, lpart, s * ns, ns, prescaled)
+                                      float(scale), opart, lpart, 1, ns, prescaled)
+                if s < n - 1:
+                    ops.flash_fwd_merge(opart, lpart, lrun, int(H))
+                    lpart[0].copy_(lrun)
                 ring.advance()
             o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
             ctx.save_for_backward(kk, qv, o, lse)
@@ -170,6 +181,7 @@ class RingAttention(torch.autograd.Function):
         return o
 
     @staticmethod
+    @_ext.pinned
     def backward(ctx, do):
         k, qv, o, lse = ctx.saved_tensors
         comm, H, scale = ctx.comm, ctx.H, ctx.scale
@@ -193,7 +205,9 @@ class RingAttention(torch.autograd.Function):
             hi = _side_stream(do.device) if two else cur  # XDOT_RING_OVERLAP (utils/env.py)
             delta = flash.bwd_delta(do, o, H)
             nsr = int(ops.flash_splits(B, R, R, H, True))
-            dpart = torch.empty(n * nsr, B, R, C, dtype=torch.float32, device=k.device)
+            # slot 0: running fp32 dk, slots 1..nsr: this step's column-split partials
+            dpart = torch.empty(1 + nsr, B, R, C, dtype=torch.float32, device=k.device)
+            dpart[0].zero_()
         else:
             cdt = lse.dtype
             delta = (_heads(do, H, cdt) * _heads(o, H, cdt)).sum(-1)
@@ -212,7 +226,9 @@ class RingAttention(torch.autograd.Function):
                                                 fp32_out=True, prescaled=ctx.prescaled)
                 bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                 ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                           flags, int(H), float(scale), dpart, s * nsr, nsr, ctx.prescaled)
+                                           flags, int(H), float(scale), dpart, 1, nsr, ctx.prescaled)
+                if s < n - 1:
+                    ops.sum_partials_into(dpart, dpart[0])
                 cur.wait_stream(hi)
                 contrib.record_stream(cur)
             else:
