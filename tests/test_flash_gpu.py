@@ -242,10 +242,10 @@ def test_mask_cache_and_all_false_short_circuit(gpu):
     from xdot.ops import flash
 
     flash.MASK_CACHE.clear()
-    B, R, T = 1, 64, 192
+    B, R, T = 1, 64, 192  # 3 column tiles: the flag rows carry one padding tile
     z = torch.zeros(B, R, T, dtype=torch.bool, device=gpu)
     first = flash.prepare_mask_cached(z, B, R, T)
-    assert first is not None and int(first.flags.max()) == 0
+    assert first is not None and int(first.flags[..., :3].max()) == 0
     torch.cuda.synchronize()
     assert flash.prepare_mask_cached(z, B, R, T) is None
     m = torch.rand(B, R, T, device=gpu) < 0.3

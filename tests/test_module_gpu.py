@@ -52,8 +52,16 @@ def _module_case(rank, ws, impl, masked):
     assert _rel(gx, xf.grad) <= 3e-2, "input grad"
     names = [n for n, _ in ref.named_parameters()]
     assert len(names) == 8  # keys/queries/values/composition x (weight, bias)
+    rgrad = {n: q.grad for n, q in ref.named_parameters()}
     for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
         assert p.grad is not None, n
+        if n == "queries.bias":
+            # exactly 0 in exact arithmetic (softmax is shift invariant along the gathered axis:
+            # the bias adds k·b to a whole score row), so only rounding noise is left: bound it
+            # against the same kind of row sum on the other side, the keys bias gradient
+            err = (p.grad.float() - q.grad.float()).norm() / rgrad["keys.bias"].float().norm()
+            assert err <= 3e-2, f"grad of {n}: {err:.3e}"
+            continue
         assert _rel(p.grad, q.grad) <= 3e-2, f"grad of {n}: {_rel(p.grad, q.grad):.3e}"
 
 

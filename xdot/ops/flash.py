@@ -88,7 +88,10 @@ class MaskCache:
         e.none_ev, e.none_host = None, None
         if packed.flags.is_cuda:
             e.none_host = torch.empty((), dtype=torch.bool, pin_memory=True)
-            e.none_host.copy_(packed.flags.any(), non_blocking=True)
+            # the flag rows are padded to a multiple of 4 tiles with 1 ("all masked"): only the
+            # ceil(T/64) real column tiles count
+            nkt = (packed.shape[-1] + 63) // 64
+            e.none_host.copy_(packed.flags[..., :nkt].any(), non_blocking=True)
             e.none_ev = torch.cuda.Event()
             e.none_ev.record()
         if len(self._d) >= self.capacity:
