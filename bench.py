@@ -166,7 +166,9 @@ def main(argv=None, comm=None):
             "loss": lossv,
         }
         if emulated:
-            rec["metric"] = "EMULATED per-rank step (no transport; diagnostics only): " + metric
+            link = getattr(comm, "link_gbps", None)
+            what = "no transport" if link is None else f"link model {link:g} GB/s collectives, {comm.p2p_gbps:g} GB/s hops"
+            rec["metric"] = f"EMULATED per-rank step ({what}; diagnostics only): " + metric
             rec["config"]["parallelism"] += "-emulated"
         print(json.dumps(rec), flush=True)
     if not emulated:

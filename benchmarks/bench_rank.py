@@ -6,7 +6,12 @@ device-local copies.  The result is the per-rank compute + launch cost of the N-
 (what the scaling run adds on top is the RCCL transport).  Prints ``bench.py``'s JSON line
 with the metric and parallelism marked EMULATED.
 
+``--link-gbps G`` turns on the link model: every collective runs on its own stream as a
+spin of (bytes on the wire / G GB/s) plus the copy, so the step shows how much of an
+xGMI-sized transfer the schedule hides (an ASSUMED rate, not a measurement of RCCL).
+
     python benchmarks/bench_rank.py --world 8 --steps 20 --warmup 5
+    python benchmarks/bench_rank.py --world 8 --link-gbps 300 --p2p-gbps 64
 """
 from __future__ import annotations
 
@@ -21,12 +26,15 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--world", type=int, nargs="+", default=[8])
+    ap.add_argument("--link-gbps", type=float, default=None,
+                    help="emulated collective bus bandwidth per rank (GB/s); default: no transfer time")
+    ap.add_argument("--p2p-gbps", type=float, default=None, help="emulated ring-hop link rate (GB/s)")
     a, rest = ap.parse_known_args()
     import bench
     from xdot.utils.comm import EmulatedComm
 
     for n in a.world:
-        bench.main(["--gpus", str(n)] + rest, comm=EmulatedComm(n))
+        bench.main(["--gpus", str(n)] + rest, comm=EmulatedComm(n, link_gbps=a.link_gbps, p2p_gbps=a.p2p_gbps))
 
 
 if __name__ == "__main__":

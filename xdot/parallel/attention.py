@@ -81,8 +81,10 @@ def _row_chunks(n: int, R: int, hip: bool, nchunks: Optional[int] = None) -> Lis
     one MI355X with emulated 8-rank shapes, 2 chunks cost ≈0.23 ms more compute per step
     (per-chunk mask copies, split partials, half-occupied last workgroup rounds), about what
     the overlap can save over xGMI."""
-    nc = (nchunks or FLAGS.gather_chunks) if (hip and n > 1) else 1
-    nc = max(1, min(nc, R // 64))
+    if n == 1:
+        return [(0, R)]
+    nc = nchunks or (FLAGS.gather_chunks if hip else 1)
+    nc = max(1, min(nc, R if nchunks else R // 64))  # an explicit plan is honoured down to 1-row chunks
     base, extra = divmod(R, nc)
     out, r0 = [], 0
     for c in range(nc):
@@ -146,6 +148,38 @@ def _ref_fwd(k, qg, vg, mask, H, scale):
     return o.transpose(1, 2).reshape(B, R, H * dv).to(k.dtype), lse
 
 
+def _ref_fwd_partial(k, kc, vc, mask, H, scale):
+    """One column segment of the forward in torch: ``kc``/``vc`` (B, Tseg, ·) in the segment's
+    column order, ``mask`` (B, R, Tseg) or None -> (o (B, R, H*dv) normalised over the
+    segment, lse (B, H, R)); a row the segment masks entirely gets o = 0, lse = -inf."""
+    cdt = _cdt(k)
+    B, R, C = k.shape
+    dh = C // H
+    T = kc.shape[1]
+    dv = vc.shape[-1] // H
+    kh = k.view(B, R, H, dh).transpose(1, 2).to(cdt)
+    qh = kc.reshape(B, T, H, dh).transpose(1, 2).to(cdt)
+    vh = vc.reshape(B, T, H, dv).transpose(1, 2).to(cdt)
+    s = torch.matmul(kh, qh.transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s.masked_fill(mask.unsqueeze(1), -float("inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    p = torch.exp(s - lse.clamp_min(torch.finfo(cdt).min).unsqueeze(-1))
+    o = torch.matmul(p, vh)
+    return o.transpose(1, 2).reshape(B, R, H * dv), lse
+
+
+def _ref_combine(parts, dtype):
+    """Merge segment partials [(o, lse)] -> (o in ``dtype``, lse); NaN for fully masked rows."""
+    L = torch.stack([l for _, l in parts])                      # (S, B, H, R)
+    lse = torch.logsumexp(L, dim=0)
+    w = torch.exp(L - lse.unsqueeze(0))                         # NaN only where every segment is -inf
+    B, H, R = lse.shape
+    o = sum(wi.transpose(1, 2).repeat_interleave(oi.shape[-1] // H, dim=-1) * oi
+            for wi, (oi, _) in zip(w, parts))
+    return o.to(dtype), lse
+
+
 def _ref_bwd(do, k, qg, vg, o, lse, mask, H, scale):
     cdt = _cdt(k)
     B, R, C = k.shape
@@ -177,6 +211,79 @@ def _ref_bwd(do, k, qg, vg, o, lse, mask, H, scale):
     return dk, rank_major(dq_all, dh), rank_major(dv_all, dv)
 
 
+def _segment_plan(n: int, rank: int, nchunks: int, local_first: bool) -> List[Tuple[int, int, int]]:
+    """Peer segments (chunk c, source ranks j0..j1-1) of the segmented forward, in launch order;
+    the own rank is left out of every chunk when its block runs first."""
+    plan = []
+    for c in range(nchunks):
+        ranges = [(0, rank), (rank + 1, n)] if local_first else [(0, n)]
+        plan += [(c, j0, j1) for j0, j1 in ranges if j1 > j0]
+    return plan
+
+
+def _mask_cols(B: int, R: int, n: int, j0: int, j1: int, r0: int, rc: int):
+    """Mask columns of source ranks j0..j1-1, rows r0..r0+rc of each (global column j*R + r0 + i)."""
+    return lambda m: m.reshape(B, R, n, R)[..., j0:j1, r0:r0 + rc].reshape(B, R, (j1 - j0) * rc)
+
+
+def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled):
+    """Forward of a multi-rank step as column segments merged by one log-sum-exp combine:
+    the rank's OWN [q|v] block first (it needs no communication, so its partial runs while the
+    all-gather is in flight), then each gathered chunk's peer blocks as soon as that chunk
+    lands.  Every segment is a subset of a row's columns, so the partials (o normalised over
+    the segment, its lse) merge exactly.  -> (o, lse, gathered buffers saved for backward)."""
+    B, R, C = k.shape
+    chunks = pending.chunks
+    local_first = FLAGS.local_first
+    plan = _segment_plan(n, rank, len(chunks), local_first)
+    own = _mask_cols(B, R, n, rank, rank + 1, 0, R)
+    if use_hip:
+        from ..ops import flash
+
+        ops = _ext.ops()
+        widths = ([R] if local_first else []) + [(j1 - j0) * chunks[c][1] for c, j0, j1 in plan]
+        ns = [int(ops.flash_splits(B, R, w, H, False)) for w in widths]
+        opart = torch.empty(sum(ns), B, R, C, dtype=torch.float32, device=k.device)
+        lpart = torch.empty(sum(ns), B, H, R, dtype=torch.float32, device=k.device)
+        slot = [0, 0]  # next partial slot, next entry of ns
+
+        def run(kc, vc, mk):
+            bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
+            nsi = ns[slot[1]]
+            ops.flash_fwd_partial(k, flash._kv(kc), flash._kv(vc), bits, flags, int(H), float(scale), opart, lpart,
+                                  slot[0], nsi, prescaled)
+            slot[0] += nsi
+            slot[1] += 1
+
+        if local_first:
+            mk = flash.prepare_mask_cached(mask, B, R, R, tag=("own", rank, n), view=own)
+            run(qv[..., :C], qv[..., C:], mk)
+        bufs = []
+        for c, (r0, rc) in enumerate(chunks):
+            g = flash.gathered_to_btc(pending.wait(c))          # (B, N*rc, 2C)
+            bufs.append(g)
+            for _, j0, j1 in (p for p in plan if p[0] == c):
+                mk = flash.prepare_mask_cached(mask, B, R, (j1 - j0) * rc, tag=("seg", r0, rc, n, j0, j1),
+                                               view=_mask_cols(B, R, n, j0, j1, r0, rc))
+                seg = g[:, j0 * rc:j1 * rc]
+                run(seg[..., :C], seg[..., C:], mk)
+        o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
+        return o, lse, bufs
+    parts = []
+    if local_first:
+        parts.append(_ref_fwd_partial(k, qv[..., :C], qv[..., C:], None if mask is None else own(mask), H, scale))
+    gs = []
+    for c, (r0, rc) in enumerate(chunks):
+        g = pending.wait(c)                                      # (N, B, rc, 2C)
+        gs.append(g)
+        for _, j0, j1 in (p for p in plan if p[0] == c):
+            seg = _as_global(g[j0:j1])
+            m = None if mask is None else _mask_cols(B, R, n, j0, j1, r0, rc)(mask)
+            parts.append(_ref_fwd_partial(k, seg[..., :C], seg[..., C:], m, H, scale))
+    o, lse = _ref_combine(parts, k.dtype)
+    return o, lse, [torch.cat(gs, dim=2) if len(gs) > 1 else gs[0]]
+
+
 _SIDE = {}
 
 
@@ -201,12 +308,13 @@ class SeqParallelAttention(torch.autograd.Function):
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
         B, R = k.shape[0], k.shape[1]
-        n = comm.world_size
+        n, rank = comm.world_size, comm.rank
         use_hip = _hip_ok(k, qv, H)
         if pending is None:
             pending = _PendingGather(comm, qv, _row_chunks(n, qv.shape[1], use_hip))
         chunks = pending.chunks
         prescaled = False
+        packed_full = None  # the whole-row packed mask, when the caller packed it ahead
         if use_hip:
             from ..ops import flash
 
@@ -216,53 +324,27 @@ class SeqParallelAttention(torch.autograd.Function):
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0)
             if prescaled:
                 k = flash.prescale(k, scale)
-            # masks are packed per chunk while the gathers are in flight (or were packed on a
-            # side stream before the projections: flash.PendingMask)
-            mks = []
             if isinstance(mask, flash.PendingMask):
                 if len(chunks) == 1:
-                    mks.append(mask.get())
+                    packed_full = mask.get()
                 mask = mask.raw
-            for r0, rc in chunks:
-                if mks and len(chunks) == 1:
-                    break
-                if mask is None:
-                    mks.append(None)
-                    continue
-                # chunk columns j*R + r0 + i: a strided slice per source rank (index_select on the
-                # last dim of a (B, R, T) bool tensor is a slow gather); packed once per mask
-                # tensor (flash.MASK_CACHE: re-passing the same mask costs nothing)
-                if len(chunks) == 1:
-                    mks.append(flash.prepare_mask_cached(mask, B, R, n * rc))
-                else:
-                    mks.append(flash.prepare_mask_cached(
-                        mask, B, R, n * rc, tag=(r0, rc, n),
-                        view=lambda m, r0=r0, rc=rc: m.view(B, R, n, R)[..., r0:r0 + rc].reshape(B, R, n * rc)))
-            if len(chunks) == 1:
+        mask = getattr(mask, "raw", mask)
+        segmented = n > 1 and (FLAGS.local_first or len(chunks) > 1)
+        if not segmented:
+            if use_hip:
+                mk = packed_full if packed_full is not None else flash.prepare_mask_cached(mask, B, R, n * R)
                 qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
-                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mks[0], H, scale, prescaled=prescaled)
-                bufs = [qvg]
+                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mk, H, scale, prescaled=prescaled)
+                bufs, mks = [qvg], [mk]
             else:
-                ops = _ext.ops()
-                ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, False))
-                opart = torch.empty(len(chunks) * ns, B, R, C, dtype=torch.float32, device=k.device)
-                lpart = torch.empty(len(chunks) * ns, B, H, R, dtype=torch.float32, device=k.device)
-                bufs = []
-                for c in range(len(chunks)):
-                    g = flash.gathered_to_btc(pending.wait(c))   # (B, N*rc, 2C)
-                    bufs.append(g)
-                    bits, flags = (mks[c].bits, mks[c].flags) if mks[c] is not None else (None, None)
-                    ops.flash_fwd_partial(k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                          float(scale), opart, lpart, c * ns, ns, prescaled)
-                o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
+                qvg = pending.wait(0)                            # (N, B, R, 2C)
+                o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
+                bufs, mks = [qvg], [mask]
         else:
-            mask = getattr(mask, "raw", mask)
-            mks = [mask]
-            qvg = torch.cat(pending.wait_all(), dim=2) if len(chunks) > 1 else pending.wait(0)  # (N, B, R, 2C)
-            o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
-            bufs = [qvg]
+            o, lse, bufs = _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled)
+            mks = [packed_full] if packed_full is not None else None  # backward packs its own (cached)
         ctx.save_for_backward(k, o, lse, *bufs)
-        ctx.mks, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, chunks, H, scale, comm, use_hip
+        ctx.mks, ctx.mask, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, mask, chunks, H, scale, comm, use_hip
         ctx.prescaled = prescaled
         return o
 
@@ -286,6 +368,11 @@ class SeqParallelAttention(torch.autograd.Function):
         if ctx.use_hip:
             from ..ops import flash
 
+            mks = ctx.mks
+            if mks is None:  # segmented forward: the whole-chunk masks (packed once per mask tensor)
+                mks = [flash.prepare_mask_cached(ctx.mask, B, R, n * rc, tag=None if len(chunks) == 1 else (r0, rc, n),
+                                                 view=None if len(chunks) == 1 else _mask_cols(B, R, n, 0, n, r0, rc))
+                       for r0, rc in chunks]
             # δ, then two independent streams: 1) gathered-side grads, chunk by chunk, on a
             # HIGH-priority stream, each chunk followed there by ITS reduce-scatter (chunk c's
             # collective overlaps chunk c+1's kernel), and 2) the row-side dk on the current
@@ -308,7 +395,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     g = bufs[c]
                     # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
                     # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
-                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[c], H, scale, delta,
+                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[c], H, scale, delta,
                                             fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
                     h, oc = reduce_async(flash.btc_to_rank_major(dkv, n), None if dqv is None else dqv[:, r0:r0 + rc])
                     handles.append(h)
@@ -317,7 +404,7 @@ class SeqParallelAttention(torch.autograd.Function):
             delta.record_stream(cur)
             if len(chunks) == 1:
                 g = bufs[0]
-                dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, ctx.mks[0], H, scale,
+                dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
                                     prescaled=ctx.prescaled)
             else:
                 ops = _ext.ops()
@@ -325,7 +412,7 @@ class SeqParallelAttention(torch.autograd.Function):
                 dpart = torch.empty(len(chunks) * ns, B, R, C, dtype=torch.float32, device=k.device)
                 for c in range(len(chunks)):
                     g = bufs[c]
-                    mk = ctx.mks[c]
+                    mk = mks[c]
                     bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                     ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
                                                flags, int(H), float(scale), dpart, c * ns, ns, ctx.prescaled)
@@ -339,7 +426,7 @@ class SeqParallelAttention(torch.autograd.Function):
                 dqv.record_stream(cur)
         else:
             qvg = bufs[0]
-            dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mks[0], H, scale)
+            dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mask, H, scale)
             h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))
             handles = [h]
         for h in handles:

@@ -146,6 +146,9 @@ class LocalComm(Communicator):
         return Handle(out=recv) if async_op else None
 
 
+_LINK = {}
+
+
 class EmulatedComm(LocalComm):
     """Rank ``rank`` of a pretend ``world_size``-rank job on ONE device (diagnostics only).
 
@@ -154,23 +157,87 @@ class EmulatedComm(LocalComm):
     runs exactly the per-rank compute of an N-GPU step, without the transport.  Used by
     ``benchmarks/bench_rank.py`` to study the N=8 per-rank step on the one-GPU box; never
     by tests of numerical results (the math of an emulated job is not a real N-rank job).
+
+    Link model (``link_gbps`` set, GPU tensors): every collective runs on its own "link"
+    stream, ordered after the caller's stream, as a spin of ``bytes on the wire / rate``
+    followed by the copy; ``Handle.wait()`` orders the waiting stream after it.  So the
+    one-GPU timeline shows what overlaps a transfer of that length and what waits for it —
+    the async stream discipline of the RCCL path (a collective's stream, events, recycled
+    buffers) is exercised for real.  Bytes on the wire per rank: all-gather and
+    reduce-scatter ``(N-1)/N`` of the full buffer, all-reduce twice that, at ``link_gbps``
+    (an all-gather bus bandwidth); a ring hop ``send.nbytes`` at ``p2p_gbps`` (one xGMI link).
     """
 
-    def __init__(self, world_size: int, rank: int = 0):
+    def __init__(self, world_size: int, rank: int = 0, link_gbps: Optional[float] = None,
+                 p2p_gbps: Optional[float] = None):
         self.world_size, self.rank = int(world_size), int(rank)
+        self.link_gbps = link_gbps
+        self.p2p_gbps = p2p_gbps or link_gbps
+        self._cycles_per_s = None
 
     @property
     def backend(self):
         return "emulated"
 
+    def _spin_cycles(self, seconds: float, dev) -> int:
+        if self._cycles_per_s is None:  # calibrate torch.cuda._sleep's counter once
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(1000)
+            s.record()
+            torch.cuda._sleep(2_000_000)
+            e.record()
+            e.synchronize()
+            self._cycles_per_s = 2_000_000 / (s.elapsed_time(e) * 1e-3)
+        return int(seconds * self._cycles_per_s)
+
+    def _transfer(self, out, nbytes, rate_gbps, fn, async_op, keep=()):
+        if rate_gbps is None or not out.is_cuda:
+            fn()
+            return Handle(out=out) if async_op else None
+        dev = out.device
+        cur = torch.cuda.current_stream(dev)
+        link = _LINK.get(dev)
+        if link is None:
+            # one high-priority link stream per device for every emulated communicator (as RCCL's
+            # TORCH_NCCL_HIGH_PRIORITY streams): each extra stream takes a hardware queue
+            # (GPU_MAX_HW_QUEUES = 4), and past that streams share queues and serialise
+            link = _LINK[dev] = torch.cuda.Stream(device=dev, priority=-1)
+        link.wait_stream(cur)
+        with torch.cuda.stream(link):
+            cyc = self._spin_cycles(nbytes / (rate_gbps * 1e9), dev)
+            if cyc > 0:
+                torch.cuda._sleep(cyc)
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(link)
+        for t in (out,) + tuple(keep):
+            t.record_stream(link)
+        h = Handle(out=out, post=lambda: torch.cuda.current_stream(dev).wait_event(ev))
+        if async_op:
+            return h
+        h.wait()
+        return None
+
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
-        out.view(self.world_size, -1).copy_(inp.reshape(1, -1).expand(self.world_size, -1))
-        return Handle(out=out) if async_op else None
+        n = self.world_size
+        return self._transfer(out, out.nbytes * (n - 1) // n, self.link_gbps,
+                              lambda: out.view(n, -1).copy_(inp.reshape(1, -1).expand(n, -1)), async_op, (inp,))
 
     def reduce_scatter(self, out, inp, async_op=False):
-        out.view(-1).copy_(inp.reshape(self.world_size, -1)[self.rank])
-        return Handle(out=out) if async_op else None
+        n = self.world_size
+        return self._transfer(out, inp.nbytes * (n - 1) // n, self.link_gbps,
+                              lambda: out.view(-1).copy_(inp.reshape(n, -1)[self.rank]), async_op, (inp,))
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        n = self.world_size
+        return self._transfer(t, 2 * t.nbytes * (n - 1) // n, self.link_gbps, lambda: None, async_op)
+
+    def sendrecv(self, send, recv, dst, src, async_op=False):
+        def hop():
+            if recv.data_ptr() != send.data_ptr():
+                recv.copy_(send)
+        return self._transfer(recv, send.nbytes, self.p2p_gbps, hop, async_op, (send,))
 
     def all_gather_object(self, obj):
         return [obj] * self.world_size

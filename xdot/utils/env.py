@@ -19,6 +19,10 @@
                                overlaps half the gather with the kernels at +0.32 / +0.23 /
                                +0.10 ms of compute per step at N = 2 / 4 / 8 (emulated, T=25000),
                                about what it hides over xGMI: worth it on a slower interconnect)
+``XDOT_LOCAL_FIRST``           ``0``: with several ranks the fused forward waits for the whole
+                               all-gather, then runs one kernel over all T columns (default 1:
+                               the rank's own block runs first, under the gather, then the peer
+                               blocks of each chunk as it lands; one log-sum-exp combine)
 ``XDOT_MASK_ASYNC``            ``1``: pack the attention mask on a side stream, overlapping the
                                projection GEMMs (default off: neutral at N=1, 1.7 % slower at the
                                emulated N=8 rank, profiles/r1_s7_mask_async_ab.md; with several
@@ -65,6 +69,7 @@ class _Flags:
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
         self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
         self.mask_async = _flag("XDOT_MASK_ASYNC")
+        self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
 
