@@ -96,15 +96,31 @@ def _row_chunks(n: int, R: int, hip: bool, nchunks: Optional[int] = None) -> Lis
 
 class _PendingGather:
     """All-gathers of the row chunks of one packed operand, issued back to back on the
-    collective stream; ``wait(c)`` orders the current stream after chunk c only."""
+    collective stream; ``wait(c)`` orders the current stream after chunk c only.
+
+    With several chunks every chunk lands in its own slice of ONE buffer: chunk c's gather
+    output (N, B, rc, ·) starts where chunk c-1's ends, so for B = 1 the buffer read as
+    (1, T, ·) holds every gathered row in (chunk, source rank, row) order — a column
+    permutation of the rank-major order that attention does not see (the mask columns are
+    permuted to match, :func:`_perm_cols`), and the backward runs ONE kernel pair over it."""
 
     def __init__(self, comm, x: Tensor, chunks: List[Tuple[int, int]]):
         self.chunks = chunks
-        self.n = comm.world_size
+        self.n = n = comm.world_size
         x = x.contiguous()
+        self.flat = None
+        if n > 1 and len(chunks) > 1:
+            self.flat = torch.empty(n * x.numel(), dtype=x.dtype, device=x.device)
         self.handles = []
+        off = 0
         for r0, rc in chunks:
-            self.handles.append(_gather_rows(comm, x[:, r0:r0 + rc]))
+            xc = x[:, r0:r0 + rc]
+            if self.flat is None:
+                self.handles.append(_gather_rows(comm, xc))
+                continue
+            out = self.flat[off:off + n * xc.numel()].view((n,) + tuple(xc.shape))
+            off += out.numel()
+            self.handles.append(comm.all_gather_into(out, xc.contiguous(), async_op=True))
         self._bufs: List[Optional[Tensor]] = [None] * len(chunks)
 
     def wait(self, c: int) -> Tensor:
@@ -114,6 +130,21 @@ class _PendingGather:
 
     def wait_all(self) -> List[Tensor]:
         return [self.wait(c) for c in range(len(self.chunks))]
+
+    def permuted(self) -> Optional[Tensor]:
+        """(1, T, ·) view of the single buffer in (chunk, rank, row) column order (B = 1, several
+        chunks, every chunk waited for), else None."""
+        if self.flat is None or self._bufs[0].shape[1] != 1 or any(b is None for b in self._bufs):
+            return None
+        return self.flat.view(1, -1, self._bufs[0].shape[-1])
+
+
+def _perm_cols(B: int, R: int, n: int, chunks: List[Tuple[int, int]]):
+    """Mask columns in the (chunk, source rank, row) order of :meth:`_PendingGather.permuted`."""
+    def view(m):
+        m4 = m.reshape(B, R, n, R)
+        return torch.cat([m4[..., r0:r0 + rc].reshape(B, R, n * rc) for r0, rc in chunks], dim=-1)
+    return view
 
 
 def _as_global(g: Tensor) -> Tensor:
@@ -268,7 +299,8 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
                 seg = g[:, j0 * rc:j1 * rc]
                 run(seg[..., :C], seg[..., C:], mk)
         o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
-        return o, lse, bufs
+        perm = pending.permuted()
+        return o, lse, ([perm] if perm is not None else bufs)
     parts = []
     if local_first:
         parts.append(_ref_fwd_partial(k, qv[..., :C], qv[..., C:], None if mask is None else own(mask), H, scale))
@@ -368,41 +400,61 @@ class SeqParallelAttention(torch.autograd.Function):
         if ctx.use_hip:
             from ..ops import flash
 
+            one = len(bufs) == 1  # one gathered buffer: natural order, or chunks permuted (B = 1)
             mks = ctx.mks
-            if mks is None:  # segmented forward: the whole-chunk masks (packed once per mask tensor)
-                mks = [flash.prepare_mask_cached(ctx.mask, B, R, n * rc, tag=None if len(chunks) == 1 else (r0, rc, n),
-                                                 view=None if len(chunks) == 1 else _mask_cols(B, R, n, 0, n, r0, rc))
-                       for r0, rc in chunks]
-            # δ, then two independent streams: 1) gathered-side grads, chunk by chunk, on a
-            # HIGH-priority stream, each chunk followed there by ITS reduce-scatter (chunk c's
-            # collective overlaps chunk c+1's kernel), and 2) the row-side dk on the current
-            # stream.  2) fills the partly occupied last workgroup rounds of 1) while the
-            # priority keeps 1) (and so the collectives) nearly as early as when it runs
-            # alone.  δ runs on the priority stream too, so 1) reaches the GPU first.
+            if mks is None or (one and len(chunks) > 1):  # segmented forward: masks packed here (cached)
+                if one:
+                    mks = [flash.prepare_mask_cached(ctx.mask, B, R, n * R,
+                                                     tag=None if len(chunks) == 1 else ("perm", tuple(chunks), n),
+                                                     view=None if len(chunks) == 1 else _perm_cols(B, R, n, chunks))]
+                else:
+                    mks = [flash.prepare_mask_cached(ctx.mask, B, R, n * rc, tag=(r0, rc, n),
+                                                     view=_mask_cols(B, R, n, 0, n, r0, rc)) for r0, rc in chunks]
+            # δ, then two independent streams: 1) gathered-side grads on a HIGH-priority stream,
+            # followed there by their reduce-scatter(s), and 2) the row-side dk on the current
+            # stream.  2) fills the partly occupied last workgroup rounds of 1) and hides the
+            # reduce-scatter, while the priority keeps 1) (and so the collective) nearly as
+            # early as when it runs alone.  δ runs on the priority stream too, so 1) reaches
+            # the GPU first.  Per-chunk kernels (chunk c's reduce-scatter under chunk c+1's
+            # kernel) only when the chunks are separate buffers (B > 1).
             cur = torch.cuda.current_stream(do.device)
             hi = _side_stream(do.device)
             hi.wait_stream(cur)
             handles, outs = [], []
+            gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
             with torch.cuda.stream(hi):
                 delta = flash.bwd_delta(do, o, H)
                 ev = torch.cuda.Event()
                 ev.record(hi)
                 dqv = None
                 if n > 1 and len(chunks) > 1 and B == 1:
-                    dqv = torch.empty(B, R, 2 * C, dtype=k.dtype if not FLAGS.grad_fp32 else torch.float32,
-                                      device=k.device)
-                for c, (r0, rc) in enumerate(chunks):
-                    g = bufs[c]
-                    # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
-                    # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
-                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[c], H, scale, delta,
+                    dqv = torch.empty(B, R, 2 * C, dtype=gdt, device=k.device)
+                # partials rounded once to the compute dtype in the kernel (XDOT_GRAD_FP32=1
+                # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
+                if one:
+                    g = bufs[0]
+                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
                                             fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
-                    h, oc = reduce_async(flash.btc_to_rank_major(dkv, n), None if dqv is None else dqv[:, r0:r0 + rc])
-                    handles.append(h)
-                    outs.append(oc)
+                    off = 0
+                    for r0, rc in chunks:  # (chunk, rank, row) order: chunk c's ranks are contiguous
+                        part = dkv if len(chunks) == 1 else dkv[:, off:off + n * rc]
+                        off += n * rc
+                        h, oc = reduce_async(flash.btc_to_rank_major(part, n),
+                                             None if dqv is None else dqv[:, r0:r0 + rc])
+                        handles.append(h)
+                        outs.append(oc)
+                else:
+                    for c, (r0, rc) in enumerate(chunks):
+                        g = bufs[c]
+                        dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[c], H, scale, delta,
+                                                fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
+                        h, oc = reduce_async(flash.btc_to_rank_major(dkv, n),
+                                             None if dqv is None else dqv[:, r0:r0 + rc])
+                        handles.append(h)
+                        outs.append(oc)
             cur.wait_event(ev)
             delta.record_stream(cur)
-            if len(chunks) == 1:
+            if one:
                 g = bufs[0]
                 dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
                                     prescaled=ctx.prescaled)
