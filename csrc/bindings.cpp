@@ -248,7 +248,8 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   TORCH_CHECK(rows.is_cuda() && kc.is_cuda() && vc.is_cuda(), "xdot.flash: GPU tensors required");
   TORCH_CHECK(rows.is_contiguous(), "xdot.flash: rows must be contiguous");
   TORCH_CHECK(rows.scalar_type() == kc.scalar_type() && rows.scalar_type() == vc.scalar_type(), "xdot.flash: dtype mismatch");
-  TORCH_CHECK(rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kHalf, "xdot.flash: bf16/fp16 only");
+  TORCH_CHECK(rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kHalf || rows.scalar_type() == at::kFloat,
+              "xdot.flash: bf16/fp16/fp32 only");
   TORCH_CHECK(rows.dim() == 3 && kc.dim() == 3 && vc.sizes() == kc.sizes(), "xdot.flash: rows (B,R,C), cols (B,T,C)");
   FlashGeom g{rows.size(0), rows.size(1), rows.size(2), kc.size(1), 0, kc.stride(1)};
   TORCH_CHECK(kc.size(0) == g.B && kc.size(2) == g.C, "xdot.flash: batch / feature mismatch");
@@ -375,7 +376,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
     delta = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   }
   a.dkc = dkv.data_ptr(); a.dvc = static_cast<char*>(dkv.data_ptr()) + g.C * dkv.element_size(); a.ldg = 2 * g.C;
-  a.dkv16 = fp32_out ? 0 : 1;
+  a.dkv16 = (fp32_out || rows.scalar_type() == at::kFloat) ? 0 : 1;
   a.delta = delta.data_ptr<float>();
   auto lse2 = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   a.lse2 = lse2.data_ptr<float>();

@@ -667,6 +667,7 @@ extern "C" int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const voi
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (dt == DT_F32) return xdot_flash_bwd_prep_f32_launch(a, out, delta, D, st);
 #define XP(DTV, DV) launch_bwd_delta<DTV, DV>(*a, out, delta, st)
   XB_DISPATCH(XP)
 #undef XP
@@ -676,6 +677,7 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (dt == DT_F32) return xdot_flash_bwd_cols_f32_launch(a, D, st);
 #define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
 #undef XC
@@ -686,6 +688,7 @@ extern "C" int xdot_flash_bwd_rows_sum_launch(const xdot::fa::BwdArgs* a, int dt
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (dt == DT_F32) return xdot_flash_rows_sum_f32_launch(a, D, st);
 #define XS(DTV, DV) launch_rows_sum<DTV, DV>(*a, st)
   XB_DISPATCH(XS)
 #undef XS
@@ -695,6 +698,11 @@ extern "C" int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (dt == DT_F32) {
+    const int rc = xdot_flash_bwd_rows_f32_launch(a, D, st);
+    if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_rows_sum_f32_launch(a, D, st);
+    return rc;
+  }
 #define XR(DTV, DV) launch_bwd_rows<DTV, DV>(*a, st)
   XB_DISPATCH(XR)
 #undef XR

@@ -1,0 +1,537 @@
+// xdot — fp32 flash attention (forward + both backward kernels) for gfx950 (MI355X).
+//
+// The reference computes the module in fp32 only (distributed_dot_product/module.py:60-71 on
+// the fp32 buffers of multiplication/functions.py:86,198).  The 16-bit kernels in
+// flash_fwd.hip / flash_bwd.hip would round fp32 operands to 8 significant bits; these kernels
+// keep every product exact in fp32 with v_mfma_f32_32x32x2_f32 (an fmaf chain, 64 FLOP/clk/SIMD
+// = the fp32 vector rate, 1/16 of bf16), so an fp32 module never falls back to materialising
+// the (B, H, R, T) scores (20 GB per tensor at T = 25000, impossible at T = 200000).
+//
+// Same decomposition, layouts, masks and partial/combine protocol as the 16-bit kernels
+// (rows = this rank's R query-side rows, cols = the T gathered key/value rows, head-interleaved
+// (B, ·, H*D) tensors, packed masks from mask_pack.hip), restructured for the f32 MFMA:
+//   * 32x32x2: lane l of the A operand holds A[l&31][l>>5], of B B[l>>5][l&31]; the C/D map
+//     is the 32x32x16 one (lane = column l&31, register r = row (r&3)+8(r>>2)+4(l>>5)), so the
+//     transposed-score trick of the 16-bit kernels carries over: softmax rows stay lane-local;
+//   * the K index of a product over the head dim is permuted so that every lane fetches four
+//     consecutive floats with ONE ds_read_b128 per four MFMAs (MFMA 4g+t, lane half h, uses
+//     d = 8g + 4h + t, for the LDS image AND the register-resident fragments);
+//   * a product over a 32-row/column tile index takes its B operand straight from the previous
+//     product's accumulator register (MFMA s uses tile index (s&3)+8(s>>2)+4h = register s's
+//     row) and its A operand with one ds_read_b32 from the image, read "transposed";
+//   * images are 32 rows x (D + 4) floats: the 4-float pad makes the 16-lane ds_read_b128
+//     groups conflict-free ((D+4)/4 odd);
+//   * 32-row tiles staged global -> VGPR -> LDS one tile ahead (double-buffered LDS, one
+//     barrier per tile): at 64+ MFMA cycles per 64-bit of operand this kernel family is MFMA
+//     bound, so the simple staging costs nothing measurable.
+#include "flash_common.h"
+
+namespace xdot {
+namespace fa32 {
+
+using fa::FwdArgs;
+using fa::BwdArgs;
+using fa::LOG2E;
+using fa::LN2;
+using fa::pair_max;
+using fa::pair_sum;
+
+__device__ __forceinline__ f32x16 mm(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int D> struct Cfg {
+  static constexpr int P = D + 4;       // image row stride (floats)
+  static constexpr int IMG = 32 * P;    // one 32-row image
+  static constexpr int KG = D / 8;      // b128 groups over the head dim (4 MFMAs each)
+  static constexpr int DB = D / 32;     // 32-wide output blocks
+  static constexpr int NC = D / 32;     // f32x4 chunks per thread per image (256 threads)
+  static constexpr int AUX = 64;        // per-stage row constants (lse2, delta) of the column kernel
+  static constexpr int STAGE = 2 * IMG + AUX;
+};
+
+// two 32-row images (rows row0.., clamped to row0 + rmax) global -> registers -> LDS
+template <int D> struct Stager {
+  using CF = Cfg<D>;
+  f32x4 r[2][CF::NC];
+  __device__ __forceinline__ void load(const float* b0, const float* b1, int64_t ld, int64_t row0, int rmax, int tid) {
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      const int64_t off = (row0 + min(row, rmax)) * ld + 4 * c;
+      r[0][i] = *reinterpret_cast<const f32x4*>(b0 + off);
+      r[1][i] = *reinterpret_cast<const f32x4*>(b1 + off);
+    }
+  }
+  __device__ __forceinline__ void store(float* img, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      *reinterpret_cast<f32x4*>(img + row * CF::P + 4 * c) = r[0][i];
+      *reinterpret_cast<f32x4*>(img + CF::IMG + row * CF::P + 4 * c) = r[1][i];
+    }
+  }
+};
+
+// register-resident fragments of one 32-row block: f[4g + t] = X[row][8g + 4h + t]
+template <int D>
+__device__ __forceinline__ void load_frag(float (&f)[D / 2], const float* p, bool ok) {
+#pragma unroll
+  for (int g = 0; g < D / 8; ++g) {
+    const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(p + 8 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) f[4 * g + t] = v[t];
+  }
+}
+
+// acc += img rows (lane&31) · fragᵀ over the head dim (A from the image, B from registers)
+template <int D>
+__device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D / 2], f32x16 acc, int lane) {
+  const float* p = img + (lane & 31) * Cfg<D>::P + 4 * (lane >> 5);
+#pragma unroll
+  for (int g = 0; g < D / 8; ++g) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p + 8 * g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = mm(a[t], f[4 * g + t], acc);
+  }
+  return acc;
+}
+
+// out[db] += imgᵀ (d x tile index) · x (tile index x lane column), x = an accumulator tile
+template <int D>
+__device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16 (&out)[D / 32], int lane) {
+  const int hf = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const float* row = img + ((s & 3) + 8 * (s >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) out[db] = mm(row[db * 32], x[s], out[db]);
+  }
+}
+
+// tile index of accumulator register r for lane half hf
+__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
+
+// flag of (32-row block rb32, 64-col tile kt64): 0 none / 1 all / 2 some masked
+__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
+  return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
+}
+
+// ------------------------------------------------------------------------------------------
+// forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
+template <int D>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
+  using CF = Cfg<D>;
+  constexpr int DB = CF::DB;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+
+  float kf[D / 2];
+  load_frag<D>(kf, reinterpret_cast<const float*>(a.rows) + ((int64_t)b * a.R + (row_ok ? row : 0)) * C + h * D + 4 * hf,
+               row_ok);
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* vb = reinterpret_cast<const float*>(a.vc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  float m_run = NEG_INF, l_run = 0.f;
+  f32x16 o[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) o[i] = f32x16{};
+
+  Stager<D> st;
+  if (kt_beg < kt_end) {
+    st.load(qb, vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    st.store(sm, tid);
+    __syncthreads();
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (more) st.load(qb, vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    const float* qi = sm + ((kt - kt_beg) & 1) * CF::STAGE;
+    const float* vi = qi + CF::IMG;
+    int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
+      const int valid = a.T - kt * 32;
+      if (flag == 2 || valid < 32) {
+        uint32_t w = 0;
+        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = tidx(r, hf);
+          if (((w >> c) & 1u) || c >= valid) s[r] = NEG_INF;
+        }
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+      mx = pair_max(mx) * c2;
+      const float m_new = fmaxf(m_run, mx);
+      if (m_new > m_run) {
+        const float alpha = ex2(m_run - m_new);  // m_run = -inf: 0
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < DB; ++i) o[i] *= alpha;
+        m_run = m_new;
+      }
+      const float m_use = m_run == NEG_INF ? 0.f : m_run;
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = ex2(__builtin_fmaf(s[r], c2, -m_use));
+        ls += s[r];
+      }
+      l_run += ls;
+      trprod<D>(vi, s, o, lane);  // Oᵀ += Vᵀ · Pᵀ
+    }
+    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
+    __syncthreads();
+  }
+
+  const float l_tot = pair_sum(l_run);
+  const float inv = 1.f / l_tot;
+  if (!row_ok) return;
+  const float lse = (m_run + __log2f(l_tot)) * LN2;
+  float* op;
+  if (a.nsplit == 1 && !a.force_partial) {
+    op = reinterpret_cast<float*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
+    if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = lse;
+  } else {
+    op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
+    if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = lse;
+  }
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
+}
+
+// merge split partials (fp32 out); see flash_fwd_combine
+__global__ __launch_bounds__(256) void combine_kernel(FwdArgs a, int D) {
+  const int C = a.H * D;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.R * (C / 4);
+  if (idx >= total) return;
+  const int c4 = (int)(idx % (C / 4));
+  const int64_t br = idx / (C / 4);
+  const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int h = (c4 * 4) / D;
+  const int64_t lstride = (int64_t)a.B * a.H * a.R, ostride = (int64_t)a.B * a.R * C;
+  const float* lp = a.lpart + ((int64_t)b * a.H + h) * a.R + row;
+  float mx = -__builtin_inff();
+  for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, lp[s * lstride]);
+  float sum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* opp = a.opart + br * C + c4 * 4;
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float l = lp[s * lstride];
+    if (l == -__builtin_inff()) continue;
+    const float wgt = __expf(l - mx);
+    sum += wgt;
+    acc += wgt * *reinterpret_cast<const f32x4*>(opp + s * ostride);
+  }
+  const float inv = 1.f / sum;  // fully masked row: NaN output, -inf lse (as the reference)
+  f32x4 v = acc * inv;
+  if (sum == 0.f) v = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+  *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.out) + br * C + c4 * 4) = v;
+  if ((c4 * 4) % D == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
+}
+
+// δ = rowsum(dO ⊙ O) (unless delta == nullptr) and lse2 = lse * log2 e, per (b, h, row)
+__global__ __launch_bounds__(256) void prep_kernel(BwdArgs a, const float* out, float* delta, int D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)a.B * a.R * a.H) return;
+  const int h = (int)(idx % a.H);
+  const int64_t br = idx / a.H;
+  const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int64_t li = ((int64_t)b * a.H + h) * a.R + row;
+  if (a.lse2) a.lse2[li] = a.lse[li] * LOG2E;
+  if (!delta) return;
+  const float* o = out + br * (int64_t)(a.H * D) + h * D;
+  const float* d = reinterpret_cast<const float*>(a.dout) + br * (int64_t)(a.H * D) + h * D;
+  float acc = 0.f;
+  for (int c = 0; c < D; c += 4) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(o + c), y = *reinterpret_cast<const f32x4*>(d + c);
+    acc += x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3];
+  }
+  delta[li] = acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, row side: dK = scale · Σ_cols dS · Q_cols.  4 waves x 32 rows, column split.
+template <int D>
+__global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  constexpr int DB = CF::DB;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+
+  float kf[D / 2], df[D / 2];
+  {
+    const int64_t off = ((int64_t)b * a.R + (row_ok ? row : 0)) * C + h * D + 4 * hf;
+    load_frag<D>(kf, reinterpret_cast<const float*>(a.rows) + off, row_ok);
+    load_frag<D>(df, reinterpret_cast<const float*>(a.dout) + off, row_ok);
+  }
+  const int64_t li = ((int64_t)b * a.H + h) * a.R + (row_ok ? row : 0);
+  const float lse2 = row_ok ? a.lse[li] * LOG2E : 0.f, dlt = row_ok ? a.delta[li] : 0.f;
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* vb = reinterpret_cast<const float*>(a.vc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+
+  Stager<D> st;
+  if (kt_beg < kt_end) {
+    st.load(qb, vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    st.store(sm, tid);
+    __syncthreads();
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (more) st.load(qb, vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    const float* qi = sm + ((kt - kt_beg) & 1) * CF::STAGE;
+    const float* vi = qi + CF::IMG;
+    int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D>(qi, kf, f32x16{}, lane);   // Sᵀ  (col x row)
+      f32x16 dp = rowprod<D>(vi, df, f32x16{}, lane);  // dPᵀ (col x row)
+      const int valid = a.T - kt * 32;
+      uint32_t w = 0;
+      const bool chk = flag == 2 || valid < 32;
+      if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = __builtin_fmaf(s[r], c2, -lse2);
+        if (chk) {
+          const int c = tidx(r, hf);
+          if (((w >> c) & 1u) || c >= valid) x = NEG_INF;
+        }
+        s[r] = ex2(x) * (dp[r] - dlt);  // dSᵀ / scale
+      }
+      trprod<D>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+    }
+    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
+    __syncthreads();
+  }
+  if (!row_ok) return;
+  float* op = (a.nsplit > 1 || a.force_partial) ? a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D
+                                                : reinterpret_cast<float*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dk[db][4 * g] * sc, dk[db][4 * g + 1] * sc, dk[db][4 * g + 2] * sc, dk[db][4 * g + 3] * sc};
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, gathered side: dQ_cols = scale · Σ_rows dSᵀ · K_rows, dV_cols = Σ_rows Pᵀ · dO.
+// 4 waves x 32 columns of one (b, h); sweeps 32-row tiles of K_rows / dO + their lse2 / δ.
+template <int D>
+__global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  constexpr int DB = CF::DB;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = (a.T + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = lin % ncb, bh = lin / ncb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
+  const bool col_ok = col < a.T;
+  const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
+  const int NRT = (a.R + 31) / 32;
+
+  float qf[D / 2], vf[D / 2];
+  {
+    const int64_t off = ((int64_t)b * a.T + (col_ok ? col : 0)) * a.ldkv + h * D + 4 * hf;
+    load_frag<D>(qf, reinterpret_cast<const float*>(a.kc) + off, col_ok);
+    load_frag<D>(vf, reinterpret_cast<const float*>(a.vc) + off, col_ok);
+  }
+  const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
+  const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
+  const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
+  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dq[DB], dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) { dq[i] = f32x16{}; dv[i] = f32x16{}; }
+
+  // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
+  auto aux_load = [&](int rt) -> float {
+    const int rr = rt * 32 + (tid & 31);
+    if (tid < 32) return rr < a.R ? lse2[rr] : __builtin_inff();
+    if (tid < 64) return rr < a.R ? dlt[rr] : 0.f;
+    return 0.f;
+  };
+  Stager<D> st;
+  float ax = 0.f;
+  if (NRT > 0) {
+    st.load(kb, db_, C, 0, a.R - 1, tid);
+    ax = aux_load(0);
+    st.store(sm, tid);
+    if (tid < 64) sm[2 * CF::IMG + tid] = ax;
+    __syncthreads();
+  }
+  for (int rt = 0; rt < NRT; ++rt) {
+    const bool more = rt + 1 < NRT;
+    if (more) {
+      st.load(kb, db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      ax = aux_load(rt + 1);
+    }
+    const float* ki = sm + (rt & 1) * CF::STAGE;
+    const float* di = ki + CF::IMG;
+    const float* ls = ki + 2 * CF::IMG;  // lse2[32], δ[32]
+    int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D>(ki, qf, f32x16{}, lane);   // S  (row x col)
+      f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
+      uint32_t w = 0;
+      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = tidx(r, hf);
+        float x = __builtin_fmaf(s[r], c2, -ls[i]);
+        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
+        const float p = ex2(x);
+        s[r] = p;
+        dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
+      }
+      trprod<D>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
+      trprod<D>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+    }
+    if (more) {
+      float* nx = sm + ((rt + 1) & 1) * CF::STAGE;
+      st.store(nx, tid);
+      if (tid < 64) nx[2 * CF::IMG + tid] = ax;
+    }
+    __syncthreads();
+  }
+  if (!col_ok) return;
+  float* pq = reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dq[db][4 * g] * sc, dq[db][4 * g + 1] * sc, dq[db][4 * g + 2] * sc, dq[db][4 * g + 3] * sc};
+      *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+    }
+}
+
+// sum a.nsplit slots of a.dpart into the fp32 row-side grad
+__global__ __launch_bounds__(256) void rows_sum_kernel(BwdArgs a, int D) {
+  const int64_t total4 = (int64_t)a.B * a.R * a.H * D / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total4) return;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(a.dpart + idx * 4);
+  for (int s = 1; s < a.nsplit; ++s) acc += *reinterpret_cast<const f32x4*>(a.dpart + s * total4 * 4 + idx * 4);
+  *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.drows) + idx * 4) = acc;
+}
+
+template <int D> constexpr int lds_bytes() { return 2 * Cfg<D>::STAGE * 4; }
+
+}  // namespace fa32
+}  // namespace xdot
+
+#define XF32_DISPATCH(CALL)            \
+  switch (D) {                         \
+    case 32: CALL(32); return 0;       \
+    case 64: CALL(64); return 0;       \
+    case 96: CALL(96); return 0;       \
+    case 128: CALL(128); return 0;     \
+    default: return -1;                \
+  }
+
+extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa32;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
+  const int nrb = (a->R + 127) / 128;
+  const dim3 grid(nrb * a->B * a->H * a->nsplit);
+#define L(DV) hipLaunchKernelGGL(fwd_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
+  XF32_DISPATCH(L)
+#undef L
+}
+
+extern "C" int xdot_flash_combine_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st) {
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  const int64_t n = (int64_t)a->B * a->R * (a->H * D / 4);
+  hipLaunchKernelGGL(xdot::fa32::combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a, D);
+  return 0;
+}
+
+extern "C" int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int D,
+                                              hipStream_t st) {
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  const int64_t n = (int64_t)a->B * a->R * a->H;
+  hipLaunchKernelGGL(xdot::fa32::prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a,
+                     reinterpret_cast<const float*>(out), delta, D);
+  return 0;
+}
+
+extern "C" int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa32;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (a->prescaled) return -1;
+  const int nrb = (a->R + 127) / 128;
+  const dim3 grid(nrb * a->B * a->H * a->nsplit);
+#define L(DV) hipLaunchKernelGGL(bwd_rows_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
+  XF32_DISPATCH(L)
+#undef L
+}
+
+extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa32;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (a->prescaled || a->dkv16) return -1;
+  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+#define L(DV) hipLaunchKernelGGL(bwd_cols_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
+  XF32_DISPATCH(L)
+#undef L
+}
+
+extern "C" int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
+  if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  const int64_t n4 = (int64_t)a->B * a->R * a->H * D / 4;
+  hipLaunchKernelGGL(xdot::fa32::rows_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, *a, D);
+  return 0;
+}

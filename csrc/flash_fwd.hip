@@ -643,6 +643,7 @@ extern "C" int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt,
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (dt == DT_F32 && !a->out32) return xdot_flash_combine_f32_launch(a, D, st);
 #define XF(DTV, DV) if (dt == DTV && D == DV) { launch_combine<DTV, DV>(*a, st); return 0; }
   XF(DT_BF16, 32) XF(DT_BF16, 64) XF(DT_BF16, 96) XF(DT_BF16, 128)
   XF(DT_F16, 32) XF(DT_F16, 64) XF(DT_F16, 96) XF(DT_F16, 128)
@@ -654,6 +655,11 @@ extern "C" int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, 
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (dt == DT_F32) {
+    const int rc = xdot_flash_fwd_f32_launch(a, D, st);
+    if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_combine_f32_launch(a, D, st);
+    return rc;
+  }
 #define XF(DTV, DV) if (dt == DTV && D == DV) { launch_fwd<DTV, DV>(*a, st); return 0; }
   XF(DT_BF16, 32) XF(DT_BF16, 64) XF(DT_BF16, 96) XF(DT_BF16, 128)
   XF(DT_F16, 32) XF(DT_F16, 64) XF(DT_F16, 96) XF(DT_F16, 128)

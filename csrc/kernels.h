@@ -133,4 +133,11 @@ int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
 int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
 // sum a->nsplit slots of a->dpart into a->drows
 int xdot_flash_bwd_rows_sum_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
+// exact-fp32 flash family (csrc/flash_f32.hip); the launchers above route DT_F32 here
+int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st);
+int xdot_flash_combine_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st);
+int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int D, hipStream_t st);
+int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 }

@@ -1,0 +1,176 @@
+"""Exact-fp32 flash kernels (csrc/flash_f32.hip) vs an fp64 PyTorch reference (GPU only).
+
+The reference module runs in fp32 (module.py:60-71); here fp32 inputs stay fp32 through the
+fused path (v_mfma_f32_32x32x2_f32), so the bound is fp32 accuracy: relative Frobenius error
+<= 2e-5 on outputs and gradients (bf16 kernels: ~1e-2).  Head dims 32-128, ragged R / T, rank-
+major gathered layouts, masks with fully masked tiles, column splits, a fully masked row
+(NaN parity), the module's default fp32 path, and T = 200000 at the N=8 per-rank shape.
+"""
+import math
+
+import pytest
+import torch
+
+from test_flash_gpu import CASES, _to_gathered
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+
+def _ref64(rows, kc, vc, mask, H, scale):
+    N, B, Rc, C = kc.shape
+    R, D, T = rows.shape[1], C // H, N * Rc
+    k = rows.double().view(B, R, H, D).transpose(1, 2).clone().requires_grad_(True)
+    q = kc.double().permute(1, 0, 2, 3).reshape(B, T, H, D).transpose(1, 2).clone().requires_grad_(True)
+    v = vc.double().permute(1, 0, 2, 3).reshape(B, T, H, D).transpose(1, 2).clone().requires_grad_(True)
+    s = (k @ q.transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s.masked_fill(mask.unsqueeze(1), -float("inf"))
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ v
+    return k, q, v, o.transpose(1, 2).reshape(B, R, C), lse
+
+
+def _inputs(case, mask_kind, gpu):
+    B, R, N, Rc, H, D = case
+    C, T = H * D, N * Rc
+    g = torch.Generator(device="cpu").manual_seed(sum(case) + 1)
+    rows = torch.randn(B, R, C, generator=g).to(gpu)
+    kc = torch.randn(N, B, Rc, C, generator=g).to(gpu)
+    vc = torch.randn(N, B, Rc, C, generator=g).to(gpu)
+    do = torch.randn(B, R, C, generator=g).to(gpu)
+    mask = None
+    if mask_kind == "random":
+        mask = torch.rand(B, R, T, generator=g) < 0.4
+    elif mask_kind == "blocks":
+        mask = torch.zeros(B, R, T, dtype=torch.bool)
+        mask[:, :, : min(T, 128)] = True
+        r1 = min(R, 90)
+        mask[:, 40:r1, 128:] = torch.rand(B, r1 - 40, max(0, T - 128), generator=g) < 0.5
+    if mask is not None:
+        mask[..., T - 1] = False
+        mask = mask.to(gpu)
+    return rows, kc, vc, do, mask
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
+def test_flash_f32_fwd_bwd(gpu, case, mask_kind):
+    from xdot.ops import flash
+
+    B, R, N, Rc, H, D = case
+    T = N * Rc
+    rows, kc, vc, do, mask = _inputs(case, mask_kind, gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    out, lse = flash.fwd(rows, kb, vb, mk, H, scale)
+    assert out.dtype == torch.float32
+    k, q, v, ref_o, ref_lse = _ref64(rows, kc, vc, mask, H, scale)
+    assert _rel(out, ref_o) <= 2e-5, f"fwd out {_rel(out, ref_o):.2e}"
+    assert (lse.double() - ref_lse).abs().max().item() < 1e-5
+    drows, dkc, dvc = flash.bwd(do, rows, kb, vb, out, lse, mk, H, scale)
+    dkc, dvc = flash.btc_to_rank_major(dkc, N), flash.btc_to_rank_major(dvc, N)
+    ref_o.backward(do.double())
+    for what, got, ref in (("d rows", drows, k.grad.transpose(1, 2).reshape(B, R, H * D)),
+                           ("d cols (q)", dkc, _to_gathered(q.grad, N, B, Rc, H * D)),
+                           ("d cols (v)", dvc, _to_gathered(v.grad, N, B, Rc, H * D))):
+        assert got.dtype == torch.float32
+        assert _rel(got, ref) <= 2e-5, f"{what}: {_rel(got, ref):.2e}"
+
+
+@pytest.mark.parametrize("nsplit", [2, 5])
+def test_flash_f32_column_split(gpu, nsplit):
+    from xdot.ops import flash
+
+    case = (1, 150, 1, 1000, 2, 96)
+    rows, kc, vc, do, mask = _inputs(case, "blocks", gpu)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    mk = flash.prepare_mask(mask, 1, 150, 1000)
+    o1, l1 = flash.fwd(rows, kb, vb, mk, 2, 0.1, nsplit=1)
+    o2, l2 = flash.fwd(rows, kb, vb, mk, 2, 0.1, nsplit=nsplit)
+    assert _rel(o2, o1) <= 1e-6 and (l1 - l2).abs().max().item() < 1e-5
+    dkv, delta = flash.bwd_cols(do, rows, kb, vb, o1, l1, mk, 2, 0.1)
+    d1 = flash.bwd_rows(do, rows, kb, vb, l1, delta, mk, 2, 0.1, nsplit=1)
+    d2 = flash.bwd_rows(do, rows, kb, vb, l1, delta, mk, 2, 0.1, nsplit=nsplit)
+    assert _rel(d2, d1) <= 1e-6
+
+
+def test_flash_f32_fully_masked_row_nan(gpu):
+    from xdot.ops import flash
+
+    rows = torch.randn(1, 64, 128, device=gpu)
+    kc = torch.randn(1, 96, 128, device=gpu)
+    mask = torch.zeros(1, 64, 96, dtype=torch.bool, device=gpu)
+    mask[0, 5] = True
+    out, _ = flash.fwd(rows, kc, kc, flash.prepare_mask(mask, 1, 64, 96), 2, 0.125)
+    assert torch.isnan(out[0, 5]).all() and not torch.isnan(out[0, 4]).any()
+
+
+def test_module_fp32_default_is_fused_and_exact(gpu):
+    """An fp32 module takes the fused path by default (no (B,H,R,T) scores) and matches the
+    fp64 dense module: outputs, input grads and all eight parameter grads."""
+    import xdot
+    from xdot.utils.comm import LocalComm, use_comm
+
+    torch.manual_seed(0)
+    D, H, T = 384, 4, 500
+    with use_comm(LocalComm()):
+        m = xdot.DistributedDotProductAttn(D, num_heads=H, add_bias=True).to(gpu)
+        x = torch.randn(1, T, D, device=gpu, requires_grad=True)
+        assert m._pick_impl(x) == "flash"
+        ref = xdot.DistributedDotProductAttn(D, num_heads=H, add_bias=True, distributed=False,
+                                             impl="materialized").to(gpu, torch.float64)
+        ref.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+        mask = torch.rand(1, T, T, device=gpu) < 0.3
+        mask[..., 0] = False
+        out = m(x, x, x, mask)
+        out.square().sum().backward()
+        xd = x.detach().double().requires_grad_(True)
+        ro = ref(xd, xd, xd, mask)
+        ro.square().sum().backward()
+    assert _rel(out, ro) <= 1e-5
+    assert _rel(x.grad, xd.grad) <= 1e-4
+    rg = {n: q.grad for n, q in ref.named_parameters()}
+    for n, p in m.named_parameters():
+        if n == "queries.bias":  # exactly zero in exact arithmetic (softmax shift invariance)
+            assert (p.grad.double() - rg[n]).norm().item() <= 1e-4 * rg["keys.bias"].norm().item()
+            continue
+        assert _rel(p.grad, rg[n]) <= 1e-4, n
+
+
+def test_flash_f32_long_context_sampled(gpu):
+    """T = 200000 in fp32 at the N=8 per-rank shape (R = 25000): no score tensor exists (a
+    materialised fp32 (R, T) block alone would be 20 GB per head); sampled rows/columns are
+    recomputed exactly in fp64."""
+    from xdot.ops import flash
+
+    R, T, H, D = 25_000, 200_000, 1, 96
+    scale = 1.0 / math.sqrt(D)
+    g = torch.Generator(device=gpu).manual_seed(7)
+    rows = torch.randn(1, R, D, device=gpu, generator=g)
+    kc = torch.randn(1, T, D, device=gpu, generator=g)
+    vc = torch.randn(1, T, D, device=gpu, generator=g)
+    do = torch.randn(1, R, D, device=gpu, generator=g)
+    out, lse = flash.fwd(rows, kc, vc, None, H, scale)
+    dkv, delta = flash.bwd_cols(do, rows, kc, vc, out, lse, None, H, scale)
+    drows = flash.bwd_rows(do, rows, kc, vc, lse, delta, None, H, scale)
+    K, V, Q, dO = kc[0].double(), vc[0].double(), rows[0].double(), do[0].double()
+    ri = torch.randint(0, R, (16,), device=gpu, generator=g)
+    s = (Q[ri] @ K.t()) * scale
+    lse_ref = torch.logsumexp(s, -1)
+    p = torch.exp(s - lse_ref[:, None])
+    o_ref = p @ V
+    assert _rel(out[0, ri], o_ref) <= 2e-5
+    d_ref = (dO[ri] * o_ref).sum(-1)
+    ds = p * ((dO[ri] @ V.t()) - d_ref[:, None])
+    assert _rel(drows[0, ri], scale * (ds @ K)) <= 5e-5
+    cj = torch.randint(0, T, (16,), device=gpu, generator=g)
+    sc = (Q @ K[cj].t()) * scale
+    pc = torch.exp(sc - lse[0, 0].double()[:, None])
+    dsc = pc * ((dO @ V[cj].t()) - delta[0, 0].double()[:, None])
+    assert _rel(dkv[0, cj, D:], pc.t() @ dO) <= 5e-5
+    assert _rel(dkv[0, cj, :D], scale * (dsc.t() @ Q)) <= 5e-5

@@ -40,10 +40,13 @@ __all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "start_gat
            "SeqParallelAttention"]
 
 FLASH_HEAD_DIMS = (32, 64, 96, 128)
+# bf16/fp16: 32x32x16 MFMA kernels (csrc/flash_fwd.hip, flash_bwd.hip); fp32: exact-f32 MFMA
+# kernels (csrc/flash_f32.hip) — the reference's own precision without materialised scores
+FLASH_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
 
 def flash_supported(x: Tensor, head_dim: int, v_head_dim: int) -> bool:
-    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
+    if not x.is_cuda or x.dtype not in FLASH_DTYPES:
         return False
     if head_dim not in FLASH_HEAD_DIMS or v_head_dim != head_dim:
         return False
@@ -54,7 +57,7 @@ def _hip_ok(k: Tensor, qv: Tensor, H: int) -> bool:
     """The HIP kernels take this call: a GPU bf16/fp16 row side, a supported head dim and a
     value width equal to the key width (otherwise the torch path runs, as documented)."""
     C = k.shape[-1]
-    return (k.is_cuda and k.dtype in (torch.bfloat16, torch.float16) and C % H == 0
+    return (k.is_cuda and k.dtype in FLASH_DTYPES and C % H == 0
             and C // H in FLASH_HEAD_DIMS and qv.shape[-1] == 2 * C and _ext.use_hip(k)
             and hasattr(_ext.ops(), "flash_fwd"))
 
@@ -353,7 +356,7 @@ class SeqParallelAttention(torch.autograd.Function):
             # the row side pre-multiplied by scale*log2 e once (XDOT_PRESCALE, default on): the
             # forward and both backward kernels read this same buffer and seed their score
             # accumulators instead of scaling every score (saved in place of k for backward)
-            prescaled = FLAGS.prescale and (k.numel() % 8 == 0)
+            prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
             if prescaled:
                 k = flash.prescale(k, scale)
             if isinstance(mask, flash.PendingMask):
@@ -493,7 +496,7 @@ def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None,
     projection GEMM) and hand the result to :func:`seq_parallel_attention_packed`.
     ``chunks``: row chunks of the pipeline (default ``XDOT_GATHER_CHUNKS``)."""
     comm = comm or _comm.get_comm()
-    hip = _ext.use_hip(qv) and qv.dtype in (torch.bfloat16, torch.float16)
+    hip = _ext.use_hip(qv) and qv.dtype in FLASH_DTYPES
     return _PendingGather(comm, qv.detach(), _row_chunks(comm.world_size, qv.shape[1], hip, chunks))
 
 

@@ -119,9 +119,9 @@ class RingAttention(torch.autograd.Function):
         check_consistent(comm, "ring_attention", k, qv, H)
         B, R, C = k.shape
         n = comm.world_size
-        from .attention import FLASH_HEAD_DIMS
+        from .attention import FLASH_DTYPES, FLASH_HEAD_DIMS
 
-        use_hip = (_ext.use_hip(k) and k.dtype in (torch.bfloat16, torch.float16) and qv.shape[-1] == 2 * C
+        use_hip = (_ext.use_hip(k) and k.dtype in FLASH_DTYPES and qv.shape[-1] == 2 * C
                    and C // H in FLASH_HEAD_DIMS)
         qv = qv.contiguous()
         ring = _Ring(comm, qv)
@@ -131,7 +131,7 @@ class RingAttention(torch.autograd.Function):
             from ..ops import flash
 
             ops = _ext.ops()
-            prescaled = FLAGS.prescale and (k.numel() % 8 == 0)
+            prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
             kk = flash.prescale(k, scale) if prescaled else k.contiguous()
             ns = int(ops.flash_splits(B, R, R, H, False))
             # slot 0: the running (O, LSE) of the blocks seen so far (fp32), slots 1..ns: the
