@@ -38,6 +38,8 @@ def parse(argv=None):
                     help="nt/all/tn: forward of the distributed product (reference modes); "
                          "*_fb: forward+backward of the corresponding autograd op")
     ap.add_argument("--offset", type=int, default=None, help="chunk size (default: whole shard)")
+    ap.add_argument("--link-gbps", type=float, default=None,
+                    help="with --emulate: collective transfer model in GB/s (xdot.utils.comm.EmulatedComm)")
     ap.add_argument("--scale", type=int, default=1, help="T = 75000 // scale (reference semantics)")
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--dim", type=int, default=768)
@@ -102,7 +104,7 @@ def main(argv=None):
     from xdot.utils import comm as C
     import xdot.parallel.functional as F
 
-    comm = C.EmulatedComm(a.emulate) if a.emulate else C.init("auto")
+    comm = C.EmulatedComm(a.emulate, link_gbps=a.link_gbps) if a.emulate else C.init("auto")
     ctx = C.use_comm(comm)  # the functional ops pick up the thread's communicator
     ctx.__enter__()
     n, rank = comm.world_size, comm.rank
@@ -116,7 +118,8 @@ def main(argv=None):
     R, D = T // n, a.dim
     torch.manual_seed(111)
     torch.set_grad_enabled(False)
-    rec = {"mode": a.mode, "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype}
+    rec = {"mode": a.mode, "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype,
+           "link_gbps": a.link_gbps}
 
     fb = a.mode.endswith("_fb")
     torch.set_grad_enabled(fb)

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   // ---- epilogue: per wave, 4 passes of 16 rows x 64 cols through LDS ----
   char* ep = smem + wave * 16 * EPI_ROW;
   constexpr int EO = 16 / sizeof(TO);  // output elements per 16-byte store
-  const bool vec_out = VEC && ((p.ldc % EO) == 0);
+  const bool vec_ld = (p.ldc % EO) == 0;  // + the strip's own address, tested per store
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
     const float* src = reinterpret_cast<const float*>(ep + row * EPI_ROW + c0 * 4);
     if (gm < p.M) {
       TO* dst = C + (int64_t)gm * p.ldc + gn;
-      if (vec_out && gn + 16 <= p.N) {
+      if (vec_ld && gn + 16 <= p.N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
 #pragma unroll
         for (int v = 0; v < 16 / EO; ++v) {
           union { u32x4 u; TO e[EO]; } o;

@@ -339,7 +339,7 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
         } else {
           TO* dst = reinterpret_cast<TO*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)gm * p.ldc + gn;
           constexpr int EO = 16 / sizeof(TO);
-          if (gn + 16 <= p.N && (p.ldc % EO) == 0) {
+          if (gn + 16 <= p.N && (p.ldc % EO) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
 #pragma unroll
             for (int c = 0; c < 16 / EO; ++c) {
               union { u32x4 u; TO e[EO]; } o;

@@ -50,3 +50,50 @@ def test_gather_pipeline_order_and_content(ws):
 
     res = ThreadGroup(ws).run(body)
     assert all(s == [(0, 3), (3, 6), (6, 7)] for s in res)
+
+
+def test_grouped_row_gathers_keep_offset_granularity(monkeypatch):
+    """nt / all with a small offset: every all-gather moves exactly one offset-row chunk (the
+    reference's wire granularity), several chunks feed one GEMM per group, and at least two
+    groups keep the gathers of group g+1 in flight under the GEMM of group g."""
+    import xdot.parallel.functional as F
+    import xdot.parallel.schedule as S
+    from xdot.utils.comm import ThreadComm, ThreadGroup
+
+    sizes, groups = [], []
+    orig = ThreadComm.all_gather_into
+
+    def spy(self, out, inp, async_op=False):
+        if self.rank == 0:
+            sizes.append(tuple(inp.shape))
+        return orig(self, out, inp, async_op)
+
+    monkeypatch.setattr(ThreadComm, "all_gather_into", spy)
+    monkeypatch.setattr(S, "GROUP_BYTES", 7 * 3 * 2 * 6 * 8)  # 2 chunks of 3 rows per group (P=2, D=6, fp64)
+    R, D, n = 10, 6, 3
+    g = torch.Generator().manual_seed(0)
+    L = torch.randn(2, n * R, D, generator=g, dtype=torch.float64)
+    Rt = torch.randn(2, n * R, D, generator=g, dtype=torch.float64)
+
+    def body(r):
+        sl = slice(r * R, (r + 1) * R)
+        orig_consume = S.gather_rows_grouped
+
+        def wrapped(comm, r3, chunks, consume):
+            def c2(s, e, gathered):
+                if comm.rank == 0:
+                    groups.append((s, e))
+                consume(s, e, gathered)
+            return orig_consume(comm, r3, chunks, c2)
+
+        F.gather_rows_grouped = wrapped
+        try:
+            return F.distributed_matmul_nt(L[:, sl], Rt[:, sl], 3)
+        finally:
+            F.gather_rows_grouped = orig_consume
+
+    outs = ThreadGroup(n).run(body)
+    ref = L @ Rt.transpose(-1, -2)
+    torch.testing.assert_close(torch.cat(outs, dim=1), ref)
+    assert sizes == [(3, 2, 6)] * 3 + [(1, 2, 6)]          # (rows, P, D) per all-gather: offset rows each
+    assert groups == [(0, 6), (6, 10)]                       # 2 chunks per group -> 2 GEMMs

@@ -120,6 +120,16 @@ def tn_partials_into(send: torch.Tensor, left: torch.Tensor, right: torch.Tensor
     if _ext.use_hip(send, left, right) and hip_dtype_ok(left, right) and send.dtype in _HIP_IN:
         left = left.contiguous()
         right = right.contiguous()
+        if (R * left.element_size()) % 16:
+            # column blocks j*R of `left` start off 16-byte boundaries (odd T/N): ONE GEMM over all
+            # T columns instead (leftᵀ (T x R) @ right, rows t = j*R + r), whose operand rows are aligned
+            T_ = N * R
+            dst = send.view(T_, D) if Pn == 1 else torch.empty(Pn, T_, D, dtype=send.dtype, device=send.device)
+            strided_gemm(left, right, dst, M=T_, N=D, K=R, nb2=Pn, lda=T_, ldb=D, ldc=D, sA2=R * T_, sB2=R * D,
+                         sC2=T_ * D, a_mc=True, b_mc=True)
+            if Pn > 1:
+                send.copy_(dst.view(Pn, N, R, D).transpose(0, 1))
+            return
         strided_gemm(left, right, send, M=R, N=D, K=R, nb1=N, nb2=Pn,
                      lda=T, ldb=D, ldc=D, sA1=R, sA2=R * T, sB1=0, sB2=R * D,
                      sC1=Pn * R * D, sC2=R * D, a_mc=True, b_mc=True)
@@ -127,6 +137,20 @@ def tn_partials_into(send: torch.Tensor, left: torch.Tensor, right: torch.Tensor
     ct = torch.promote_types(left.dtype, right.dtype)
     blocks = left.view(Pn, R, N, R).permute(2, 0, 3, 1).to(ct)        # (N, Pn, R_col, R_row)
     send.copy_(torch.matmul(blocks, right.to(ct).unsqueeze(0)).to(send.dtype))
+
+
+def matmul_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+    """``out[p] = a[p] @ b[p]``: (Pn, M, K) x (Pn, K, N) -> (Pn, M, N) contiguous ``out``."""
+    Pn, M, K = a.shape
+    N = b.shape[-1]
+    if _ext.use_hip(out, a, b) and hip_dtype_ok(a, b) and out.dtype in _HIP_IN:
+        a = a.contiguous()
+        b = b.contiguous()
+        strided_gemm(a, b, out, M=M, N=N, K=K, nb2=Pn, lda=K, ldb=N, ldc=N, sA2=M * K, sB2=K * N,
+                     sC2=M * N, a_mc=False, b_mc=True)
+        return
+    ct = torch.promote_types(a.dtype, b.dtype)
+    out.copy_(torch.matmul(a.to(ct), b.to(ct)))
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, *, trans_b: bool = False, alpha: float = 1.0,

@@ -47,7 +47,8 @@ from ..ops import gemm as G
 from ..utils import comm as _comm
 from ..utils.checks import check_consistent
 from ..utils.profiling import measure
-from .schedule import Offset, gather_pipeline, plan_chunks, resolve_offset
+from .schedule import (GROUP_BYTES, Offset, gather_pipeline, gather_rows_grouped, gather_rows_whole,
+                       plan_chunks, resolve_offset)
 
 __all__ = ["distributed_matmul_nt", "distributed_matmul_all", "distributed_matmul_tn",
            "distributed_matmul_block", "gather_sequence"]
@@ -97,8 +98,11 @@ def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offse
     def consume(s, e, gathered):  # gathered: (N, Pn, c, D)
         G.nt_chunk_into(out, l3, gathered, s, alpha)
 
-    gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
-                    right.device, consume)
+    if len(chunks) > 1:  # offset-row all-gathers, grouped per GEMM (schedule.gather_rows_grouped)
+        gather_rows_grouped(comm, r3, chunks, consume)
+    else:
+        gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
+                        right.device, consume)
     return out.view(*P, R, T)
 
 
@@ -144,14 +148,19 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
     l3 = left.reshape(Pn, R, T)
     r3 = right.reshape(Pn, Rr, D)
 
+    if chunking == "rows" and Rr > 0 and n * Pn * Rr * D * right.element_size() <= 4 * GROUP_BYTES:
+        # the whole gathered `right` fits the budget: every offset chunk still travels in its own
+        # all-gather, then ONE K = T GEMM reads `left` whole (aligned rows, no per-rank K
+        # segments starting off 16-byte boundaries when T/N is odd)
+        G.matmul_into(out, l3, gather_rows_whole(comm, r3, chunks if by_rows else [(0, Rr)]))
+        return out.view(*P, R, D)
     if by_rows:
         acc = out if out.dtype in (torch.float32, torch.float64) else torch.empty_like(out, dtype=torch.float32)
 
         def consume_rows(s, e, gathered):  # (N, Pn, c, D)
             G.all_rows_chunk_into(acc, l3, gathered, s, accumulate=s > 0)
 
-        gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
-                        right.device, consume_rows)
+        gather_rows_grouped(comm, r3, chunks, consume_rows)
         if acc is not out:
             out.copy_(acc)
         return out.view(*P, R, D)

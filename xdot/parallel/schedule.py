@@ -14,6 +14,13 @@ Here:
 * with several chunks the gather of chunk i+1 is issued (async, on RCCL's stream) before the
   GEMM of chunk i and waited for on the compute stream only when needed — a two-deep
   ring of preallocated buffers, no host synchronisation;
+* :func:`gather_rows_grouped` — the row-chunk plan of ``nt`` / ``all`` with small offsets: the
+  per-chunk cost of the loop above is host work (a collective call and a GEMM launch per
+  chunk: 98 chunks of 32 rows at T=25000, N=8), so consecutive chunks form groups: each chunk
+  is still ONE all-gather of exactly its rows (the reference's granularity on the wire), but
+  a group's gathers are issued together (one coalesced RCCL launch), land in one buffer and
+  feed ONE GEMM, while the next group's gathers are in flight (two groups double-buffered,
+  within ``XDOT_CHUNK_BUDGET_MB`` / a 256 MB default per group);
 * :func:`auto_offset` sizes chunks from free HBM when the caller asks for ``offset='auto'``.
 """
 from __future__ import annotations
@@ -87,3 +94,102 @@ def gather_pipeline(comm, chunks: Sequence[Tuple[int, int]], make_send: Callable
         h.wait()
         consume(s, e, out)
         pending = nxt
+
+
+GROUP_BYTES = 256 * 2**20
+
+
+def gather_rows_grouped(comm, r3: torch.Tensor, chunks: Sequence[Tuple[int, int]],
+                        consume: Callable[[int, int, torch.Tensor], None]) -> None:
+    """Row chunks ``[s, e)`` of ``r3`` (Pn, Rr, D), each gathered by its own all-gather, consumed
+    in groups: ``consume(s0, e0, gathered)`` with ``gathered`` (N, Pn, e0 - s0, D) rank-major,
+    the rows of a whole group of consecutive chunks (at least two groups when there are at
+    least two chunks, so a group's GEMM overlaps the next group's gathers)."""
+    if not chunks:
+        return
+    n = comm.world_size
+    Pn, Rr, D = r3.shape
+    if n == 1:  # nothing travels: one consumer call over every row
+        consume(0, Rr, r3.unsqueeze(0))
+        return
+    rt = (r3[0] if Pn == 1 else r3.transpose(0, 1)).contiguous()  # (Rr, [Pn,] D): chunk rows contiguous
+    row_bytes = n * Pn * D * r3.element_size()
+    budget = FLAGS.chunk_budget_mb * 2**20 / 4 if FLAGS.chunk_budget_mb > 0 else GROUP_BYTES
+    c = max(e - s for s, e in chunks)
+    per_group = max(1, min(-(-len(chunks) // 2), int(budget // max(1, c * row_bytes))))
+    groups = [list(chunks[i:i + per_group]) for i in range(0, len(chunks), per_group)]
+    maxrows = max(g[-1][1] - g[0][0] for g in groups)
+    nslot = min(2, len(groups))
+    raws = [torch.empty(n * maxrows * Pn * D, dtype=r3.dtype, device=r3.device) for _ in range(nslot)]
+    dests = [torch.empty(n * Pn * maxrows * D, dtype=r3.dtype, device=r3.device) for _ in range(nslot)]
+
+    def issue(g):
+        grp = groups[g]
+        s0, e0 = grp[0][0], grp[-1][1]
+        raw = raws[g % nslot][:n * (e0 - s0) * Pn * D]
+        return comm.all_gather_chunks(raw, rt[s0:e0], [e - s for s, e in grp], async_op=True), raw
+
+    pend = issue(0)
+    for g, grp in enumerate(groups):
+        nxt = issue(g + 1) if g + 1 < len(groups) else None
+        h, raw = pend
+        h.wait()
+        s0, e0 = grp[0][0], grp[-1][1]
+        dest = dests[g % nslot][:n * Pn * (e0 - s0) * D].view(n, Pn, e0 - s0, D)
+        off = r = 0
+        for cc, cnt in _runs([e - s for s, e in grp]):  # (cnt, N, cc, Pn, D) -> (N, Pn, cnt*cc, D)
+            seg = raw[off:off + cnt * n * cc * Pn * D].view(cnt, n, cc, Pn, D)
+            dest[:, :, r:r + cnt * cc].unflatten(2, (cnt, cc)).copy_(seg.permute(1, 3, 0, 2, 4))
+            off += cnt * n * cc * Pn * D
+            r += cnt * cc
+        consume(s0, e0, dest)
+        pend = nxt
+
+
+def gather_rows_whole(comm, r3: torch.Tensor, chunks: Sequence[Tuple[int, int]]) -> torch.Tensor:
+    """Every row chunk of ``r3`` (Pn, Rr, D) all-gathered by its own collective (grouped launches,
+    all in flight together) into ONE (Pn, N*Rr, D) buffer in global row order: the B operand of
+    ``all``'s single K = T GEMM.  Each group is reordered as soon as it lands, under the
+    transfers of the later groups."""
+    n = comm.world_size
+    Pn, Rr, D = r3.shape
+    if n == 1:
+        return r3
+    if len(chunks) == 1 and Pn == 1:  # one gather, already (N*Rr, D) in global row order
+        dest = torch.empty(n * Rr * D, dtype=r3.dtype, device=r3.device)
+        comm.all_gather_into(dest.view(n, Rr, D), r3[0].contiguous())
+        return dest.view(1, n * Rr, D)
+    rt = (r3[0] if Pn == 1 else r3.transpose(0, 1)).contiguous()
+    row_bytes = n * Pn * D * r3.element_size()
+    budget = FLAGS.chunk_budget_mb * 2**20 / 4 if FLAGS.chunk_budget_mb > 0 else GROUP_BYTES
+    c = max(e - s for s, e in chunks)
+    per_group = max(1, min(-(-len(chunks) // 2), int(budget // max(1, c * row_bytes))))
+    groups = [list(chunks[i:i + per_group]) for i in range(0, len(chunks), per_group)]
+    raw_all = torch.empty(n * Rr * Pn * D, dtype=r3.dtype, device=r3.device)
+    pend, off = [], 0
+    for grp in groups:
+        s0, e0 = grp[0][0], grp[-1][1]
+        raw = raw_all[off:off + n * (e0 - s0) * Pn * D]
+        off += raw.numel()
+        pend.append((comm.all_gather_chunks(raw, rt[s0:e0], [e - s for s, e in grp], async_op=True), raw))
+    dest = torch.empty(Pn, n, Rr, D, dtype=r3.dtype, device=r3.device)
+    for grp, (h, raw) in zip(groups, pend):
+        h.wait()
+        o = 0
+        r = grp[0][0]
+        for cc, cnt in _runs([e - s for s, e in grp]):  # (cnt, N, cc, Pn, D) -> (Pn, N, cnt*cc, D)
+            seg = raw[o:o + cnt * n * cc * Pn * D].view(cnt, n, cc, Pn, D)
+            dest[:, :, r:r + cnt * cc].unflatten(2, (cnt, cc)).copy_(seg.permute(3, 1, 0, 2, 4))
+            o += cnt * n * cc * Pn * D
+            r += cnt * cc
+    return dest.view(Pn, n * Rr, D)
+
+
+def _runs(sizes):
+    out = []
+    for c in sizes:
+        if out and out[-1][0] == c:
+            out[-1][1] += 1
+        else:
+            out.append([c, 1])
+    return out

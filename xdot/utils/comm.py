@@ -77,6 +77,19 @@ class Communicator:
         """``out`` <- sum over ranks of block ``rank`` of the rank-major ``inp``."""
         raise NotImplementedError
 
+    def all_gather_chunks(self, raw: torch.Tensor, inp: torch.Tensor, sizes, async_op: bool = False):
+        """``len(sizes)`` all-gathers issued together: chunk i = the next ``sizes[i]`` rows of the
+        contiguous ``inp`` (rows, ...), gathered rank-major into the next ``N * sizes[i]`` rows'
+        worth of the flat ``raw`` buffer (chunk i's output is (N, sizes[i], ...) contiguous).
+        Every collective moves exactly its chunk (the reference's ``offset`` granularity);
+        backends that can issue them as one grouped launch do (RCCL coalescing)."""
+        hs = [self.all_gather_into(o, i, async_op=True) for o, i in _chunk_views(raw, inp, sizes, self.world_size)]
+        h = Handle(out=raw, post=lambda: [x.wait() for x in hs if x is not None])
+        if async_op:
+            return h
+        h.wait()
+        return None
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):
         raise NotImplementedError
 
@@ -101,6 +114,31 @@ class Communicator:
 
     def __repr__(self):
         return f"{type(self).__name__}(rank={self.rank}, world_size={self.world_size}, backend={self.backend})"
+
+
+def _chunk_views(raw, inp, sizes, n):
+    """(out_i (N, c_i, ...), in_i (c_i, ...)) of :meth:`Communicator.all_gather_chunks`."""
+    rest = tuple(inp.shape[1:])
+    row = 1
+    for d in rest:
+        row *= d
+    views, off, r = [], 0, 0
+    for c in sizes:
+        views.append((raw[off:off + n * c * row].view((n, c) + rest), inp[r:r + c]))
+        off += n * c * row
+        r += c
+    return views
+
+
+def _runs(sizes):
+    """consecutive equal sizes -> [(size, count)]"""
+    out = []
+    for c in sizes:
+        if out and out[-1][0] == c:
+            out[-1][1] += 1
+        else:
+            out.append([c, 1])
+    return out
 
 
 def _check_gather(out, inp, n):
@@ -224,6 +262,20 @@ class EmulatedComm(LocalComm):
         return self._transfer(out, out.nbytes * (n - 1) // n, self.link_gbps,
                               lambda: out.view(n, -1).copy_(inp.reshape(1, -1).expand(n, -1)), async_op, (inp,))
 
+    def all_gather_chunks(self, raw, inp, sizes, async_op=False):
+        n = self.world_size
+        row = inp[0].numel() if inp.shape[0] else 0
+
+        def copy():  # one replicate copy per run of equal-size chunks
+            off = r = 0
+            for c, cnt in _runs(sizes):
+                src = inp[r:r + c * cnt].reshape(cnt, 1, c * row)
+                raw[off:off + cnt * n * c * row].view(cnt, n, c * row).copy_(src.expand(cnt, n, c * row))
+                off += cnt * n * c * row
+                r += c * cnt
+        used = raw[:n * sum(sizes) * row]
+        return self._transfer(used, used.nbytes * (n - 1) // n, self.link_gbps, copy, async_op, (inp,))
+
     def reduce_scatter(self, out, inp, async_op=False):
         n = self.world_size
         return self._transfer(out, inp.nbytes * (n - 1) // n, self.link_gbps,
@@ -275,6 +327,20 @@ class TorchDistComm(Communicator):
         inp = inp.contiguous()
         w = dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
         return Handle(w, out) if async_op else None
+
+    def all_gather_chunks(self, raw, inp, sizes, async_op=False):
+        views = _chunk_views(raw, inp, sizes, self.world_size)
+        if self._backend != "nccl" or len(views) < 2 or not hasattr(dist, "_coalescing_manager"):
+            return super().all_gather_chunks(raw, inp, sizes, async_op)
+        # one grouped RCCL launch for every chunk's all-gather
+        with dist._coalescing_manager(group=self.group, device=raw.device, async_ops=True) as cm:
+            for o, i in views:
+                dist.all_gather_into_tensor(o.view(-1), i.contiguous().view(-1), group=self.group)
+        h = Handle(cm, raw)
+        if async_op:
+            return h
+        h.wait()
+        return None
 
     def reduce_scatter(self, out, inp, async_op=False):
         if inp.numel() != out.numel() * self.world_size:
