@@ -9,7 +9,9 @@
 ``XDOT_ALLOW_TORCH_FALLBACK``  ``1`` lets GPU ops fall back to torch when ``_C.so`` is absent
                                (default: fail loudly)
 ``XDOT_COMM_TIMEOUT_S``        collective timeout in seconds (default 600)
-``XDOT_CHUNK_BUDGET_MB``       transient-buffer budget used by the chunk planner
+``XDOT_CHUNK_BUDGET_MB``       transient-buffer budget used by the chunk planner (``offset='auto'``)
+                               and by the grouped offset-row gathers of ``nt`` / ``all`` (a
+                               quarter per group; default 256 MB per group)
 ``XDOT_GRAD_FP32``             ``1``: the fused attention's gathered-side gradient partials are
                                kept and reduce-scattered in fp32 (default: rounded once to
                                the bf16/fp16 compute dtype in the kernel, half the bytes)
