@@ -124,7 +124,7 @@ def main(argv=None):
     fb = a.mode.endswith("_fb")
     torch.set_grad_enabled(fb)
     # single-GPU torch baseline on the full problem (reference: rank 0 only)
-    if rank == 0 and not a.no_local and not fb and not a.emulate:
+    if rank == 0 and not a.no_local and not fb:
         _peak_reset()
         if a.mode == "nt":
             x = torch.rand(1, T, D, device=dev, dtype=dt)
