@@ -10,7 +10,7 @@ from _dist import run_gloo
 pytestmark = pytest.mark.gpu
 
 
-def _ops_case(rank, ws, dt_name, offset):
+def _ops_case(rank, ws, dt_name, offset, heads=False):
     import xdot.parallel.functional as F
 
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt_name]
@@ -28,15 +28,29 @@ def _ops_case(rank, ws, dt_name, offset):
     def rel(a, b):
         return ((a.double() - b).norm() / b.norm()).item()
 
-    nt = F.distributed_matmul_nt(L[:, sl].to(dev, dt), Q[:, sl].to(dev, dt), offset)
+    def shard(X):  # (P, T, c) -> this rank's rows, optionally as the module's head-split view
+        x = X[:, sl].to(dev, dt)
+        if heads:  # (1, R, P*c) contiguous, viewed (1, P, R, c): R-major, read in place
+            x = x.transpose(0, 1).contiguous().view(1, R, P, -1).transpose(1, 2)
+        return x
+
+    def flat(y):  # back to (P, R, c)
+        return y.reshape(P, R, -1) if heads else y
+
+    nt = flat(F.distributed_matmul_nt(shard(L), shard(Q), offset))
     assert rel(nt.cpu(), (L @ Q.transpose(-1, -2))[:, sl]) <= tol, "nt"
-    al = F.distributed_matmul_all(S[:, sl].to(dev, dt), Q[:, sl].to(dev, dt), offset)
+    al = flat(F.distributed_matmul_all(S[:, sl].to(dev, dt).unsqueeze(0) if heads else S[:, sl].to(dev, dt),
+                                       shard(Q), offset))
     assert rel(al.cpu(), (S @ Q)[:, sl]) <= tol, "all"
-    tn = F.distributed_matmul_tn(S[:, sl].to(dev, dt), Q[:, sl].to(dev, dt))
+    tn = flat(F.distributed_matmul_tn(S[:, sl].to(dev, dt).unsqueeze(0) if heads else S[:, sl].to(dev, dt),
+                                      shard(Q)))
     assert rel(tn.cpu(), (S.transpose(-1, -2) @ Q)[:, sl]) <= tol, "tn"
 
 
 @pytest.mark.parametrize("dt_name", ["bf16", "fp32"])
 @pytest.mark.parametrize("offset", [32, 100, None])
-def test_distributed_products_three_ranks(gpu, dt_name, offset):
-    run_gloo(_ops_case, 3, dt_name, offset, timeout=300)
+@pytest.mark.parametrize("heads", [False, True])
+def test_distributed_products_three_ranks(gpu, dt_name, offset, heads):
+    """``heads``: operands are (1, P, R, c) head-split views of (1, R, P*c) tensors (the
+    materialised module's layout): read and produced in place, no transpose copies."""
+    run_gloo(_ops_case, 3, dt_name, offset, heads, timeout=300)

@@ -40,21 +40,42 @@ def _flat(t: torch.Tensor, lead: int) -> torch.Tensor:
     return t.view(-1, *t.shape[t.dim() - lead:]) if lead else t
 
 
+def _m3(x: torch.Tensor):
+    """(Pn, rows, cols) operand read in place: -> (tensor, batch stride, row stride) when its
+    inner stride is 1 (e.g. the (1, H, R, d) head-split view of a (1, R, H*d) projection, batch
+    stride d, row stride H*d: no head-transpose copy), else a contiguous copy."""
+    if x.dim() == 3 and (x.stride(-1) == 1 or x.shape[-1] == 1):
+        P, r, c = x.shape
+        return x, (x.stride(0) if P > 1 else 0), (x.stride(1) if r > 1 else c)
+    x = x.contiguous()
+    return x, x.shape[1] * x.shape[2], x.shape[2]
+
+
+def _m4(x: torch.Tensor):
+    """(N, Pn, rows, cols) operand in place -> (tensor, stride N, stride Pn, row stride)."""
+    if x.stride(-1) == 1 or x.shape[-1] == 1:
+        N, P, r, c = x.shape
+        return x, (x.stride(0) if N > 1 else 0), (x.stride(1) if P > 1 else 0), (x.stride(2) if r > 1 else c)
+    x = x.contiguous()
+    return x, x.shape[1] * x.shape[2] * x.shape[3], x.shape[2] * x.shape[3], x.shape[3]
+
+
 # ---------------------------------------------------------------------------------------
 # nt: out[p, :, j*R + c0 : j*R + c0 + c] = alpha * left[p] @ chunk[j, p]^T
 # ---------------------------------------------------------------------------------------
 def nt_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, c0: int,
                   alpha: float = 1.0) -> None:
-    """``out``: (Pn, R, N*Rr) contiguous; ``left``: (Pn, R, D); ``chunk``: (N, Pn, c, D)."""
+    """``out``: (Pn, R, N*Rr) contiguous; ``left``: (Pn, R, D); ``chunk``: (N, Pn, c, D); the
+    operands may be strided views with unit inner stride (read in place)."""
     N, Pn, c, D = chunk.shape
     R = left.shape[-2]
     T = out.shape[-1]
     Rr = T // N  # rows per rank of the gathered operand
     if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
-        left = left.contiguous()
-        chunk = chunk.contiguous()
+        left, sA, lda = _m3(left)
+        chunk, sBj, sBp, ldb = _m4(chunk)
         strided_gemm(left, chunk, out[..., c0:], M=R, N=c, K=D, nb1=N, nb2=Pn,
-                     lda=D, ldb=D, ldc=T, sA1=0, sA2=R * D, sB1=Pn * c * D, sB2=c * D,
+                     lda=lda, ldb=ldb, ldc=T, sA1=0, sA2=sA, sB1=sBj, sB2=sBp,
                      sC1=Rr, sC2=R * T, a_mc=False, b_mc=False, alpha=alpha)
         return
     part = torch.matmul(left.unsqueeze(0).to(torch.promote_types(left.dtype, chunk.dtype)),
@@ -72,16 +93,16 @@ def all_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, d
     """``out``: (Pn, R, D); ``left``: (Pn, R, T); ``chunk``: (N, Pn, R, c) feature columns."""
     N, Pn, R, c = chunk.shape
     T = left.shape[-1]
-    D = out.shape[-1]
     if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
-        left = left.contiguous()
-        chunk = chunk.contiguous()
+        left, sA, lda = _m3(left)
+        chunk, sBj, sBp, ldb = _m4(chunk)
+        out, sC, ldc = _m3(out)
         strided_gemm(left, chunk, out[..., d0:], M=R, N=c, K=R, nseg=N, nb1=1, nb2=Pn,
-                     lda=T, ldb=c, ldc=D, sA2=R * T, sB2=R * c, sC2=R * D,
-                     sAseg=R, sBseg=Pn * R * c, a_mc=False, b_mc=True)
+                     lda=lda, ldb=ldb, ldc=ldc, sA2=sA, sB2=sBp, sC2=sC,
+                     sAseg=R, sBseg=sBj, a_mc=False, b_mc=True)
         return
     ct = torch.promote_types(left.dtype, chunk.dtype)
-    splits = left.view(Pn, R, N, R).permute(2, 0, 1, 3).to(ct)        # view, no stack copy
+    splits = left.reshape(Pn, R, N, R).permute(2, 0, 1, 3).to(ct)     # no stack copy
     res = torch.matmul(splits, chunk.to(ct)).sum(0)                   # (Pn, R, c)
     out[..., d0:d0 + c] = res.to(out.dtype)
 
@@ -96,11 +117,14 @@ def all_rows_chunk_into(acc: torch.Tensor, left: torch.Tensor, chunk: torch.Tens
     R, T = left.shape[-2], left.shape[-1]
     Rr = T // N
     if _ext.use_hip(acc, left, chunk) and hip_dtype_ok(left, chunk) and acc.dtype in _HIP_IN:
-        left = left.contiguous()
-        chunk = chunk.contiguous()
-        strided_gemm(left[..., r0:], chunk, acc, M=R, N=D, K=c, nseg=N, nb1=1, nb2=Pn,
-                     lda=T, ldb=D, ldc=D, sA2=R * T, sB2=c * D, sC2=R * D,
-                     sAseg=Rr, sBseg=Pn * c * D, a_mc=False, b_mc=True, beta=1.0 if accumulate else 0.0)
+        left, sA, lda = _m3(left)
+        chunk, sBj, sBp, ldb = _m4(chunk)
+        acc_, sC, ldc = _m3(acc)
+        strided_gemm(left[..., r0:], chunk, acc_, M=R, N=D, K=c, nseg=N, nb1=1, nb2=Pn,
+                     lda=lda, ldb=ldb, ldc=ldc, sA2=sA, sB2=sBp, sC2=sC,
+                     sAseg=Rr, sBseg=sBj, a_mc=False, b_mc=True, beta=1.0 if accumulate else 0.0)
+        if acc_ is not acc:
+            acc.copy_(acc_)
         return
     ct = acc.dtype if acc.dtype in (torch.float32, torch.float64) else torch.float32
     part = sum(torch.matmul(left[..., j * Rr + r0:j * Rr + r0 + c].to(ct), chunk[j].to(ct)) for j in range(N))
@@ -114,40 +138,54 @@ def all_rows_chunk_into(acc: torch.Tensor, left: torch.Tensor, chunk: torch.Tens
 # tn: send[j, p] = left[p, :, j*R:(j+1)*R]^T @ right[p]   (reduce-scatter send buffer)
 # ---------------------------------------------------------------------------------------
 def tn_partials_into(send: torch.Tensor, left: torch.Tensor, right: torch.Tensor) -> None:
-    """``send``: (N, Pn, R, D); ``left``: (Pn, R, T); ``right``: (Pn, R, D)."""
+    """``send``: (N, Pn, R, D) (any view with unit inner stride, e.g. an (N, R, Pn, D) buffer
+    permuted); ``left``: (Pn, R, T); ``right``: (Pn, R, D), read in place."""
     N, Pn, R, D = send.shape
     T = left.shape[-1]
     if _ext.use_hip(send, left, right) and hip_dtype_ok(left, right) and send.dtype in _HIP_IN:
-        left = left.contiguous()
-        right = right.contiguous()
-        if (R * left.element_size()) % 16:
+        left, sA, lda = _m3(left)
+        right, sB, ldb = _m3(right)
+        assert send.stride(-1) == 1, "tn_partials_into: send needs a unit inner stride"
+        sCj, sCp, ldc = send.stride(0), send.stride(1), send.stride(2)
+        if (R * left.element_size()) % 16 and send.stride() == (R * Pn * D, D, Pn * D, 1):
+            # R-major send buffer (n, R, Pn, D): rows t = j*R + r of head p are uniformly Pn*D apart,
+            # so the single T-row GEMM below writes it in place
+            T_ = N * R
+            strided_gemm(left, right, send, M=T_, N=D, K=R, nb2=Pn, lda=lda, ldb=ldb, ldc=Pn * D, sA2=sA,
+                         sB2=sB, sC2=D, a_mc=True, b_mc=True)
+            return
+        if (R * left.element_size()) % 16 and send.is_contiguous():
             # column blocks j*R of `left` start off 16-byte boundaries (odd T/N): ONE GEMM over all
             # T columns instead (leftᵀ (T x R) @ right, rows t = j*R + r), whose operand rows are aligned
             T_ = N * R
             dst = send.view(T_, D) if Pn == 1 else torch.empty(Pn, T_, D, dtype=send.dtype, device=send.device)
-            strided_gemm(left, right, dst, M=T_, N=D, K=R, nb2=Pn, lda=T_, ldb=D, ldc=D, sA2=R * T_, sB2=R * D,
+            strided_gemm(left, right, dst, M=T_, N=D, K=R, nb2=Pn, lda=lda, ldb=ldb, ldc=D, sA2=sA, sB2=sB,
                          sC2=T_ * D, a_mc=True, b_mc=True)
             if Pn > 1:
                 send.copy_(dst.view(Pn, N, R, D).transpose(0, 1))
             return
         strided_gemm(left, right, send, M=R, N=D, K=R, nb1=N, nb2=Pn,
-                     lda=T, ldb=D, ldc=D, sA1=R, sA2=R * T, sB1=0, sB2=R * D,
-                     sC1=Pn * R * D, sC2=R * D, a_mc=True, b_mc=True)
+                     lda=lda, ldb=ldb, ldc=ldc, sA1=R, sA2=sA, sB1=0, sB2=sB,
+                     sC1=sCj, sC2=sCp, a_mc=True, b_mc=True)
         return
     ct = torch.promote_types(left.dtype, right.dtype)
-    blocks = left.view(Pn, R, N, R).permute(2, 0, 3, 1).to(ct)        # (N, Pn, R_col, R_row)
+    blocks = left.reshape(Pn, R, N, R).permute(2, 0, 3, 1).to(ct)     # (N, Pn, R_col, R_row)
     send.copy_(torch.matmul(blocks, right.to(ct).unsqueeze(0)).to(send.dtype))
 
 
 def matmul_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
-    """``out[p] = a[p] @ b[p]``: (Pn, M, K) x (Pn, K, N) -> (Pn, M, N) contiguous ``out``."""
+    """``out[p] = a[p] @ b[p]``: (Pn, M, K) x (Pn, K, N) -> (Pn, M, N); every operand may be a
+    view with unit inner stride (read / written in place)."""
     Pn, M, K = a.shape
     N = b.shape[-1]
     if _ext.use_hip(out, a, b) and hip_dtype_ok(a, b) and out.dtype in _HIP_IN:
-        a = a.contiguous()
-        b = b.contiguous()
-        strided_gemm(a, b, out, M=M, N=N, K=K, nb2=Pn, lda=K, ldb=N, ldc=N, sA2=M * K, sB2=K * N,
-                     sC2=M * N, a_mc=False, b_mc=True)
+        a, sA, lda = _m3(a)
+        b, sB, ldb = _m3(b)
+        o, sC, ldc = _m3(out)
+        strided_gemm(a, b, o, M=M, N=N, K=K, nb2=Pn, lda=lda, ldb=ldb, ldc=ldc, sA2=sA, sB2=sB,
+                     sC2=sC, a_mc=False, b_mc=True)
+        if o is not out:
+            out.copy_(o)
         return
     ct = torch.promote_types(a.dtype, b.dtype)
     out.copy_(torch.matmul(a.to(ct), b.to(ct)))

@@ -61,6 +61,14 @@ def _prep(left: torch.Tensor, right: torch.Tensor, name: str):
         raise ValueError(f"{name}: operands on different devices")
 
 
+def _rmajor(x3: torch.Tensor) -> bool:
+    """(Pn, R, D) view whose rows are R-major, i.e. the (1, H, R, d) head split of a contiguous
+    (1, R, H*d) projection: gathered and produced in that layout, read by the GEMMs
+    through their strides — no head-transpose or head-merge copy."""
+    Pn, R, D = x3.shape
+    return Pn > 1 and R > 1 and x3.stride() == (D, Pn * D, 1)
+
+
 def _result_dtype(left, right, out_dtype):
     return out_dtype if out_dtype is not None else torch.promote_types(left.dtype, right.dtype)
 
@@ -100,6 +108,10 @@ def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offse
 
     if len(chunks) > 1:  # offset-row all-gathers, grouped per GEMM (schedule.gather_rows_grouped)
         gather_rows_grouped(comm, r3, chunks, consume)
+    elif _rmajor(r3) and n > 1:  # gather the (Rr, Pn*D) rows as they are; the GEMM reads them strided
+        g = torch.empty((n, Rr, Pn, D), dtype=right.dtype, device=right.device)
+        comm.all_gather_into(g, r3.transpose(0, 1))
+        consume(0, Rr, g.permute(0, 2, 1, 3))
     else:
         gather_pipeline(comm, chunks, lambda s, e: r3[:, s:e, :], lambda c: (Pn, c, D), right.dtype,
                         right.device, consume)
@@ -140,20 +152,24 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
     else:
         chunks = plan_chunks(D, off)
     check_consistent(comm, "all", left, right, tuple(chunks))
-    out = torch.empty((Pn, R, D), dtype=_result_dtype(left, right, out_dtype), device=left.device)
-    if R == 0 or D == 0:
-        return out.view(*P, R, D)
-    if T == 0:
-        return out.zero_().view(*P, R, D)
     l3 = left.reshape(Pn, R, T)
     r3 = right.reshape(Pn, Rr, D)
+    rm = _rmajor(r3) and R > 1
+    if rm:  # R-major like `right` (head-split view): the module's head merge is then a free view
+        out = torch.empty((R, Pn, D), dtype=_result_dtype(left, right, out_dtype), device=left.device).transpose(0, 1)
+    else:
+        out = torch.empty((Pn, R, D), dtype=_result_dtype(left, right, out_dtype), device=left.device)
+    if R == 0 or D == 0:
+        return out.reshape(*P, R, D)
+    if T == 0:
+        return out.zero_().reshape(*P, R, D)
 
     if chunking == "rows" and Rr > 0 and n * Pn * Rr * D * right.element_size() <= 4 * GROUP_BYTES:
         # the whole gathered `right` fits the budget: every offset chunk still travels in its own
         # all-gather, then ONE K = T GEMM reads `left` whole (aligned rows, no per-rank K
         # segments starting off 16-byte boundaries when T/N is odd)
         G.matmul_into(out, l3, gather_rows_whole(comm, r3, chunks if by_rows else [(0, Rr)]))
-        return out.view(*P, R, D)
+        return out.reshape(*P, R, D)
     if by_rows:
         acc = out if out.dtype in (torch.float32, torch.float64) else torch.empty_like(out, dtype=torch.float32)
 
@@ -163,14 +179,14 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
         gather_rows_grouped(comm, r3, chunks, consume_rows)
         if acc is not out:
             out.copy_(acc)
-        return out.view(*P, R, D)
+        return out.reshape(*P, R, D)
 
     def consume(s, e, gathered):  # (N, Pn, Rr, c)
         G.all_chunk_into(out, l3, gathered, s)
 
     gather_pipeline(comm, chunks, lambda s, e: r3[..., s:e], lambda c: (Pn, Rr, c), right.dtype,
                     right.device, consume)
-    return out.view(*P, R, D)
+    return out.reshape(*P, R, D)
 
 
 @measure
@@ -203,17 +219,24 @@ def distributed_matmul_tn(left: torch.Tensor, right: torch.Tensor, *,
     res_dt = _result_dtype(left, right, out_dtype)
     if reduce_dtype is None:
         reduce_dtype = torch.float32 if res_dt in (torch.bfloat16, torch.float16) and n > 1 else res_dt
-    send = torch.empty((n, Pn, Rc, D), dtype=reduce_dtype, device=left.device)
-    if R > 0 and D > 0:
-        G.tn_partials_into(send, left.reshape(Pn, R, T), right.reshape(Pn, R, D))
+    r3 = right.reshape(Pn, R, D)
+    rm = _rmajor(r3)  # R-major operand (head-split view) -> R-major send buffer and result
+    if rm:
+        sbuf = torch.empty((n, Rc, Pn, D), dtype=reduce_dtype, device=left.device)
+        send = sbuf.permute(0, 2, 1, 3)
     else:
-        send.zero_()
+        sbuf = send = torch.empty((n, Pn, Rc, D), dtype=reduce_dtype, device=left.device)
+    if R > 0 and D > 0:
+        G.tn_partials_into(send, left.reshape(Pn, R, T), r3)
+    else:
+        sbuf.zero_()
     if n == 1:
         out = send[0]
     else:
-        out = torch.empty((Pn, Rc, D), dtype=reduce_dtype, device=left.device)
-        comm.reduce_scatter(out, send)
-    return out.to(res_dt).view(*P, Rc, D)
+        obuf = torch.empty(sbuf.shape[1:], dtype=reduce_dtype, device=left.device)
+        comm.reduce_scatter(obuf, sbuf)
+        out = obuf.transpose(0, 1) if rm else obuf
+    return out.to(res_dt).reshape(*P, Rc, D)
 
 
 @measure

@@ -155,10 +155,12 @@ def gather_rows_whole(comm, r3: torch.Tensor, chunks: Sequence[Tuple[int, int]])
     Pn, Rr, D = r3.shape
     if n == 1:
         return r3
-    if len(chunks) == 1 and Pn == 1:  # one gather, already (N*Rr, D) in global row order
-        dest = torch.empty(n * Rr * D, dtype=r3.dtype, device=r3.device)
-        comm.all_gather_into(dest.view(n, Rr, D), r3[0].contiguous())
-        return dest.view(1, n * Rr, D)
+    if len(chunks) == 1 and (Pn == 1 or r3.transpose(0, 1).is_contiguous()):
+        # one gather of the (Rr, Pn*D) rows as they are: (N*Rr, Pn, D) is already global row
+        # order, handed out as a (Pn, T, D) view (row stride Pn*D) for the GEMM to read in place
+        dest = torch.empty(n * Rr * Pn * D, dtype=r3.dtype, device=r3.device)
+        comm.all_gather_into(dest.view(n, Rr, Pn, D), r3.transpose(0, 1).contiguous())
+        return dest.view(n * Rr, Pn, D).transpose(0, 1)
     rt = (r3[0] if Pn == 1 else r3.transpose(0, 1)).contiguous()
     row_bytes = n * Pn * D * r3.element_size()
     budget = FLAGS.chunk_budget_mb * 2**20 / 4 if FLAGS.chunk_budget_mb > 0 else GROUP_BYTES
