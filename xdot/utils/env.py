@@ -42,6 +42,8 @@
 ``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
                                row kernel (default 1: VALU of one sub-tile issues between the
                                next sub-tile's MFMAs; 1.5 % faster kernel)
+``XDOT_ROWS_NSPLIT``           column splits of the flash backward row kernel (default: the
+                               occupancy model; 1 measured 7 % / 32 % slower at N = 1 / 8 ranks)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
