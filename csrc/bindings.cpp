@@ -75,6 +75,60 @@ int gemm_mode() {
   return v;
 }
 
+// XDOT_GEMM_LIB: 1 (default) = plain GEMMs (one uniform batch level, K segments contiguous,
+// output dtype = input dtype) that fill >= 2 rounds of 256x256 tiles go to the library GEMM
+// (at::baddbmm -> hipBLASLt) on in-place strided views; 0 = always the xdot kernels
+int gemm_lib() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM_LIB");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+// The library route of xdot.gemm: true when it ran.  opA / opB / C are expressed as strided
+// views of the operands' storage (no copies; the BLAS reads leading dimensions / batch
+// strides directly).  Measured (scripts/gemm_lib_ab.sh, MI355X): hipBLASLt 1.2-1.35x the
+// 256x256 kernel on bf16 nt 75000^2 x 768 and all 75000 x 768 x 75000, 1.2x the 128x128 fp32
+// kernel; the xdot kernels stay ahead on skinny long-K bf16 products (all3: 25000 x 768 x
+// 75000, split-K: 1.4x) and own every layout a single strided batch cannot express (two batch
+// levels, scattered K segments, mixed dtypes, small products).
+bool gemm_library(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K,
+                  int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA1,
+                  int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1, int64_t sC2, int64_t sAseg, int64_t sBseg,
+                  bool a_mc, bool b_mc, double alpha, double beta) {
+  if (C.scalar_type() != A.scalar_type() || K == 0) return false;
+  // one batch level
+  int64_t nb = nb1 * nb2, sa = 0, sb = 0, sc = 0;
+  if (nb1 == 1) { sa = sA2; sb = sB2; sc = sC2; }
+  else if (nb2 == 1) { sa = sA1; sb = sB1; sc = sC1; }
+  else if (sA1 == nb2 * sA2 && sB1 == nb2 * sB2 && sC1 == nb2 * sC2) { sa = sA2; sb = sB2; sc = sC2; }
+  else return false;
+  if (nb > 1 && sc == 0) return false;  // (a broadcast operand, batch stride 0, is fine)
+  // K segments that continue each other are one longer K
+  if (nseg > 1) {
+    if (sAseg != (a_mc ? K * lda : K) || sBseg != (b_mc ? K * ldb : K)) return false;
+    K *= nseg;
+  }
+  // 16-bit: only where the output alone fills >= 2 rounds of 256x256 tiles (skinny long-K
+  // products keep the split-K kernel); fp32: the library's exact-fp32 GEMM is ahead everywhere
+  // measured (1.1-1.2x the 128x128 kernel), so every large plain product
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb;
+  const double flop = 2.0 * (double)M * (double)N * (double)K * (double)nb;
+  if (flop < 2e10 || (A.element_size() == 2 && tiles < 512)) return false;
+  const int64_t oa = A.storage_offset(), ob = B.storage_offset(), oc = C.storage_offset();
+  at::Tensor a = A.as_strided({nb, M, K}, {nb > 1 ? sa : M * K, a_mc ? 1 : lda, a_mc ? lda : 1}, oa);
+  at::Tensor b = B.as_strided({nb, K, N}, {nb > 1 ? sb : K * N, b_mc ? ldb : 1, b_mc ? 1 : ldb}, ob);
+  at::Tensor c = C.as_strided({nb, M, N}, {nb > 1 ? sc : M * N, ldc, 1}, oc);
+  if (nb == 1) {
+    at::Tensor c2 = c.select(0, 0);
+    at::addmm_out(c2, c2, a.select(0, 0), b.select(0, 0), beta, alpha);
+  } else {
+    at::baddbmm_out(c, c, a, b, beta, alpha);
+  }
+  return true;
+}
+
 void check_launch(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "xdot: ", what, " launch failed: ", hipGetErrorString(e));
 }
@@ -127,6 +181,10 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   // leave CUs idle.  XDOT_GEMM=v1|v2 forces a path (v2 still needs the layout rules).
   // path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call; XDOT_GEMM overrides auto)
   const int mode = path ? (int)path : gemm_mode();
+  if (mode == 0 && gemm_lib() &&
+      gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
+                   b_mc, alpha, beta))
+    return;
   const bool half = A.element_size() == 2;
   bool v2 = half && vec && mode != 1;
   if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;

@@ -80,3 +80,53 @@ def test_gemm2_persistent_many_items(gpu, a_mc, b_mc):
 
 def test_gemm2_split_k_many_items(gpu):
     _run(gpu, torch.float16, False, True, 264, 512, 6000, batches=6, alpha=1.0)
+
+
+@pytest.mark.parametrize("K", [32, 64, 256])
+@pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
+def test_gemm2_persistent_interior_items(gpu, K, out_dt):
+    """interior 256x256 items only (uniform epilogue stores), more items than CUs, K % 32 == 0:
+    short items put epilogues back to back while the ring keeps streaming"""
+    _run(gpu, torch.bfloat16, False, False, 2304, 2560, K, batches=3, out_dt=out_dt)
+    _run(gpu, torch.bfloat16, False, True, 2304, 2560, K, batches=3, out_dt=out_dt)
+
+
+def test_gemm_library_route_matches_kernels(gpu):
+    """large plain products take the library route (in-place strided views, one batch level,
+    merged K segments); they must agree with the xdot kernels (path=2) on the same layouts"""
+    from xdot.ops.gemm import all_chunk_into, nt_chunk_into, tn_partials_into
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    N, Pn, R, D = 2, 2, 2048, 128
+    T = N * R
+    left = torch.randn(Pn, R, D, generator=g).to(gpu, torch.bfloat16)
+    chunk = torch.randn(N, Pn, R, D, generator=g).to(gpu, torch.bfloat16)
+    out = torch.empty(Pn, R, T, device=gpu, dtype=torch.bfloat16)
+    nt_chunk_into(out, left, chunk, 0)                      # nb1 = N, nb2 = Pn: merged batch? (no: sC1 = Rr)
+    ref = torch.cat([left.float() @ chunk.float()[j].transpose(-1, -2) for j in range(N)], -1)
+    assert torch.allclose(out.float(), ref, atol=0.1, rtol=2e-2)
+
+    # plain nt (N = 1): one batched GEMM over heads, output (Pn, R, T) in place
+    T1 = 16384
+    left1 = torch.randn(1, 4096, 256, generator=g).to(gpu, torch.bfloat16)
+    chunk1 = torch.randn(1, 1, T1, 256, generator=g).to(gpu, torch.bfloat16)
+    out1 = torch.empty(1, 4096, T1, device=gpu, dtype=torch.bfloat16)
+    nt_chunk_into(out1, left1, chunk1, 0, alpha=0.5)
+    ref1 = 0.5 * (left1.float() @ chunk1.float()[0].transpose(-1, -2))
+    assert torch.allclose(out1.float(), ref1, atol=0.25, rtol=2e-2)
+
+    # all with K segments that continue each other (merged into one K = T GEMM)
+    leftA = torch.randn(1, 4096, 4 * 4096, generator=g).to(gpu, torch.bfloat16) / 64
+    chunkA = torch.randn(4, 1, 4096, 1024, generator=g).to(gpu, torch.bfloat16)
+    outA = torch.empty(1, 4096, 1024, device=gpu, dtype=torch.bfloat16)
+    all_chunk_into(outA, leftA, chunkA, 0)
+    refA = sum(leftA.float()[..., j * 4096:(j + 1) * 4096] @ chunkA.float()[j] for j in range(4))
+    assert torch.allclose(outA.float(), refA, atol=0.1, rtol=2e-2)
+
+    # tn partials: N blocks (nb1 = N) of leftᵀ @ right
+    leftT = torch.randn(1, 4096, 2 * 4096, generator=g).to(gpu, torch.bfloat16) / 64
+    rightT = torch.randn(1, 4096, 1024, generator=g).to(gpu, torch.bfloat16)
+    send = torch.empty(2, 1, 4096, 1024, device=gpu, dtype=torch.bfloat16)
+    tn_partials_into(send, leftT, rightT)
+    refT = torch.stack([leftT.float()[..., j * 4096:(j + 1) * 4096].transpose(-1, -2) @ rightT.float() for j in range(2)])
+    assert torch.allclose(send.float(), refT, atol=0.1, rtol=2e-2)
