@@ -85,7 +85,7 @@ def main(argv=None, comm=None):
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
     sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
     # projection's all-reduce overlaps the attention backward
-    crit = torch.nn.MSELoss()
+    crit = xdot.MSELoss()  # fused loss + gradient pass (torch.nn.MSELoss semantics)
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.rand(a.batch, R, a.dim, device=dev, dtype=dt, generator=g)

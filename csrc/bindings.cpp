@@ -467,6 +467,28 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
   return out;
 }
 
+// fused MSE loss forward: (mean (y - t)^2 in y's dtype, dy = 2 (y - t) / n)
+std::tuple<at::Tensor, at::Tensor> mse_fwd(const at::Tensor& y, const at::Tensor& t) {
+  Range rr_("xdot.mse_fwd");
+  const auto st_ = y.scalar_type();
+  TORCH_CHECK(y.is_cuda() && t.is_cuda() && y.is_contiguous() && t.is_contiguous() && t.scalar_type() == st_ &&
+                  y.sizes() == t.sizes() && (st_ == at::kBFloat16 || st_ == at::kHalf || st_ == at::kFloat) &&
+                  aligned16(y.data_ptr()) && aligned16(t.data_ptr()) && y.numel() % (16 / y.element_size()) == 0 &&
+                  y.numel() > 0,
+              "xdot.mse_fwd: same-shape contiguous 16-byte aligned bf16/fp16/fp32 device tensors, numel % (16 B) == 0");
+  auto dy = at::empty_like(y);
+  const int64_t nv = y.numel() / (16 / y.element_size());
+  const int nparts = (int)std::min<int64_t>(1024, (nv + 255) / 256);
+  auto part = at::empty({nparts}, y.options().dtype(at::kFloat));
+  auto loss = at::empty({}, y.options());
+  c10::DeviceGuard guard(y.device());
+  TORCH_CHECK(xdot_mse_fwd_launch(y.data_ptr(), t.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), nparts,
+                                  loss.data_ptr(), y.numel(), dt_code(st_), cur_stream(y)) == 0,
+              "xdot.mse_fwd: launch rejected");
+  check_launch(hipGetLastError(), "mse_fwd");
+  return {loss, dy};
+}
+
 // row side of the flash kernels pre-multiplied by scale * log2(e), in the input dtype
 at::Tensor flash_prescale(const at::Tensor& x, double scale) {
   Range rr_("xdot.flash_prescale");
@@ -737,6 +759,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
+  m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
@@ -754,6 +777,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_delta", &flash_bwd_delta);
   m.impl("sum_partials", &sum_partials);
   m.impl("flash_prescale", &flash_prescale);
+  m.impl("mse_fwd", &mse_fwd);
   m.impl("flash_fwd_partial", &flash_fwd_partial);
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);

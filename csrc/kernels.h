@@ -129,6 +129,8 @@ int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, 
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
 int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
+int xdot_mse_fwd_launch(const void* y, const void* t, void* dy, float* part, int nparts, void* loss, int64_t n, int dt,
+                        hipStream_t st);
 // merge a->nsplit partial slots (a->opart, a->lpart) into a->out / a->lse
 int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
 // sum a->nsplit slots of a->dpart into a->drows

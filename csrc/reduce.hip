@@ -35,7 +35,75 @@ __global__ __launch_bounds__(256) void prescale_rows_kernel(const u32x4* __restr
   out[i] = v.u;
 }
 
+// Fused MSE loss, forward half: one pass over (y, t) writes dy = (2 / n) (y - t) in the input
+// dtype (the backward then only scales it by the incoming gradient) and one fp32 partial of
+// sum (y - t)^2 per workgroup; mse_final sums the partials in order (deterministic) into the
+// mean.  Replaces torch's MSELoss chain (sub, pow, mean-reduce, and a second pass over y and t
+// plus fills in the backward).
+template <int DT>
+__global__ __launch_bounds__(256) void mse_fwd_kernel(const u32x4* __restrict__ y, const u32x4* __restrict__ t,
+                                                       u32x4* __restrict__ dy, float* __restrict__ part, int64_t nv,
+                                                       float g2) {
+  using TT = typename dt_traits<DT>::T;
+  constexpr int V = 16 / sizeof(TT);
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+    union { u32x4 u; TT e[V]; } a, b, o;
+    a.u = y[i];
+    b.u = t[i];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float d = (float)a.e[e] - (float)b.e[e];
+      acc = __builtin_fmaf(d, d, acc);
+      o.e[e] = (TT)(d * g2);
+    }
+    dy[i] = o.u;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void mse_final_kernel(const float* __restrict__ part, int np, void* __restrict__ loss,
+                                                         float inv_n) {
+  using TT = typename dt_traits<DT>::T;
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *reinterpret_cast<TT*>(loss) = (TT)(((red[0] + red[1]) + (red[2] + red[3])) * inv_n);
+}
+
 }  // namespace xdot
+
+extern "C" int xdot_mse_fwd_launch(const void* y, const void* t, void* dy, float* part, int nparts, void* loss,
+                                   int64_t n, int dt, hipStream_t st) {
+  using namespace xdot;
+  if (n == 0) return -1;
+  const int V = dt == DT_F32 ? 4 : 8;
+  if (n % V) return -1;
+  const int64_t nv = n / V;
+  const u32x4* yi = reinterpret_cast<const u32x4*>(y);
+  const u32x4* ti = reinterpret_cast<const u32x4*>(t);
+  u32x4* o = reinterpret_cast<u32x4*>(dy);
+  const float g2 = 2.f / (float)n, inv_n = 1.f / (float)n;
+#define XDOT_MSE(D)                                                                                          \
+  hipLaunchKernelGGL(mse_fwd_kernel<D>, dim3(nparts), dim3(256), 0, st, yi, ti, o, part, nv, g2);            \
+  hipLaunchKernelGGL(mse_final_kernel<D>, dim3(1), dim3(256), 0, st, part, nparts, loss, inv_n);
+  if (dt == DT_BF16) { XDOT_MSE(DT_BF16) }
+  else if (dt == DT_F16) { XDOT_MSE(DT_F16) }
+  else if (dt == DT_F32) { XDOT_MSE(DT_F32) }
+  else return -1;
+#undef XDOT_MSE
+  return 0;
+}
 
 extern "C" int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, int dt, hipStream_t st) {
   using namespace xdot;

@@ -15,4 +15,4 @@ from .parallel import (distributed_matmul_nt, distributed_matmul_all, distribute
                        LeftTransposeMultiplication, seq_parallel_attention, broadcast_parameters,
                        allreduce_gradients, GradSync, gather_sequence)
 from .models import DistributedDotProductAttn  # noqa: E402,F401
-from .ops import scale_mask_softmax, linear, FusedAdamW  # noqa: E402,F401
+from .ops import scale_mask_softmax, linear, FusedAdamW, MSELoss, mse_loss  # noqa: E402,F401

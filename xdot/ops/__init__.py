@@ -4,3 +4,4 @@ from .softmax import (ScaleMaskSoftmax, scale_mask_softmax, scale_mask_softmax_f
                       scale_mask_softmax_bwd)
 from .linear import linear, weight_grad  # noqa: F401
 from .optim import FusedAdamW  # noqa: F401
+from .loss import mse_loss, MSELoss  # noqa: F401
