@@ -482,7 +482,10 @@ class SeqParallelAttention(torch.autograd.Function):
         else:
             qvg = bufs[0]
             dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mask, H, scale)
-            h, dqv = reduce_async(torch.cat([dq_parts, dv_parts], dim=-1))
+            parts = torch.cat([dq_parts, dv_parts], dim=-1)
+            if k.dtype in (torch.bfloat16, torch.float16) and not FLAGS.grad_fp32:
+                parts = parts.to(k.dtype)  # the HIP path's wire dtype (one rounding per partial)
+            h, dqv = reduce_async(parts)
             handles = [h]
         for h in handles:
             if h is not None:

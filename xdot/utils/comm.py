@@ -428,8 +428,13 @@ class ThreadGroup:
     through :meth:`comm`.  Device work is ordered with events, so the collectives are
     stream-correct on a GPU (each thread may use its own stream)."""
 
-    def __init__(self, world_size: int, timeout: float = 120.0):
+    def __init__(self, world_size: int, timeout: float = 120.0, ring_reduce: bool = False):
+        """``ring_reduce``: reduce-scatter 16-bit tensors the way RCCL's ring does -- in the
+        tensor's own dtype, one rounding per hop, block r accumulated from rank r+1 around to
+        rank r -- instead of gloo's fp32 accumulation (numerics tests of the default bf16
+        gradient partials)."""
         self.world_size = world_size
+        self.ring_reduce = ring_reduce
         self._barrier = threading.Barrier(world_size, timeout=timeout)
         self._slots: List[object] = [None] * world_size
 
@@ -507,6 +512,15 @@ class ThreadComm(Communicator):
     def reduce_scatter(self, out, inp, async_op=False):
         parts = self._exchange(inp.contiguous())
         n = out.numel()
+        if self.g.ring_reduce and out.dtype in (torch.bfloat16, torch.float16):
+            ws = self.world_size
+            blk = [p.reshape(-1)[self.rank * n:(self.rank + 1) * n] for p in parts]
+            acc = blk[(self.rank + 1) % ws].clone()
+            for s in range(2, ws + 1):  # one rounding to the wire dtype per ring hop
+                acc = (acc.float() + blk[(self.rank + s) % ws].float()).to(out.dtype)
+            out.view(-1).copy_(acc) if out.is_contiguous() else out.copy_(acc.view(out.shape))
+            self._done(out)
+            return Handle(out=out) if async_op else None
         acc_dt = torch.float32 if out.dtype in (torch.bfloat16, torch.float16) else out.dtype
         acc = torch.zeros(n, dtype=acc_dt, device=out.device)
         for p in parts:
