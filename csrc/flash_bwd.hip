@@ -26,6 +26,18 @@
 
 #include <type_traits>
 
+// Compile-time scheduling knobs (A/B'd with scripts/build_variant.sh + scripts/so_ab.sh,
+// profiles/r2_sched_variants.md); -1 disables an iglp hint.
+#ifndef XDOT_A0_AHEAD
+#define XDOT_A0_AHEAD 2   // rows kernel, phase A0: operand reads ahead of the MFMAs (3/4: no gain)
+#endif
+#ifndef XDOT_A0_IGLP
+#define XDOT_A0_IGLP 1    // rows kernel, phase A0: LLVM iglp_opt(1) MFMA/DS interleave (-2 % at N=1)
+#endif
+#ifndef XDOT_COLS_IGLP
+#define XDOT_COLS_IGLP 0  // cols kernel tile body: iglp_opt(0) (-1 %; iglp_opt(1) +0.6 %)
+#endif
+
 namespace xdot {
 namespace fa {
 
@@ -174,16 +186,24 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     auto opnd = [&](int tt, int i) { return (i & 1) ? row_frag<D>(vs, tt * 32, i >> 1, L) : row_frag<D>(qs, tt * 32, i >> 1, L); };
     f32x16 s0, d0, s1, d1;
     {
-      u32x4 o0 = opnd(0, 0), o1 = opnd(0, 1);
+      // A0: operand reads XDOT_A0_AHEAD MFMAs ahead (s1/d1 are not live yet, so the window
+      // can be deeper here than in the later phases)
+      constexpr int AH = XDOT_A0_AHEAD;
+      u32x4 ow[NA];
+#pragma unroll
+      for (int i = 0; i < AH && i < NA; ++i) ow[i] = opnd(0, i);
+#if XDOT_A0_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(XDOT_A0_IGLP);
+#endif
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        u32x4 o2 = o1;
-        if (i + 2 < NA) o2 = opnd(0, i + 2);
+        if (i + AH < NA) ow[i + AH] = opnd(0, i + AH);
         const int ks = i >> 1;
-        if (i & 1) d0 = mfma32<DT>::run(o0, df[ks], ks == 0 ? dseed : d0);
-        else s0 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sseed : s0);
-        o0 = o1;
-        o1 = o2;
+        if (i & 1) d0 = mfma32<DT>::run(ow[i], df[ks], ks == 0 ? dseed : d0);
+        else s0 = mfma32<DT>::run(ow[i], kf[ks], ks == 0 ? sseed : s0);
+#ifdef XDOT_A0_PIN
+        __builtin_amdgcn_sched_barrier(0);
+#endif
       }
     }
     {
@@ -494,6 +514,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       flag = __builtin_amdgcn_readfirstlane((f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2));
     }
     if (flag != 1 && c0 < a.T) {
+#if XDOT_COLS_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(XDOT_COLS_IGLP);
+#endif
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], PS ? lse_seed(ls, tt) : f32x16{});

@@ -129,8 +129,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   // ---- software-pipelined sweep ----------------------------------------------------
   // Iteration kt overlaps the MFMAs of one tile with the VALU work of another:
   //   block A: Sᵀ(kt+1) = Q(kt+1)·Kᵀ (12 MFMAs)   ||  P(kt) = 2^(S(kt)·c2 - m), packed to bf16
-  //   block B: Oᵀ += V(kt)ᵀ·P(kt)ᵀ (12 MFMAs)     ||  row sums of P(kt), row max of S(kt+1)
-  // then the (rare, deferred) rescale for tile kt+1.  The score registers alternate between
+  //   block B: Oᵀ += V(kt)ᵀ·P(kt)ᵀ (12 MFMAs)     ||  row sums of P(kt)
+  // then the row max of S(kt+1) and the (rare, deferred) rescale for tile kt+1 (moving the max
+  // into block B's MFMA gaps measured 1.5 % slower: profiles/r2_sched_variants.md).  The score registers alternate between
   // two sets (PAR) and the ring stage rotates over three (BUF): the loop is unrolled by 6 so
   // both are compile-time.  Iteration kt DMAs Q(kt+3) and V(kt+2): each has one full
   // iteration in flight before the wait at the bottom of the next one.
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
           for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
           asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
+
           __builtin_amdgcn_sched_barrier(0);
           v0 = v1;
           v1 = v2;
