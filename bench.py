@@ -126,6 +126,7 @@ def main(argv=None, comm=None):
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
+    th = time.perf_counter()  # host done enqueuing (diagnostic: close to t1 = host-bound step)
     sync_all()
     t1 = time.perf_counter()
     if prof is not None:
@@ -163,6 +164,7 @@ def main(argv=None, comm=None):
                        "seq_len": T, "parallelism": f"sp{n}", "impl": impl, "mask": a.mask,
                        "step": "fwd+bwd+grad-allreduce+AdamW" if not a.no_optim else "fwd+bwd+grad-allreduce"},
             "tokens_per_s": round(a.batch * T / (ms / 1e3), 1),
+            "host_enqueue_ms_per_step": round((th - t0) * 1e3 / max(1, a.steps), 4),
             "loss": lossv,
         }
         if emulated:
