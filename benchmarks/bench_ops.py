@@ -48,6 +48,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-local", action="store_true", help="skip the single-GPU torch.matmul baseline")
     ap.add_argument("--file", default=None, help="JSON list to append the record to")
+    ap.add_argument("--p2p-gbps", type=float, default=None, help="emulated ring-hop link rate (GB/s, --emulate)")
+    ap.add_argument("--schedule", default=None, choices=["gather", "ring"],
+                    help="product schedule (default XDOT_OPS_SCHEDULE / gather); also used by the *_fb modes")
     ap.add_argument("--emulate", type=int, default=None, metavar="N",
                     help="run ONE rank of an N-rank job on this device (EmulatedComm: collectives are "
                          "device-local copies) -- per-rank compute of the reference's N=3 setup on 1 GPU")
@@ -104,7 +107,7 @@ def main(argv=None):
     from xdot.utils import comm as C
     import xdot.parallel.functional as F
 
-    comm = C.EmulatedComm(a.emulate, link_gbps=a.link_gbps) if a.emulate else C.init("auto")
+    comm = C.EmulatedComm(a.emulate, link_gbps=a.link_gbps, p2p_gbps=a.p2p_gbps) if a.emulate else C.init("auto")
     ctx = C.use_comm(comm)  # the functional ops pick up the thread's communicator
     ctx.__enter__()
     n, rank = comm.world_size, comm.rank
@@ -118,8 +121,11 @@ def main(argv=None):
     R, D = T // n, a.dim
     torch.manual_seed(111)
     torch.set_grad_enabled(False)
-    rec = {"mode": a.mode, "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype,
-           "link_gbps": a.link_gbps}
+    if a.schedule:
+        from xdot.utils.env import FLAGS
+        FLAGS.ops_schedule = a.schedule
+    rec = {"mode": a.mode, "schedule": a.schedule or "gather", "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype,
+           "link_gbps": a.link_gbps, "p2p_gbps": a.p2p_gbps}
 
     fb = a.mode.endswith("_fb")
     torch.set_grad_enabled(fb)

@@ -104,12 +104,21 @@ bool gemm_library(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64
   else if (nb2 == 1) { sa = sA1; sb = sB1; sc = sC1; }
   else if (sA1 == nb2 * sA2 && sB1 == nb2 * sB2 && sC1 == nb2 * sC2) { sa = sA2; sb = sB2; sc = sC2; }
   else return false;
-  if (nb > 1 && sc == 0) return false;  // (a broadcast operand, batch stride 0, is fine)
   // K segments that continue each other are one longer K
   if (nseg > 1) {
     if (sAseg != (a_mc ? K * lda : K) || sBseg != (b_mc ? K * ldb : K)) return false;
     K *= nseg;
   }
+  // conservative layouts only: every batch its own dense-strided matrix (no broadcast operand,
+  // no batches interleaved inside one output row -- the per-rank column blocks of nt's (P, R, T)
+  // output stay on the xdot kernels), 16-byte aligned bases, leading dims and batch strides
+  if (nb > 1 && (sa < (a_mc ? K * lda : M * lda) || sb < (b_mc ? K * ldb : N * ldb) || sc < M * ldc)) return false;
+  const int64_t ev = 16 / (int64_t)A.element_size();
+  auto al = [&](int64_t v) { return v % ev == 0; };
+  if (ldc != N) return false;  // whole output rows (no column-slice views)
+  if (!aligned16(A.data_ptr()) || !aligned16(B.data_ptr()) || !aligned16(C.data_ptr()) || !al(lda) || !al(ldb) ||
+      !al(ldc) || (nb > 1 && (!al(sa) || !al(sb) || !al(sc))))
+    return false;
   // 16-bit: only where the output alone fills >= 2 rounds of 256x256 tiles (skinny long-K
   // products keep the split-K kernel); fp32: the library's exact-fp32 GEMM is ahead everywhere
   // measured (1.1-1.2x the 128x128 kernel), so every large plain product

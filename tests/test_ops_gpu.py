@@ -10,8 +10,12 @@ from _dist import run_gloo
 pytestmark = pytest.mark.gpu
 
 
-def _ops_case(rank, ws, dt_name, offset, heads=False):
+def _ops_case(rank, ws, dt_name, offset, heads=False, schedule=None):
     import xdot.parallel.functional as F
+    from xdot.utils.env import FLAGS
+
+    if schedule is not None:
+        FLAGS.ops_schedule = schedule
 
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32}[dt_name]
     dev = torch.device("cuda", 0)
@@ -54,3 +58,12 @@ def test_distributed_products_three_ranks(gpu, dt_name, offset, heads):
     """``heads``: operands are (1, P, R, c) head-split views of (1, R, P*c) tensors (the
     materialised module's layout): read and produced in place, no transpose copies."""
     run_gloo(_ops_case, 3, dt_name, offset, heads, timeout=300)
+
+
+@pytest.mark.parametrize("dt_name", ["bf16", "fp32"])
+@pytest.mark.parametrize("heads", [False, True])
+def test_distributed_products_ring_schedule(gpu, dt_name, heads):
+    """the same products as point-to-point ring hops (XDOT_OPS_SCHEDULE=ring): nt / all consume
+    each arriving shard with one GEMM into its column block / K slice, tn's fp32 accumulators
+    travel the ring; odd R = 333 and head-split views included"""
+    run_gloo(_ops_case, 3, dt_name, None, heads, "ring", timeout=300)

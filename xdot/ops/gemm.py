@@ -86,6 +86,28 @@ def nt_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, c0
     ov[..., c0:c0 + c] = part.permute(1, 2, 0, 3).to(out.dtype)
 
 
+def nt_block_into(out: torch.Tensor, left: torch.Tensor, blk: torch.Tensor, alpha: float = 1.0) -> None:
+    """``out[p] = alpha * left[p] @ blk[p]ᵀ``: (Pn, R, D) x (Pn, c, D) -> (Pn, R, c).  Every operand
+    may be a strided view with unit inner stride (``out``: e.g. one source rank's column block
+    of the (Pn, R, T) ``nt`` result, written in place by the ring schedule)."""
+    Pn, R, D = left.shape
+    c = blk.shape[-2]
+    if _ext.use_hip(out, left, blk) and hip_dtype_ok(left, blk) and out.dtype in _HIP_IN:
+        a, sA, lda = _m3(left)
+        b, sB, ldb = _m3(blk)
+        o, sC, ldc = _m3(out)
+        strided_gemm(a, b, o, M=R, N=c, K=D, nb2=Pn, lda=lda, ldb=ldb, ldc=ldc, sA2=sA, sB2=sB, sC2=sC,
+                     a_mc=False, b_mc=False, alpha=alpha)
+        if o is not out:
+            out.copy_(o)
+        return
+    ct = torch.promote_types(left.dtype, blk.dtype)
+    r = torch.matmul(left.to(ct), blk.to(ct).transpose(-1, -2))
+    if alpha != 1.0:
+        r = r * alpha
+    out.copy_(r.to(out.dtype))
+
+
 # ---------------------------------------------------------------------------------------
 # all: out[p, :, d0:d0+c] = sum_j left[p, :, j*R:(j+1)*R] @ chunk[j, p]
 # ---------------------------------------------------------------------------------------

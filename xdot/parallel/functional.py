@@ -32,6 +32,14 @@ MI355X design, per op:
   1/N the collective launches of the reference's N full all-reduces (with N-1 leaked
   handles).  Half-precision partials are reduced in fp32.
 * No host barrier before each op (reference calls ``MPI.Barrier`` each time).
+* ``schedule='ring'`` (or ``XDOT_OPS_SCHEDULE=ring``): the same three products as a ring of
+  point-to-point hops (``Communicator.sendrecv``: RCCL ``batch_isend_irecv``): ``nt`` / ``all``
+  pass each rank's ``right`` shard around the ring and consume the arriving shard with one
+  GEMM while the next hop is in flight (two shard buffers instead of the gathered side);
+  ``tn`` sends each destination's fp32 accumulator around the ring, every rank adding its
+  partial (computed under the previous hop) — the reduce-scatter as N-1 hops.  Over xGMI's
+  full mesh the collectives are faster (one link per hop vs all seven); the ring is the
+  schedule whose resident comm buffers do not grow with N.
 
 Output dtype = input dtype (the reference hard-codes fp32 via ``torch.empty`` without dtype
 and therefore crashes in bf16); pass ``out_dtype=torch.float32`` for reference-identical fp32
@@ -46,6 +54,7 @@ import torch
 from ..ops import gemm as G
 from ..utils import comm as _comm
 from ..utils.checks import check_consistent
+from ..utils.env import FLAGS
 from ..utils.profiling import measure
 from .schedule import (GROUP_BYTES, Offset, gather_pipeline, gather_rows_grouped, gather_rows_whole,
                        plan_chunks, resolve_offset)
@@ -76,7 +85,7 @@ def _result_dtype(left, right, out_dtype):
 @measure
 def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offset = None, *,
                           comm: Optional[_comm.Communicator] = None, alpha: float = 1.0,
-                          out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+                          out_dtype: Optional[torch.dtype] = None, schedule: Optional[str] = None) -> torch.Tensor:
     """Row block ``r`` of ``L·Rᵀ``: (P, R, D) x (P, R, D) -> (P, R, T).
 
     ``offset``: rows of ``right`` gathered per step (``None``: whole shard; ``'auto'``:
@@ -102,6 +111,9 @@ def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offse
         return out.view(*P, R, T)
     l3 = left.reshape(Pn, R, D)
     r3 = right.reshape(Pn, Rr, D)
+    if _schedule(schedule) == "ring" and n > 1:
+        _ring_nt(comm, l3, r3, out, alpha)
+        return out.view(*P, R, T)
 
     def consume(s, e, gathered):  # gathered: (N, Pn, c, D)
         G.nt_chunk_into(out, l3, gathered, s, alpha)
@@ -121,7 +133,8 @@ def distributed_matmul_nt(left: torch.Tensor, right: torch.Tensor, offset: Offse
 @measure
 def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offset = None, *,
                            comm: Optional[_comm.Communicator] = None,
-                           out_dtype: Optional[torch.dtype] = None, chunking: str = "rows") -> torch.Tensor:
+                           out_dtype: Optional[torch.dtype] = None, chunking: str = "rows",
+                           schedule: Optional[str] = None) -> torch.Tensor:
     """Row block ``r`` of ``L·R``: (P, R, T) x (P, R, D) -> (P, R, D).
 
     ``offset`` bounds the per-step gather buffer exactly as in the reference, where a step
@@ -154,6 +167,14 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
     check_consistent(comm, "all", left, right, tuple(chunks))
     l3 = left.reshape(Pn, R, T)
     r3 = right.reshape(Pn, Rr, D)
+    if _schedule(schedule) == "ring" and n > 1:
+        out = torch.empty((Pn, R, D), dtype=_result_dtype(left, right, out_dtype), device=left.device)
+        if R == 0 or D == 0:
+            return out.reshape(*P, R, D)
+        if T == 0:
+            return out.zero_().reshape(*P, R, D)
+        _ring_all(comm, l3, r3, out)
+        return out.reshape(*P, R, D)
     rm = _rmajor(r3) and R > 1
     if rm:  # R-major like `right` (head-split view): the module's head merge is then a free view
         out = torch.empty((R, Pn, D), dtype=_result_dtype(left, right, out_dtype), device=left.device).transpose(0, 1)
@@ -193,7 +214,7 @@ def distributed_matmul_all(left: torch.Tensor, right: torch.Tensor, offset: Offs
 def distributed_matmul_tn(left: torch.Tensor, right: torch.Tensor, *,
                           comm: Optional[_comm.Communicator] = None,
                           out_dtype: Optional[torch.dtype] = None,
-                          reduce_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+                          reduce_dtype: Optional[torch.dtype] = None, schedule: Optional[str] = None) -> torch.Tensor:
     """Row block ``r`` of ``Lᵀ·R``: (P, R, T) x (P, R, D) -> (P, R, D).
 
     One batched GEMM into an (N, P, R, D) send buffer + one reduce-scatter.
@@ -220,6 +241,10 @@ def distributed_matmul_tn(left: torch.Tensor, right: torch.Tensor, *,
     if reduce_dtype is None:
         reduce_dtype = torch.float32 if res_dt in (torch.bfloat16, torch.float16) and n > 1 else res_dt
     r3 = right.reshape(Pn, R, D)
+    if _schedule(schedule) == "ring" and n > 1:
+        if R == 0 or D == 0:
+            return torch.zeros((*P, Rc, D), dtype=res_dt, device=left.device)
+        return _ring_tn(comm, left.reshape(Pn, R, T), r3, reduce_dtype).to(res_dt).reshape(*P, Rc, D)
     rm = _rmajor(r3)  # R-major operand (head-split view) -> R-major send buffer and result
     if rm:
         sbuf = torch.empty((n, Rc, Pn, D), dtype=reduce_dtype, device=left.device)
@@ -237,6 +262,81 @@ def distributed_matmul_tn(left: torch.Tensor, right: torch.Tensor, *,
         comm.reduce_scatter(obuf, sbuf)
         out = obuf.transpose(0, 1) if rm else obuf
     return out.to(res_dt).reshape(*P, Rc, D)
+
+
+# ---------------------------------------------------------------------------------------
+# ring schedule (point-to-point hops)
+# ---------------------------------------------------------------------------------------
+def _schedule(schedule: Optional[str]) -> str:
+    s = (schedule or FLAGS.ops_schedule or "gather").lower()
+    if s not in ("gather", "ring"):
+        raise ValueError(f"schedule must be 'gather' or 'ring', got {s!r}")
+    return s
+
+
+def _ring_pass(comm: _comm.Communicator, shard: torch.Tensor, consume) -> None:
+    """Every rank's ``shard`` visits every rank: at step s rank r holds the shard of rank
+    (r - s) mod N and calls ``consume(src, buf)`` on it while the hop of step s+1 is in flight.
+    The rank's own shard is sent from the caller's tensor (never written); two receive buffers
+    alternate.  Stream-ordered: a buffer is re-received into only after the hop that sent it
+    completed and after the GEMM that read it was enqueued before that receive."""
+    n, r = comm.world_size, comm.rank
+    nxt, prv = (r + 1) % n, (r - 1) % n
+    cur = shard.contiguous()
+    spare = [torch.empty_like(cur), torch.empty_like(cur)]
+    for s in range(n):
+        h = None
+        nb = None
+        if s < n - 1:
+            nb = spare[s % 2]
+            h = comm.sendrecv(cur, nb, nxt, prv, async_op=True)
+        consume((r - s) % n, cur)
+        if h is not None:
+            h.wait()
+            cur = nb
+
+
+def _ring_nt(comm, l3, r3, out, alpha):
+    Rr = r3.shape[1]
+    _ring_pass(comm, r3, lambda j, blk: G.nt_block_into(out[..., j * Rr:(j + 1) * Rr], l3, blk, alpha))
+
+
+def _ring_all(comm, l3, r3, out):
+    Rr = r3.shape[1]
+    acc = out if out.dtype in (torch.float32, torch.float64) else torch.empty_like(out, dtype=torch.float32)
+    first = [True]
+
+    def consume(j, blk):
+        G.all_rows_chunk_into(acc, l3, blk.unsqueeze(0), j * Rr, accumulate=not first[0])
+        first[0] = False
+
+    _ring_pass(comm, r3, consume)
+    if acc is not out:
+        out.copy_(acc)
+
+
+def _ring_tn(comm, l3, r3, reduce_dtype):
+    """Ring reduce-scatter of the tn partials: the accumulator of destination d starts at rank
+    d+1 and travels N-1 hops, each rank adding left[:, :, d*R:(d+1)*R]ᵀ·right (computed while
+    the previous hop is in flight); rank r ends holding destination r's sum."""
+    n, r = comm.world_size, comm.rank
+    Pn, R, D = r3.shape
+    nxt, prv = (r + 1) % n, (r - 1) % n
+
+    def partial(d, dst):
+        G.tn_partials_into(dst.unsqueeze(0), l3[..., d * R:(d + 1) * R], r3)
+
+    cur = torch.empty((Pn, R, D), dtype=reduce_dtype, device=r3.device)
+    nb = torch.empty_like(cur)
+    part = torch.empty_like(cur)
+    partial((r - 1) % n, cur)
+    for s in range(1, n):
+        h = comm.sendrecv(cur, nb, nxt, prv, async_op=True)
+        partial((r - 1 - s) % n, part)
+        h.wait()
+        nb.add_(part)
+        cur, nb = nb, cur
+    return cur
 
 
 @measure

@@ -44,6 +44,11 @@
                                next sub-tile's MFMAs; 1.5 % faster kernel)
 ``XDOT_ROWS_NSPLIT``           column splits of the flash backward row kernel (default: the
                                occupancy model; 1 measured 7 % / 32 % slower at N = 1 / 8 ranks)
+``XDOT_OPS_SCHEDULE``          ``ring``: the distributed products (``nt`` / ``all`` / ``tn`` and the
+                               autograd ops / materialised path built on them) move the shards
+                               rank to rank over point-to-point send/recv instead of all-gather /
+                               reduce-scatter (default ``gather``: faster over xGMI's full mesh;
+                               the ring holds two shards instead of the gathered side)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
@@ -76,6 +81,7 @@ class _Flags:
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
+        self.ops_schedule = os.environ.get("XDOT_OPS_SCHEDULE", "gather").strip().lower() or "gather"
 
 
 FLAGS = _Flags()
