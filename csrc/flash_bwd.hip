@@ -37,6 +37,12 @@
 #ifndef XDOT_COLS_IGLP
 #define XDOT_COLS_IGLP 0  // cols kernel tile body: iglp_opt(0) (-1 %; iglp_opt(1) +0.6 %)
 #endif
+#ifndef XDOT_ROWS_PIN
+#define XDOT_ROWS_PIN 1   // rows kernel, phases A1 / K0: MFMA + VALU order pinned by sched_barrier
+#endif
+#ifndef XDOT_ROWS_PHASE_IGLP
+#define XDOT_ROWS_PHASE_IGLP -1  // rows kernel, phases A1 / K0: iglp_opt hint
+#endif
 
 namespace xdot {
 namespace fa {
@@ -207,6 +213,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
       }
     }
     {
+#if XDOT_ROWS_PHASE_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(XDOT_ROWS_PHASE_IGLP);
+#endif
       u32x4 o0 = opnd(1, 0), o1 = opnd(1, 1);
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -217,13 +226,18 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         else s1 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sseed : s1);
 #pragma unroll
         for (int j = (i * 16) / NA; j < ((i + 1) * 16) / NA; ++j) elem(s0, d0, 0, j);
+#if XDOT_ROWS_PIN
         __builtin_amdgcn_sched_barrier(0);
+#endif
         o0 = o1;
         o1 = o2;
       }
     }
     const u32x4 p00 = acc_to_frag<DT>(s0, 0), p01 = acc_to_frag<DT>(s0, 1);
     {
+#if XDOT_ROWS_PHASE_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(XDOT_ROWS_PHASE_IGLP);
+#endif
       u32x4 t0 = tr_frag<D>(qs, 0, 0, L), t1 = tr_frag<D>(qs, 16, 0, L);
 #pragma unroll
       for (int i = 0; i < NK; ++i) {
@@ -232,7 +246,9 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         dk[i >> 1] = mfma32<DT>::run(t0, (i & 1) ? p01 : p00, dk[i >> 1]);
 #pragma unroll
         for (int j = (i * 16) / NK; j < ((i + 1) * 16) / NK; ++j) elem(s1, d1, 1, j);
+#if XDOT_ROWS_PIN
         __builtin_amdgcn_sched_barrier(0);
+#endif
         t0 = t1;
         t1 = t2;
       }

@@ -28,6 +28,14 @@
 
 #include <type_traits>
 
+// scheduling knobs (A/B: scripts/build_variant.sh + scripts/so_ab.sh, profiles/r2_sched_variants.md)
+#ifndef XDOT_FWD_PIN
+#define XDOT_FWD_PIN 1    // blocks A / B: MFMA + VALU issue order pinned by sched_barrier
+#endif
+#ifndef XDOT_FWD_IGLP
+#define XDOT_FWD_IGLP -1  // blocks A / B: iglp_opt hint (-1: none)
+#endif
+
 namespace xdot {
 namespace fa {
 
@@ -224,6 +232,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       constexpr int NA = 2 * KS, NB = 4 * DB;
       u32x4 pf[4];
       {
+#if XDOT_FWD_IGLP >= 0
+        __builtin_amdgcn_iglp_opt(XDOT_FWD_IGLP);
+#endif
         u32x4 q0 = row_frag<D>(nxt, 0, 0, L), q1 = row_frag<D>(nxt, (1 / KS) * 32, 1 % KS, L);
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
@@ -236,7 +247,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
             sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
             if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
           }
+#if XDOT_FWD_PIN
           __builtin_amdgcn_sched_barrier(0);
+#endif
           q0 = q1;
           q1 = q2;
         }
@@ -244,6 +257,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       // ---- block B: P(kt)·V(kt) MFMAs, each followed by its share of the row sums ----
       float ls = 0.f;
       {
+#if XDOT_FWD_IGLP >= 0
+        __builtin_amdgcn_iglp_opt(XDOT_FWD_IGLP);
+#endif
         u32x4 v0 = tr_frag<D>(cur + IMG, 0, 0, L), v1 = tr_frag<D>(cur + IMG, 16, 0, L);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
@@ -255,7 +271,9 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
           for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
           asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
 
+#if XDOT_FWD_PIN
           __builtin_amdgcn_sched_barrier(0);
+#endif
           v0 = v1;
           v1 = v2;
         }

@@ -132,3 +132,26 @@ def test_gemm_library_route_matches_kernels(gpu):
     tn_partials_into(send, leftT, rightT)
     refT = torch.stack([leftT.float()[..., j * 4096:(j + 1) * 4096].transpose(-1, -2) @ rightT.float() for j in range(2)])
     assert torch.allclose(send.float(), refT, atol=0.1, rtol=2e-2)
+
+
+def test_nt_rank_blocks_at_eight_ranks(gpu):
+    """nt's eight per-rank column blocks of a (1, R, T) output (broadcast left, interleaved
+    output batches, odd R = 3125): the layout that must stay off the library GEMM route; and the
+    whole-shard case as one GEMM over all T columns"""
+    from xdot.ops.gemm import nt_chunk_into
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    N, R, D = 8, 3125, 768
+    left = torch.randn(1, R, D, generator=g).to(gpu, torch.bfloat16)
+    chunk = torch.randn(N, 1, R, D, generator=g).to(gpu, torch.bfloat16)
+    out = torch.empty(1, R, N * R, device=gpu, dtype=torch.bfloat16)
+    h = 1563  # two row chunks per shard: per-rank column blocks (the whole-shard case is one GEMM)
+    nt_chunk_into(out, left, chunk[:, :, :h], 0, alpha=0.25)
+    nt_chunk_into(out, left, chunk[:, :, h:], h, alpha=0.25)
+    torch.cuda.synchronize()
+    rows = torch.arange(0, R, 311)
+    ref = 0.25 * (left[0, rows].float() @ chunk[:, 0].float().reshape(N * R, D).t())
+    assert torch.allclose(out[0, rows].float(), ref, atol=0.15, rtol=2e-2)
+    out2 = torch.empty_like(out)
+    nt_chunk_into(out2, left, chunk, 0, alpha=0.25)
+    assert torch.allclose(out2[0, rows].float(), ref, atol=0.15, rtol=2e-2)

@@ -74,6 +74,14 @@ def nt_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, c0
     if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
         left, sA, lda = _m3(left)
         chunk, sBj, sBp, ldb = _m4(chunk)
+        if N > 1 and c0 == 0 and c == Rr and sBj == Rr * ldb:
+            # whole shards whose rank blocks continue each other along the rows (rank-major
+            # gather, or the R-major head-split gather): ONE GEMM over all T columns.  Per-rank
+            # column blocks would start off 16-byte boundaries whenever T/N is odd (R = 3125:
+            # 7 of 8 blocks) and fall back to element stores (measured 1.23 ms vs one GEMM)
+            strided_gemm(left, chunk, out, M=R, N=T, K=D, nb2=Pn, lda=lda, ldb=ldb, ldc=T, sA2=sA, sB2=sBp,
+                         sC2=R * T, a_mc=False, b_mc=False, alpha=alpha)
+            return
         strided_gemm(left, chunk, out[..., c0:], M=R, N=c, K=D, nb1=N, nb2=Pn,
                      lda=lda, ldb=ldb, ldc=T, sA1=0, sA2=sA, sB1=sBj, sB2=sBp,
                      sC1=Rr, sC2=R * T, a_mc=False, b_mc=False, alpha=alpha)
