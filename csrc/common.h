@@ -16,6 +16,10 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+// 16-byte vector at a 2-byte-aligned address: gfx950 under ROCm runs in unaligned-access mode,
+// so this is still ONE global_load/store_dwordx4 (GEMM epilogues writing column blocks that start
+// off 16-byte boundaries, e.g. nt's per-rank blocks at an odd T/N)
+typedef u32x4 u32x4_ua __attribute__((aligned(2)));
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 constexpr int kWave = 64;

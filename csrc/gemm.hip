@@ -240,7 +240,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   // ---- epilogue: per wave, 4 passes of 16 rows x 64 cols through LDS ----
   char* ep = smem + wave * 16 * EPI_ROW;
   constexpr int EO = 16 / sizeof(TO);  // output elements per 16-byte store
-  const bool vec_ld = (p.ldc % EO) == 0;  // + the strip's own address, tested per store
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -257,19 +256,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
     const float* src = reinterpret_cast<const float*>(ep + row * EPI_ROW + c0 * 4);
     if (gm < p.M) {
       TO* dst = C + (int64_t)gm * p.ldc + gn;
-      if (vec_ld && gn + 16 <= p.N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      if (gn + 16 <= p.N) {  // 16-byte stores at any element-aligned address (u32x4_ua)
 #pragma unroll
         for (int v = 0; v < 16 / EO; ++v) {
           union { u32x4 u; TO e[EO]; } o;
           if (p.beta != 0.f) {
-            o.u = *reinterpret_cast<const u32x4*>(dst + v * EO);
+            o.u = *reinterpret_cast<const u32x4_ua*>(dst + v * EO);
 #pragma unroll
             for (int e = 0; e < EO; ++e) o.e[e] = (TO)(src[v * EO + e] + p.beta * (float)o.e[e]);
           } else {
 #pragma unroll
             for (int e = 0; e < EO; ++e) o.e[e] = (TO)src[v * EO + e];
           }
-          *reinterpret_cast<u32x4*>(dst + v * EO) = o.u;
+          *reinterpret_cast<u32x4_ua*>(dst + v * EO) = o.u;
         }
       } else {
         for (int e = 0; e < 16; ++e)

@@ -339,17 +339,17 @@ __global__ __launch_bounds__(512) void gemm2_kernel(GemmArgs p, float* __restric
         } else {
           TO* dst = reinterpret_cast<TO*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)gm * p.ldc + gn;
           constexpr int EO = 16 / sizeof(TO);
-          if (gn + 16 <= p.N && (p.ldc % EO) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+          if (gn + 16 <= p.N) {  // 16-byte stores at any element-aligned address (u32x4_ua)
 #pragma unroll
             for (int c = 0; c < 16 / EO; ++c) {
               union { u32x4 u; TO e[EO]; } o;
-              if (p.beta != 0.f) o.u = *reinterpret_cast<const u32x4*>(dst + c * EO);
+              if (p.beta != 0.f) o.u = *reinterpret_cast<const u32x4_ua*>(dst + c * EO);
 #pragma unroll
               for (int e = 0; e < EO; ++e) {
                 const float x = v[(c * EO + e) >> 2][(c * EO + e) & 3] * p.alpha;
                 o.e[e] = (TO)(p.beta != 0.f ? x + p.beta * (float)o.e[e] : x);
               }
-              *reinterpret_cast<u32x4*>(dst + c * EO) = o.u;
+              *reinterpret_cast<u32x4_ua*>(dst + c * EO) = o.u;
             }
           } else {
 #pragma unroll
