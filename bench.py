@@ -49,6 +49,9 @@ def parse(argv=None):
                     help="collective backend (auto = RCCL on GPU); gloo lets several ranks share one GPU "
                          "for rehearsals")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step (fwd+bwd+grad sync+AdamW) in a HIP graph and replay it "
+                         "(xdot.utils.graphs.GraphedStep; single-GPU / emulated communicators)")
     return ap.parse_args(argv)
 
 
@@ -80,7 +83,8 @@ def main(argv=None, comm=None):
     model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl,
                                         comm=comm).to(dev, dt)
     if a.optim == "xdot":
-        opt = xdot.FusedAdamW(model.parameters(), lr=1e-4)  # one multi-tensor HIP launch per step
+        # one multi-tensor HIP launch per step (device-side step count when graph-captured)
+        opt = xdot.FusedAdamW(model.parameters(), lr=1e-4, capturable=a.graph)
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
     sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
@@ -108,8 +112,23 @@ def main(argv=None, comm=None):
             opt.step()
         return loss
 
-    for _ in range(a.warmup):
-        step()
+    if a.graph:
+        from xdot.utils.graphs import GraphedStep
+
+        def body():
+            out = model(x, x, x, mask)
+            loss = crit(out, y)
+            loss.backward()
+            sync.wait()
+            if not a.no_optim:
+                opt.step()
+            return loss
+
+        step = GraphedStep(body, zero_grad=opt.zero_grad, warmup=max(1, a.warmup))
+        step()  # warmup steps + capture + one replay
+    else:
+        for _ in range(a.warmup):
+            step()
     impl = model._pick_impl(x)
 
     def sync_all():
@@ -162,7 +181,8 @@ def main(argv=None, comm=None):
             "data": "synthetic (random inputs, random-init weights)",
             "config": {"model": f"DistributedDotProductAttn(d={a.dim},h={a.heads})", "global_batch": a.batch,
                        "seq_len": T, "parallelism": f"sp{n}", "impl": impl, "mask": a.mask,
-                       "step": "fwd+bwd+grad-allreduce+AdamW" if not a.no_optim else "fwd+bwd+grad-allreduce"},
+                       "step": "fwd+bwd+grad-allreduce+AdamW" if not a.no_optim else "fwd+bwd+grad-allreduce",
+                       "launch": "hip-graph" if a.graph else "eager"},
             "tokens_per_s": round(a.batch * T / (ms / 1e3), 1),
             "host_enqueue_ms_per_step": round((th - t0) * 1e3 / max(1, a.steps), 4),
             "loss": lossv,

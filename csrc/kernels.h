@@ -99,6 +99,8 @@ struct AdamArgs {
   int blk0[ADAM_MAX_T + 1];  // first block of each tensor (prefix sum)
   int nt;
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
+  const float* step_dev;  // non-null: the step count lives on the device (graph-capturable
+                          // optimizer); bc1 / bc2_sqrt are then computed from it in the kernel
 };
 }  // namespace xdot
 

@@ -24,7 +24,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   const TP* g = reinterpret_cast<const TP*>(a.g[t]);
   float* m = a.m[t];
   float* v = a.v[t];
-  const float step_size = a.lr / a.bc1, decay = 1.f - a.lr * a.wd;
+  float bc1 = a.bc1, bc2_sqrt = a.bc2_sqrt;
+  if (a.step_dev) {  // captured in a HIP graph: the step advances on the device between replays
+    const float t = *a.step_dev;
+    bc1 = 1.f - __builtin_powf(a.beta1, t);
+    bc2_sqrt = __builtin_sqrtf(1.f - __builtin_powf(a.beta2, t));
+  }
+  const float step_size = a.lr / bc1, decay = 1.f - a.lr * a.wd;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t i = base + e;
@@ -35,7 +41,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     m[i] = mi;
     v[i] = vi;
     const float pi = (float)p[i] * decay;
-    p[i] = (TP)(pi - step_size * mi / (__builtin_sqrtf(vi) / a.bc2_sqrt + a.eps));
+    p[i] = (TP)(pi - step_size * mi / (__builtin_sqrtf(vi) / bc2_sqrt + a.eps));
   }
 }
 

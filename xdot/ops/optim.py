@@ -7,6 +7,12 @@ every group in one multi-tensor kernel per (group, dtype).  Semantics follow
 ``torch.optim.AdamW`` (decoupled weight decay, bias correction, ``amsgrad=False``); CPU
 parameters and anything the kernel does not take fall back to ``torch.optim.AdamW``'s
 functional update.
+
+``capturable=True`` keeps the step count on the device (one fp32 scalar per parameter group
+and dtype, advanced by a device op before each update, the bias corrections computed in the
+kernel from it), so ``step()`` can be recorded in a HIP graph and replayed
+(:class:`xdot.utils.graphs.GraphedStep`); every parameter of the group must then have a
+gradient at every step.
 """
 from __future__ import annotations
 
@@ -21,10 +27,12 @@ __all__ = ["FusedAdamW"]
 
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2):
+                 weight_decay: float = 1e-2, capturable: bool = False):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
             raise ValueError("invalid AdamW hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.capturable = capturable
+        self._dev_step = {}  # (group index, dtype, device) -> fp32 device step count
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -32,7 +40,7 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             buckets = {}
             for p in group["params"]:
@@ -47,13 +55,23 @@ class FusedAdamW(torch.optim.Optimizer):
                 hip = (p.is_cuda and p.dtype in (torch.bfloat16, torch.float16, torch.float32) and p.is_contiguous()
                        and _ext.use_hip(p))
                 if hip:
-                    buckets.setdefault((p.dtype, p.device, st["step"]), []).append(p)
+                    buckets.setdefault((p.dtype, p.device, 0 if self.capturable else st["step"]), []).append(p)
+                elif self.capturable:
+                    raise RuntimeError("FusedAdamW(capturable=True) needs contiguous bf16/fp16/fp32 GPU parameters")
                 else:
                     self._torch_update(p, st, group, b1, b2)
-            for (_, _, step), ps in buckets.items():
+            for (dt, dev, step), ps in buckets.items():
+                step_t = None
+                if self.capturable:
+                    key = (gi, dt, dev)
+                    step_t = self._dev_step.get(key)
+                    if step_t is None:
+                        step_t = self._dev_step[key] = torch.zeros((), dtype=torch.float32, device=dev)
+                    step_t.add_(1.0)  # a device op: advances on every graph replay too
+                    step = 1
                 _ext.ops().adamw_step(ps, [p.grad.contiguous() for p in ps], [self.state[p]["exp_avg"] for p in ps],
                                       [self.state[p]["exp_avg_sq"] for p in ps], float(group["lr"]), float(b1),
-                                      float(b2), float(group["eps"]), float(group["weight_decay"]), int(step))
+                                      float(b2), float(group["eps"]), float(group["weight_decay"]), int(step), step_t)
         return loss
 
     @staticmethod
