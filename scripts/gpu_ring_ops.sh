@@ -5,7 +5,7 @@
 set -o pipefail
 O=gpurun_out/${1:-ring_ops}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py -q -m gpu --timeout 300 --timeout-method thread -x > $O/tests.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gemm2_gpu.py tests/test_ops_gpu.py -q -m gpu --timeout 300 --timeout-method thread -x > $O/tests.log 2>&1 || exit $?
 echo tests-ok
 for m in nt all tn; do
   for s in gather ring; do
