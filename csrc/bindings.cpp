@@ -109,10 +109,12 @@ bool gemm_library(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64
     if (sAseg != (a_mc ? K * lda : K) || sBseg != (b_mc ? K * ldb : K)) return false;
     K *= nseg;
   }
-  // conservative layouts only: every batch its own dense-strided matrix (no broadcast operand,
-  // no batches interleaved inside one output row -- the per-rank column blocks of nt's (P, R, T)
-  // output stay on the xdot kernels), 16-byte aligned bases, leading dims and batch strides
-  if (nb > 1 && (sa < (a_mc ? K * lda : M * lda) || sb < (b_mc ? K * ldb : N * ldb) || sc < M * ldc)) return false;
+  // conservative output layouts only: every output batch its own dense matrix (no batches
+  // interleaved inside one output row -- the per-rank column blocks of nt's (P, R, T) output,
+  // which faulted on this route, stay on the xdot kernels); input batches may interleave or be
+  // broadcast (tn's column blocks of `left` against one `right`: verified against torch in
+  // tests/test_gemm2_gpu.py); 16-byte aligned bases, leading dims and batch strides
+  if (nb > 1 && (sa < 0 || sb < 0 || sc < M * ldc)) return false;
   const int64_t ev = 16 / (int64_t)A.element_size();
   auto al = [&](int64_t v) { return v % ev == 0; };
   if (ldc != N) return false;  // whole output rows (no column-slice views)
