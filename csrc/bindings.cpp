@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
 namespace {
 
@@ -748,6 +749,94 @@ at::Tensor flash_bwd_rows_sum(const at::Tensor& dpart, int64_t H, const at::Tens
   return out;
 }
 
+
+// ---- native xGMI pull collectives (csrc/ipc.hip; driven by xdot/utils/ipc.py) ----
+void ipc_ok(int rc, const char* what) { TORCH_CHECK(rc == 0, "xdot.", what, ": HIP error ", rc); }
+
+std::vector<int64_t> ipc_info() {
+  return {xdot_ipc_sig_bytes(), xdot_ipc_max_ranks(), xdot_ipc_max_wgs(), xdot_ipc_handle_bytes(),
+          xdot_ipc_wall_clock_khz()};
+}
+int64_t ipc_alloc(int64_t nbytes, bool uncached) {
+  TORCH_CHECK(nbytes > 0, "xdot.ipc_alloc: size");
+  void* p = nullptr;
+  ipc_ok(xdot_ipc_alloc(nbytes, uncached ? 1 : 0, &p), "ipc_alloc");
+  return (int64_t)(uintptr_t)p;
+}
+void ipc_free(int64_t p) { ipc_ok(xdot_ipc_free((void*)(uintptr_t)p), "ipc_free"); }
+at::Tensor ipc_get_handle(int64_t p) {
+  auto h = at::empty({xdot_ipc_handle_bytes()}, at::TensorOptions().dtype(at::kByte));
+  ipc_ok(xdot_ipc_get_handle((void*)(uintptr_t)p, h.data_ptr()), "ipc_get_handle");
+  return h;
+}
+int64_t ipc_open(const at::Tensor& h) {
+  TORCH_CHECK(!h.is_cuda() && h.scalar_type() == at::kByte && h.is_contiguous() && h.numel() == xdot_ipc_handle_bytes(),
+              "xdot.ipc_open: a CPU uint8 handle tensor");
+  void* p = nullptr;
+  ipc_ok(xdot_ipc_open(h.data_ptr(), &p), "ipc_open");
+  return (int64_t)(uintptr_t)p;
+}
+void ipc_close(int64_t p) { ipc_ok(xdot_ipc_close((void*)(uintptr_t)p), "ipc_close"); }
+std::vector<int64_t> ipc_host_word() {
+  void *host = nullptr, *dev = nullptr;
+  ipc_ok(xdot_ipc_host_word(&host, &dev), "ipc_host_word");
+  return {(int64_t)(uintptr_t)host, (int64_t)(uintptr_t)dev};
+}
+int64_t ipc_read_word(int64_t host) { return (int64_t)*reinterpret_cast<volatile uint32_t*>((uintptr_t)host); }
+void ipc_write_word(int64_t host, int64_t v) { *reinterpret_cast<volatile uint32_t*>((uintptr_t)host) = (uint32_t)v; }
+
+xdot::ipc::Args ipc_args(const at::Tensor& inp, at::Tensor& out, at::IntArrayRef stage, at::IntArrayRef sig,
+                         int64_t status, int64_t rank, int64_t epoch, int64_t ticks, int64_t nwg, const char* what) {
+  const int64_t n = (int64_t)stage.size();
+  TORCH_CHECK(n >= 2 && n <= xdot::ipc::MAXR && (int64_t)sig.size() == n && rank >= 0 && rank < n, "xdot.", what,
+              ": ranks");
+  TORCH_CHECK(nwg >= 1 && nwg <= xdot::ipc::MAXG && epoch >= 1 && status != 0, "xdot.", what, ": config");
+  TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.is_contiguous() && out.is_contiguous() &&
+              inp.device() == out.device() && inp.element_size() >= 2 &&
+              (uintptr_t)inp.data_ptr() % 2 == 0 && (uintptr_t)out.data_ptr() % 2 == 0,
+              "xdot.", what, ": contiguous 16/32-bit device tensors");
+  xdot::ipc::Args a{};
+  a.src = static_cast<const char*>(inp.data_ptr());
+  a.out = static_cast<char*>(out.data_ptr());
+  for (int64_t p = 0; p < n; ++p) {
+    TORCH_CHECK(stage[p] != 0 && sig[p] != 0 && stage[p] % 16 == 0, "xdot.", what, ": peer pointers");
+    a.stage[p] = reinterpret_cast<char*>((uintptr_t)stage[p]);
+    a.sig[p] = reinterpret_cast<uint32_t*>((uintptr_t)sig[p]);
+  }
+  a.status = reinterpret_cast<uint32_t*>((uintptr_t)status);
+  a.timeout_ticks = ticks;
+  a.rank = (int)rank; a.n = (int)n; a.epoch = (int)epoch; a.nwg = (int)nwg;
+  return a;
+}
+
+// out (N * inp bytes, rank-major) <- every rank's inp, pulled over xGMI from the peers' staging slots
+void ipc_all_gather(const at::Tensor& inp, at::Tensor& out, at::IntArrayRef stage, at::IntArrayRef sig, int64_t status,
+                    int64_t rank, int64_t epoch, int64_t ticks, int64_t nwg) {
+  Range rr_("xdot.ipc_all_gather");
+  auto a = ipc_args(inp, out, stage, sig, status, rank, epoch, ticks, nwg, "ipc_all_gather");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(out.numel() * out.element_size() == bytes * a.n && bytes % 16 == 0, "xdot.ipc_all_gather: sizes");
+  a.shard = bytes;
+  c10::DeviceGuard guard(inp.device());
+  TORCH_CHECK(xdot_ipc_all_gather_launch(&a, cur_stream(inp)) == 0, "xdot.ipc_all_gather: config");
+  check_launch(hipGetLastError(), "ipc_all_gather");
+}
+
+// out <- Σ over ranks (rank order, fp32) of block `rank` of the rank-major inp
+void ipc_reduce_scatter(const at::Tensor& inp, at::Tensor& out, at::IntArrayRef stage, at::IntArrayRef sig,
+                        int64_t status, int64_t rank, int64_t epoch, int64_t ticks, int64_t nwg) {
+  Range rr_("xdot.ipc_reduce_scatter");
+  auto a = ipc_args(inp, out, stage, sig, status, rank, epoch, ticks, nwg, "ipc_reduce_scatter");
+  TORCH_CHECK(inp.scalar_type() == out.scalar_type(), "xdot.ipc_reduce_scatter: dtype");
+  const int64_t bytes = out.numel() * out.element_size();
+  TORCH_CHECK(inp.numel() == out.numel() * a.n && bytes % 16 == 0, "xdot.ipc_reduce_scatter: sizes");
+  a.shard = bytes;
+  a.dt = dt_code(inp.scalar_type());
+  c10::DeviceGuard guard(inp.device());
+  TORCH_CHECK(xdot_ipc_reduce_scatter_launch(&a, cur_stream(inp)) == 0, "xdot.ipc_reduce_scatter: config");
+  check_launch(hipGetLastError(), "ipc_reduce_scatter");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(xdot, m) {
@@ -777,10 +866,32 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
+  m.def("ipc_info() -> int[]");
+  m.def("ipc_alloc(int nbytes, bool uncached) -> int");
+  m.def("ipc_free(int ptr) -> ()");
+  m.def("ipc_get_handle(int ptr) -> Tensor");
+  m.def("ipc_open(Tensor handle) -> int");
+  m.def("ipc_close(int ptr) -> ()");
+  m.def("ipc_host_word() -> int[]");
+  m.def("ipc_read_word(int host) -> int");
+  m.def("ipc_write_word(int host, int v) -> ()");
+  m.def("ipc_all_gather(Tensor inp, Tensor(a!) out, int[] stage, int[] sig, int status, int rank, int epoch, "
+        "int ticks, int nwg) -> ()");
+  m.def("ipc_reduce_scatter(Tensor inp, Tensor(a!) out, int[] stage, int[] sig, int status, int rank, int epoch, "
+        "int ticks, int nwg) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
   m.impl("flash_splits", &flash_splits);
+  m.impl("ipc_info", &ipc_info);
+  m.impl("ipc_alloc", &ipc_alloc);
+  m.impl("ipc_free", &ipc_free);
+  m.impl("ipc_get_handle", &ipc_get_handle);
+  m.impl("ipc_open", &ipc_open);
+  m.impl("ipc_close", &ipc_close);
+  m.impl("ipc_host_word", &ipc_host_word);
+  m.impl("ipc_read_word", &ipc_read_word);
+  m.impl("ipc_write_word", &ipc_write_word);
 }
 
 TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
@@ -802,4 +913,6 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_fwd_merge", &flash_fwd_merge);
   m.impl("sum_partials_into", &sum_partials_into);
   m.impl("adamw_step", &adamw_step);
+  m.impl("ipc_all_gather", &ipc_all_gather);
+  m.impl("ipc_reduce_scatter", &ipc_reduce_scatter);
 }

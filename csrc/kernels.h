@@ -102,6 +102,23 @@ struct AdamArgs {
   const float* step_dev;  // non-null: the step count lives on the device (graph-capturable
                           // optimizer); bc1 / bc2_sqrt are then computed from it in the kernel
 };
+namespace ipc {
+constexpr int MAXR = 8;     // ranks of one node
+constexpr int MAXG = 256;   // workgroups (byte ranges) per collective
+constexpr int SIG_WORDS = 2 * MAXR * MAXG;  // arrive[MAXR][MAXG], done[MAXR][MAXG]
+
+// one xGMI pull collective (csrc/ipc.hip)
+struct Args {
+  const char* src;           // local input
+  char* out;                 // local output
+  char* stage[MAXR];         // staging slot of every rank (own: local pointer)
+  uint32_t* sig[MAXR];       // signal page of every rank (own: local pointer)
+  uint32_t* status;          // host-mapped error word
+  int64_t shard;             // bytes per rank block (multiple of 16)
+  int64_t timeout_ticks;     // wall-clock ticks per wait
+  int rank, n, epoch, nwg, dt;
+};
+}  // namespace ipc
 }  // namespace xdot
 
 extern "C" {
@@ -144,4 +161,18 @@ int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, 
 int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+// native xGMI pull collectives (csrc/ipc.hip)
+int xdot_ipc_sig_bytes();
+int xdot_ipc_max_ranks();
+int xdot_ipc_max_wgs();
+int xdot_ipc_alloc(int64_t bytes, int uncached, void** p);
+int xdot_ipc_free(void* p);
+int xdot_ipc_handle_bytes();
+int xdot_ipc_get_handle(void* p, void* out);
+int xdot_ipc_open(const void* handle, void** p);
+int xdot_ipc_close(void* p);
+int xdot_ipc_host_word(void** host, void** dev);
+int xdot_ipc_wall_clock_khz();
+int xdot_ipc_all_gather_launch(const xdot::ipc::Args* a, hipStream_t st);
+int xdot_ipc_reduce_scatter_launch(const xdot::ipc::Args* a, hipStream_t st);
 }

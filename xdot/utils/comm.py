@@ -617,6 +617,14 @@ def init(backend: str = "auto", timeout_s: Optional[float] = None, set_device: b
         kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group(be, **kw)
     _DEFAULT = TorchDistComm()
+    if (_DEFAULT.world_size > 1 and torch.cuda.is_available()
+            and os.environ.get("XDOT_IPC", "0").strip().lower() not in ("", "0", "false", "no", "off")):
+        # stage 2: xGMI pull all-gather / reduce-scatter (csrc/ipc.hip).  Over gloo too: several
+        # ranks sharing one GPU rehearse the device-side collectives (RCCL refuses that layout)
+        from .ipc import IpcComm
+        if be == "gloo":
+            torch.cuda.set_device(get_local_rank() % max(1, torch.cuda.device_count()) if set_device else 0)
+        _DEFAULT = IpcComm(_DEFAULT)
     return _DEFAULT
 
 
@@ -626,7 +634,9 @@ def is_initialized() -> bool:
 
 def destroy() -> None:
     global _DEFAULT
-    if isinstance(_DEFAULT, TorchDistComm) and dist.is_initialized():
+    if hasattr(_DEFAULT, "close"):
+        _DEFAULT.close()
+    if isinstance(getattr(_DEFAULT, "base", _DEFAULT), TorchDistComm) and dist.is_initialized():
         dist.destroy_process_group()
     _DEFAULT = None
 

@@ -49,6 +49,12 @@
                                rank to rank over point-to-point send/recv instead of all-gather /
                                reduce-scatter (default ``gather``: faster over xGMI's full mesh;
                                the ring holds two shards instead of the gathered side)
+``XDOT_IPC``                   ``1``: with RCCL and several ranks, all-gathers and reduce-scatters
+                               run as native xGMI pull kernels over HIP IPC
+                               (``xdot/utils/ipc.py``, ``csrc/ipc.hip``; default 0 = RCCL).
+                               ``XDOT_IPC_MB`` staging MiB per slot (512), ``XDOT_IPC_TIMEOUT_S``
+                               bound of every device-side wait (30),
+                               ``XDOT_IPC_WGS`` workgroups (byte ranges) per collective (128)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """

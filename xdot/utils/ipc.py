@@ -1,0 +1,182 @@
+"""Native xGMI pull collectives over HIP IPC (SURVEY §5.8 stage 2, ``csrc/ipc.hip``).
+
+:class:`IpcComm` wraps a ``torch.distributed`` communicator (one process per GPU of a node)
+and replaces its two bulk data movers — the ones the attention and the distributed products
+spend their bytes in (reference: ``multiplication/functions.py:89-97`` gather loop and the
+N all-reduces at ``:143-147``, ``:202-210``) — with one kernel each that reads the peers'
+memory directly over the point-to-point xGMI links:
+
+* ``all_gather_into``: every rank stages its shard in an IPC-exported buffer; every rank pulls
+  the N-1 peer shards concurrently (its workgroups start at different peers, so all 7 links of
+  an MI355X carry traffic at once instead of one ring hop per step);
+* ``reduce_scatter``: every rank pulls its own block from each peer and sums the N blocks in
+  fp32 in rank order 0..N-1 — deterministic and rounded once to the output dtype (RCCL's ring
+  rounds bf16 partials after every hop: ``tests/test_bf16_reduce.py``).
+
+Everything else (all-reduce, broadcast, p2p, object gathers, barriers) and every call the pull
+kernels do not cover (1-byte dtypes, blocks that are not a multiple of 16 bytes, messages
+beyond the staging capacity, CPU tensors) goes to the wrapped communicator.  Those decisions
+depend only on shapes and dtypes, so every rank takes the same route.
+
+Synchronisation is device-side (per (peer, byte-range) epoch flags in uncached signal pages);
+the host never blocks.  Every device wait is bounded (``XDOT_IPC_TIMEOUT_S``, default 30 s):
+a rank that stops participating makes its peers' kernels drain, set a host-mapped error word,
+and the next collective on the host raises instead of hanging the GPU.
+
+Enable with ``XDOT_IPC=1`` (``xdot.utils.comm.init`` wraps its RCCL communicator) or build one
+explicitly: ``IpcComm(comm)``.  The staging buffers hold ``XDOT_IPC_MB`` MiB per slot (two
+slots per rank, default 512 MiB: the bf16 ``[q|v]`` shard of a T=200000 rank at N=8 is 77 MB).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from .. import _ext
+from .comm import Communicator, Handle, _check_gather
+
+__all__ = ["IpcComm", "ipc_available"]
+
+
+def ipc_available() -> bool:
+    return torch.cuda.is_available() and _ext.load() and hasattr(torch.ops.xdot, "ipc_all_gather")
+
+
+class IpcError(RuntimeError):
+    pass
+
+
+class IpcComm(Communicator):
+    """Pull-based all-gather / reduce-scatter over IPC-mapped peer memory; the rest delegates
+    to ``base`` (which also exchanges the IPC handles)."""
+
+    def __init__(self, base: Communicator, capacity_mb: Optional[float] = None,
+                 timeout_s: Optional[float] = None, nwg: Optional[int] = None, device=None):
+        if not ipc_available():
+            raise IpcError("IpcComm needs a GPU and the xdot extension")
+        ops = torch.ops.xdot
+        sig_bytes, max_ranks, max_wgs, _hb, khz = ops.ipc_info()
+        self.base = base
+        self.world_size, self.rank = base.world_size, base.rank
+        if not 2 <= self.world_size <= max_ranks:
+            raise IpcError(f"IpcComm: world size {self.world_size} outside 2..{max_ranks} (one node)")
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        cap = float(capacity_mb if capacity_mb is not None else os.environ.get("XDOT_IPC_MB", "512"))
+        self.capacity = (int(cap * 2**20) + 255) // 256 * 256
+        t = float(timeout_s if timeout_s is not None else os.environ.get("XDOT_IPC_TIMEOUT_S", "30"))
+        self.ticks = int(t * khz * 1000) if khz > 0 else int(t * 1e8)
+        self.max_wgs = int(max_wgs)
+        w = int(nwg if nwg is not None else os.environ.get("XDOT_IPC_WGS", "128"))
+        self.nwg = max(1, min(self.max_wgs, w))  # byte ranges = workgroups per collective
+        self.epoch = 0
+        with torch.cuda.device(self.device):
+            self._stage = ops.ipc_alloc(2 * self.capacity, False)
+            self._sig = ops.ipc_alloc(int(sig_bytes), True)
+            self._host, self._status = ops.ipc_host_word()
+            mine = (ops.ipc_get_handle(self._stage).tolist(), ops.ipc_get_handle(self._sig).tolist(),
+                    os.getpid())
+            allh = base.all_gather_object(mine)
+            self._opened: List[int] = []
+            self.stage_ptrs, self.sig_ptrs = [], []
+            for p, (hs, hg, _pid) in enumerate(allh):
+                if p == self.rank:
+                    self.stage_ptrs.append(self._stage)
+                    self.sig_ptrs.append(self._sig)
+                    continue
+                s = ops.ipc_open(torch.tensor(hs, dtype=torch.uint8))
+                g = ops.ipc_open(torch.tensor(hg, dtype=torch.uint8))
+                self._opened += [s, g]
+                self.stage_ptrs.append(s)
+                self.sig_ptrs.append(g)
+        base.barrier()  # every rank mapped every page before the first pull
+
+    @property
+    def backend(self) -> str:
+        return f"ipc+{self.base.backend}"
+
+    # -- routing ------------------------------------------------------------------------
+    def _pullable(self, *ts: torch.Tensor, stage_bytes: int) -> bool:
+        return (all(t.is_cuda for t in ts) and all(t.element_size() >= 2 for t in ts)
+                and 0 < stage_bytes <= self.capacity)
+
+    def _wgs(self, shard_bytes: int) -> int:
+        # ONE partition for every collective of this communicator: the (peer, range) flags of
+        # epoch e are checked against those of e - 2, so the range count must never change
+        return self.nwg
+
+    def check(self) -> None:
+        """Raise if a device-side wait of an earlier collective timed out (a peer stopped)."""
+        if torch.ops.xdot.ipc_read_word(self._host):
+            raise IpcError(f"rank {self.rank}: an xGMI pull collective timed out waiting for a peer "
+                           f"(XDOT_IPC_TIMEOUT_S); its output is invalid")
+
+    def _next(self):
+        self.check()
+        self.epoch += 1
+        off = (self.epoch & 1) * self.capacity
+        return [p + off for p in self.stage_ptrs]
+
+    # -- pull collectives ---------------------------------------------------------------
+    def all_gather_into(self, out, inp, async_op=False):
+        _check_gather(out, inp, self.world_size)
+        nb = inp.numel() * inp.element_size()
+        if not (self._pullable(out, inp, stage_bytes=nb) and nb % 16 == 0):
+            return self.base.all_gather_into(out, inp, async_op)
+        o = out if out.is_contiguous() else torch.empty_like(out, memory_format=torch.contiguous_format)
+        i = inp.contiguous()
+        stage = self._next()
+        torch.ops.xdot.ipc_all_gather(i, o.view(-1), stage, self.sig_ptrs, self._status, self.rank, self.epoch,
+                                      self.ticks, self._wgs(nb))
+        if o is not out:
+            out.copy_(o)
+        return Handle(out=out) if async_op else None
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        if inp.numel() != out.numel() * self.world_size:
+            raise ValueError("reduce_scatter: size mismatch")
+        nb = out.numel() * out.element_size()
+        ok = (inp.dtype == out.dtype and inp.dtype in (torch.float32, torch.bfloat16, torch.float16)
+              and nb % 16 == 0 and self._pullable(out, inp, stage_bytes=nb * self.world_size))
+        if not ok:
+            return self.base.reduce_scatter(out, inp, async_op)
+        o = out if out.is_contiguous() else torch.empty_like(out, memory_format=torch.contiguous_format)
+        i = inp.contiguous()
+        stage = self._next()
+        torch.ops.xdot.ipc_reduce_scatter(i, o.view(-1), stage, self.sig_ptrs, self._status, self.rank, self.epoch,
+                                          self.ticks, self._wgs(nb))
+        if o is not out:
+            out.copy_(o)
+        return Handle(out=out) if async_op else None
+
+    # -- delegated ----------------------------------------------------------------------
+    def all_reduce(self, t, op="sum", async_op=False):
+        return self.base.all_reduce(t, op, async_op)
+
+    def broadcast(self, t, src=0, async_op=False):
+        return self.base.broadcast(t, src, async_op)
+
+    def all_gather_object(self, obj):
+        return self.base.all_gather_object(obj)
+
+    def barrier(self):
+        self.base.barrier()
+
+    def sendrecv(self, send, recv, dst, src, async_op=False):
+        return self.base.sendrecv(send, recv, dst, src, async_op)
+
+    def close(self) -> None:
+        """Unmap the peers' pages and free this rank's (after a device sync and a barrier, so
+        no peer is still reading them)."""
+        if getattr(self, "_stage", None) is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self.base.barrier()
+        ops = torch.ops.xdot
+        for p in self._opened:
+            ops.ipc_close(p)
+        ops.ipc_free(self._stage)
+        ops.ipc_free(self._sig)
+        self._stage = self._sig = None
+        self._opened = []
