@@ -15,6 +15,7 @@ in the caller's ``nn.Linear`` modules (``state_dict`` compatible with the refere
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch
@@ -86,10 +87,23 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
-        if ctx.needs_input_grad[1]:
-            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy2.float().sum(0).to(dy.dtype)
+        side = getattr(dy, "_xdot_ready_on", None)  # dy is complete on this stream (see below)
+        cur = torch.cuda.current_stream(dy.device) if side is not None else None
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            if ctx.needs_input_grad[1]:
+                dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                db = dy2.float().sum(0).to(dy.dtype)
+        if side is not None:
+            # the fused attention backward produced dy on its priority stream while its row-side
+            # kernel still runs on `cur`: the weight / bias gradients run there too, overlapping
+            # that kernel, and `cur` is ordered after them before they are handed on
+            x.record_stream(side)
+            dy.record_stream(side)
+            for t in (dw, db):
+                if t is not None:
+                    t.record_stream(cur)
+            cur.wait_stream(side)
         return dx, dw, db
 
 

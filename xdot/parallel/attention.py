@@ -472,13 +472,22 @@ class SeqParallelAttention(torch.autograd.Function):
                     ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
                                                flags, int(H), float(scale), dpart, c * ns, ns, ctx.prescaled)
                 dk = ops.flash_bwd_rows_sum(dpart, int(H), k)
+            with torch.cuda.stream(hi):  # the gathered-side grads complete on the priority stream
+                for h in handles:
+                    if h is not None:
+                        h.wait()
+                handles = []
+                if dqv is None:
+                    dqv = outs[0] if len(outs) == 1 else torch.cat(outs, dim=1)
             cur.wait_stream(hi)
             for oc in outs:
                 oc.record_stream(cur)
-            if dqv is None:
-                dqv = outs[0] if len(outs) == 1 else torch.cat(outs, dim=1)
-            else:
-                dqv.record_stream(cur)
+            dqv.record_stream(cur)
+            # consumers that can run on the priority stream (the packed [q|v] projection's
+            # weight gradient, xdot.ops.linear.LinearFn) start there as soon as the
+            # reduce-scatter lands, under the row-side kernel still running on `cur`
+            if FLAGS.wgrad_side and dqv.dtype == k.dtype:
+                dqv._xdot_ready_on = hi
         else:
             qvg = bufs[0]
             dk, dq_parts, dv_parts = _ref_bwd(do, k, qvg[..., :C], qvg[..., C:], o, lse, ctx.mask, H, scale)

@@ -55,6 +55,10 @@
                                ``XDOT_IPC_MB`` staging MiB per slot (512), ``XDOT_IPC_TIMEOUT_S``
                                bound of every device-side wait (30),
                                ``XDOT_IPC_WGS`` workgroups (byte ranges) per collective (128)
+``XDOT_WGRAD_SIDE``            ``0``: the packed [q|v] projection's weight gradient runs on the
+                               main stream after the attention backward (default 1: on the
+                               backward's priority stream as soon as the gathered-side gradient
+                               lands, overlapping the row-side kernel)
 ``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
 =============================  ==========================================================
 """
@@ -84,6 +88,7 @@ class _Flags:
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
         self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
         self.mask_async = _flag("XDOT_MASK_ASYNC")
+        self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
