@@ -35,11 +35,19 @@
 #ifndef XDOT_FWD_IGLP
 #define XDOT_FWD_IGLP -1  // blocks A / B: iglp_opt hint (-1: none)
 #endif
+#ifndef XDOT_FWD_MASKLESS
+#define XDOT_FWD_MASKLESS 0  // 1: a mask-less instantiation issues no placeholder DMAs per tile
+#endif
+#ifndef XDOT_FWD_MSUM
+#define XDOT_FWD_MSUM 0   // 1: row sums of P on the matrix pipe (ones · Pᵀ MFMAs) instead of VALU adds
+#endif
 
 namespace xdot {
 namespace fa {
 
-template <int DT, int D, int WPS = 2, bool PS = false>
+// MK: the launch may carry a packed mask.  MK = false (no mask, XDOT_FWD_MASKLESS) drops the two
+// per-tile mask DMAs instead of issuing placeholders of the same count.
+template <int DT, int D, int WPS = 2, bool PS = false, bool MK = true>
 __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
@@ -87,10 +95,10 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   const uint32_t moff = (uint32_t)(min((wave & 1) * 64 + lane, a.R - 1 - rb * 128) * 8 + (wave >> 1) * 4);
   // two rings over the same 3 stages: Q(t) + mask words(t) and V(t) go to stage (t - kt_beg) % 3,
   // but Q/mask are DMA'd one tile earlier than V (Q(kt+1) is read in iteration kt)
-  constexpr int NQ = ImgDma<D>::IPW + 2, NV = ImgDma<D>::IPW;  // DMAs per wave
+  constexpr int NQ = ImgDma<D>::IPW + (MK ? 2 : 0), NV = ImgDma<D>::IPW;  // DMAs per wave
   const int NKT4 = (NKT + 3) & ~3;
   const int NRB32 = (a.R + 31) / 32;
-  const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
+  const uint8_t* fwg = (MK && a.mflags) ? a.mflags + ((int64_t)b * NRB32 + rb * 4) * NKT4 : nullptr;
   const int fn = min(4, NRB32 - rb * 4);
   // Q and V tiles are issued strictly in order: running byte offsets (no per-tile 64-bit
   // products) and ring stages that are compile-time constants at every call site
@@ -100,13 +108,15 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
     char* st = smem + decltype(stc)::value * CF::STAGE;
     dma.issue(kcb + q_off, ldb, a.T - 1 - kt * 64, st, wave);  // columns past T re-read T-1 (masked)
     q_off += (int64_t)64 * ldb;
-    if (mwg) {
-      glds4(mw_next, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
-      mw_next += a.R;
-      glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
-    } else {  // same DMA count with or without a mask
-      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
-      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+    if constexpr (MK) {
+      if (mwg) {
+        glds4(mw_next, moff, st + CF::OFF_W + (wave >> 1) * 512 + (wave & 1) * 256);
+        mw_next += a.R;
+        glds_flags(fwg, NKT4, fn, kt >> 2, st + CF::OFF_F);
+      } else {  // same DMA count with or without a mask
+        glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+        glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
+      }
     }
   };
   auto issue_v = [&](int kt, auto stc) {
@@ -127,6 +137,13 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) mseed[r] = 0.f;
   float m_seed = 0.f;
+  // MSUM: l accumulates like O, as Σ_t 1 · Pᵀ[t][row] on the matrix pipe (every entry of the
+  // accumulator holds the lane's row sum); the row sums then come from the same bf16 P as O
+  f32x16 lacc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lacc[r] = 0.f;
+  constexpr uint32_t ONE2 = DT == DT_F16 ? 0x3C003C00u : 0x3F803F80u;
+  const u32x4 ones = {ONE2, ONE2, ONE2, ONE2};
   f32x16 o[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i)
@@ -196,6 +213,10 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       for (int i = 0; i < DB; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      if constexpr (XDOT_FWD_MSUM != 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
+      }
       m_run = m_new;
       if constexpr (PS) {
         const float mu = (m_run == NEG_INF) ? 0.f : m_run;
@@ -267,9 +288,14 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
           u32x4 v2 = v1;
           if (i + 2 < NB) v2 = tr_frag<D>(cur + IMG, ((i + 2) & 3) * 16, ((i + 2) >> 2) * 32, L);
           o[db] = mfma32<DT>::run(v0, pf[k4], o[db]);
+          if constexpr (XDOT_FWD_MSUM != 0) {
+            // one row-sum MFMA after every DB-th PV MFMA: its chain stays DB MFMAs apart
+            if ((i + 1) % DB == 0) lacc = mfma32<DT>::run(ones, pf[(i + 1) / DB - 1], lacc);
+          } else {
 #pragma unroll
-          for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
-          asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
+            for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
+            asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
+          }
 
 #if XDOT_FWD_PIN
           __builtin_amdgcn_sched_barrier(0);
@@ -324,7 +350,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   }
 
   // ---- epilogue ----
-  const float l_tot = pair_sum(l_run);
+  const float l_tot = XDOT_FWD_MSUM != 0 ? lacc[0] : pair_sum(l_run);
   const float inv = 1.f / l_tot;
   if (row_ok && a.nsplit == 1 && !a.force_partial) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
@@ -643,6 +669,7 @@ static void launch_fwd(const FwdArgs& a, hipStream_t st) {
     const dim3 grid(nrb * a.B * a.H * a.nsplit);
     if (a.prescaled) {
       if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1, true>), grid, dim3(256), LDS, st, a);
+      else if (XDOT_FWD_MASKLESS && !a.mbits && !a.mflags) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2, true, false>), grid, dim3(256), LDS, st, a);
       else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2, true>), grid, dim3(256), LDS, st, a);
     } else {
       if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);

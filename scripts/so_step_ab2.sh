@@ -1,0 +1,24 @@
+#!/bin/bash
+# A/B of compile-time variants (scripts/build_variant.sh): flash + module GPU tests under each
+# non-base variant, then 3 alternating rounds of {bench_flash KERNEL at N=1 and the N=8 rank
+# shape, bench.py N=1, bench_rank N=8}.  usage: so_step_ab2.sh TAG KERNEL VARIANT...
+set -o pipefail
+TAG=$1; KER=$2; shift 2
+O=gpurun_out/$TAG
+mkdir -p $O
+so() { if [ "$1" == "base" ]; then echo xdot/_C.so; else echo xdot/_C_$1.so; fi; }
+for v in "$@"; do
+  [ "$v" == "base" ] && continue
+  XDOT_EXT_PATH=$(so $v) timeout -k 10 400 python -u -m pytest tests/test_flash_gpu.py tests/test_module_gpu.py -q -m gpu \
+    --timeout 120 --timeout-method thread -x > $O/tests_$v.log 2>&1 || exit $?
+done
+echo tests-ok
+for r in 1 2 3; do
+  for v in "$@"; do
+    XDOT_EXT_PATH=$(so $v) timeout -k 10 120 python benchmarks/bench_flash.py ${FLASH_ARGS---mask} --iters 10 --only $KER >> $O/$v.log 2>&1 || exit $?
+    XDOT_EXT_PATH=$(so $v) timeout -k 10 120 python benchmarks/bench_flash.py ${FLASH_ARGS---mask} --iters 10 --only $KER --R 3125 >> $O/$v.log 2>&1 || exit $?
+    XDOT_EXT_PATH=$(so $v) timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> $O/step_$v.log 2>&1 || exit $?
+    XDOT_EXT_PATH=$(so $v) timeout -k 10 200 python benchmarks/bench_rank.py --world 8 --steps 20 --warmup 5 >> $O/step_$v.log 2>&1 || exit $?
+  done
+done
+echo ab-ok

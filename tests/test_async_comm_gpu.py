@@ -38,3 +38,30 @@ def test_link_model_matches_synchronous_collectives(gpu, impl, chunks):
     got = _step(EmulatedComm(4, rank=1, link_gbps=2.0, p2p_gbps=1.0), impl, chunks, gpu)
     for a, b in zip(ref, got):
         assert torch.equal(a, b)
+
+
+def test_ring_peak_memory_below_flash(gpu):
+    """the ring path must be the memory-lean one.  One rank of an 8-rank job
+    (EmulatedComm), T = 16384: the flash path holds the whole gathered [q|v] side (and its
+    gradient partials) while the ring holds two blocks plus running fp32 accumulators."""
+    import xdot
+    from xdot.utils.comm import EmulatedComm
+
+    def peak(impl):
+        comm = EmulatedComm(8, rank=0)
+        torch.manual_seed(0)
+        m = xdot.DistributedDotProductAttn(768, num_heads=8, impl=impl, comm=comm).to(gpu, torch.bfloat16)
+        x = torch.randn(1, 2048, 768, device=gpu, dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated(gpu)
+        torch.cuda.reset_peak_memory_stats(gpu)
+        out = m(x, x, x, None)
+        out.float().square().mean().backward()
+        torch.cuda.synchronize()
+        return torch.cuda.max_memory_allocated(gpu) - base
+
+    p_flash, p_ring = peak("flash"), peak("ring")
+    gathered = 16384 * 2 * 768 * 2  # bytes of the bf16 [q|v] gathered side
+    assert p_flash > gathered, (p_flash, gathered)
+    assert p_ring < 0.6 * p_flash, (p_ring, p_flash)
