@@ -98,8 +98,10 @@ class IpcComm(Communicator):
 
     # -- routing ------------------------------------------------------------------------
     def _pullable(self, *ts: torch.Tensor, stage_bytes: int) -> bool:
+        # not under HIP-graph capture: the epoch is a host counter baked into the launch, a
+        # replay would reuse it (the wrapped RCCL collectives are capturable)
         return (all(t.is_cuda for t in ts) and all(t.element_size() >= 2 for t in ts)
-                and 0 < stage_bytes <= self.capacity)
+                and 0 < stage_bytes <= self.capacity and not torch.cuda.is_current_stream_capturing())
 
     def _wgs(self, shard_bytes: int) -> int:
         # ONE partition for every collective of this communicator: the (peer, range) flags of
