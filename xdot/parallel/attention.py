@@ -26,6 +26,8 @@ schedule with a torch reference implementation of steps 2-5.
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -322,6 +324,14 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
 _SIDE = {}
 
 
+def _bwd_overlap(B: int, R: int, H: int) -> bool:
+    """Row-side kernel concurrent with the gathered-side kernel (XDOT_BWD_OVERLAP)?"""
+    ov = FLAGS.bwd_overlap
+    if ov != "auto":
+        return ov not in ("0", "false", "off", "no")
+    return -(-R // 128) * B * H >= int(os.environ.get("XDOT_BWD_OVERLAP_TILES", "0") or 0)
+
+
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
     """Per-device high-priority compute stream of the backward (created once)."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -455,7 +465,10 @@ class SeqParallelAttention(torch.autograd.Function):
                                              None if dqv is None else dqv[:, r0:r0 + rc])
                         handles.append(h)
                         outs.append(oc)
-            cur.wait_event(ev)
+            if _bwd_overlap(B, R, H):
+                cur.wait_event(ev)
+            else:  # small rank shapes: back to back (measured: concurrency costs more than it fills)
+                cur.wait_stream(hi)
             delta.record_stream(cur)
             if one:
                 g = bufs[0]

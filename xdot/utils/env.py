@@ -39,6 +39,12 @@
                                two streams when a block has >= 1024 row tiles of 128 x heads
                                (measured, 1x MI355X, T=25000: N=1 9.21 -> 8.71 ms with two
                                streams, emulated N=8 rank 2.46 -> 2.63 ms, i.e. worse)
+``XDOT_BWD_OVERLAP``           fused attention backward: ``1`` runs the row-side kernel concurrently
+                               with the gathered-side kernel (two streams), ``0`` after it (the
+                               reduce-scatter still overlaps it); default ``auto``: concurrent
+                               when the rank has >= XDOT_BWD_OVERLAP_TILES row tiles of 128 x heads
+                               (default 0: always; back to back measured slower at every rank
+                               shape, profiles/r2_bwd_overlap.md)
 ``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
                                row kernel (default 1: VALU of one sub-tile issues between the
                                next sub-tile's MFMAs; 1.5 % faster kernel)
@@ -92,6 +98,7 @@ class _Flags:
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
+        self.bwd_overlap = os.environ.get("XDOT_BWD_OVERLAP", "auto").strip().lower() or "auto"
         self.ops_schedule = os.environ.get("XDOT_OPS_SCHEDULE", "gather").strip().lower() or "gather"
 
 
