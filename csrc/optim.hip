@@ -10,6 +10,12 @@
 // (decoupled weight decay, bias-corrected moments, amsgrad = False).
 #include "common.h"
 
+#include <type_traits>
+
+#ifndef XDOT_ADAM_VEC
+#define XDOT_ADAM_VEC 1  // vector loads / stores for full aligned 4-element groups
+#endif
+
 namespace xdot {
 
 template <int DT>
@@ -31,6 +37,32 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     bc2_sqrt = __builtin_sqrtf(1.f - __builtin_powf(a.beta2, t));
   }
   const float step_size = a.lr / bc1, decay = 1.f - a.lr * a.wd;
+  auto upd = [&](float pi, float gi, float& mi, float& vi) {
+    mi = a.beta1 * mi + (1.f - a.beta1) * gi;
+    vi = a.beta2 * vi + (1.f - a.beta2) * gi * gi;
+    return pi * decay - step_size * mi / (__builtin_sqrtf(vi) / bc2_sqrt + a.eps);
+  };
+  // full, aligned 4-element group: one vector load / store per operand (the tensors start at
+  // allocator-aligned addresses; the check is wave-uniform per tensor)
+  constexpr int PB = 4 * (int)sizeof(TP);
+  if (XDOT_ADAM_VEC && base + 3 < n && ((uintptr_t)p | (uintptr_t)g) % PB == 0 && ((uintptr_t)m | (uintptr_t)v) % 16 == 0) {
+    using PV = typename std::conditional<PB == 16, u32x4, u32x2>::type;
+    union { PV u; TP e[4]; } pp, gg;
+    pp.u = *reinterpret_cast<const PV*>(p + base);
+    gg.u = *reinterpret_cast<const PV*>(g + base);
+    f32x4 mm = *reinterpret_cast<const f32x4*>(m + base), vv = *reinterpret_cast<const f32x4*>(v + base);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mi = mm[e], vi = vv[e];
+      pp.e[e] = (TP)upd((float)pp.e[e], (float)gg.e[e], mi, vi);
+      mm[e] = mi;
+      vv[e] = vi;
+    }
+    *reinterpret_cast<f32x4*>(m + base) = mm;
+    *reinterpret_cast<f32x4*>(v + base) = vv;
+    *reinterpret_cast<PV*>(p + base) = pp.u;
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t i = base + e;

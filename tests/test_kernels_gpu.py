@@ -132,6 +132,10 @@ def test_fused_adamw_kernel(gpu, dtype):
     gr = [torch.randn(*s, generator=g) for s in shapes]
     kw = dict(lr=3e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.05)
     ours = [p.to(gpu, dtype).requires_grad_(True) for p in p32]
+    # the last one starts one element into its storage: the kernel's unaligned (scalar) path
+    buf = torch.zeros(1 + p32[3].numel(), device=gpu, dtype=dtype)
+    buf[1:].copy_(p32[3].flatten().to(gpu, dtype))
+    ours[3] = buf[1:].view(p32[3].shape).detach().requires_grad_(True)
     ref = [p.to(gpu).requires_grad_(True) for p in p32]
     o1, o2 = FusedAdamW(ours, **kw), torch.optim.AdamW(ref, **kw)
     for s in range(3):
