@@ -49,6 +49,8 @@ def parse(argv=None):
                     help="collective backend (auto = RCCL on GPU); gloo lets several ranks share one GPU "
                          "for rehearsals")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    ap.add_argument("--no-split-step", dest="split_step", action="store_false",
+                    help="(A/B) one optimizer step after every all-reduce instead of splitting it around the last one")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd+bwd+grad sync+AdamW) in a HIP graph and replay it "
                          "(xdot.utils.graphs.GraphedStep; single-GPU / emulated communicators)")
@@ -107,8 +109,10 @@ def main(argv=None, comm=None):
         out = model(x, x, x, mask)
         loss = crit(out, y)
         loss.backward()
-        sync.wait()
-        if not a.no_optim:
+        # with several ranks the update of the buckets already reduced runs under the last
+        # gradient all-reduce (GradSync.wait(optimizer=...)); otherwise one step after the wait
+        stepped = sync.wait(optimizer=None if a.no_optim or not a.split_step else opt)
+        if not a.no_optim and not stepped:
             opt.step()
         return loss
 

@@ -35,16 +35,24 @@ class FusedAdamW(torch.optim.Optimizer):
         self._dev_step = {}  # (group index, dtype, device) -> fp32 device step count
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, params=None):
+        """``params``: update only these parameters (each must then be updated once per step —
+        :meth:`xdot.parallel.GradSync.wait` with ``optimizer=`` splits a step this way so the
+        early buckets' update overlaps the last gradient all-reduce).  Not with ``capturable``."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        only = None
+        if params is not None:
+            if self.capturable:
+                raise RuntimeError("FusedAdamW(capturable=True).step(params=...) is not supported")
+            only = {id(p) for p in params}
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             buckets = {}
             for p in group["params"]:
-                if p.grad is None:
+                if p.grad is None or (only is not None and id(p) not in only):
                     continue
                 st = self.state[p]
                 if not st:

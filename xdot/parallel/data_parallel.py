@@ -15,6 +15,7 @@ must be **summed** (not averaged) across ranks.  The reference leaves this to th
 from __future__ import annotations
 
 import contextlib
+import inspect
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -169,8 +170,16 @@ class GradSync:
         self._handles.append((i, flat, h))
 
     @torch.no_grad()
-    def wait(self) -> None:
+    def wait(self, optimizer=None) -> bool:
+        """Order the current stream after every bucket's all-reduce.  With ``optimizer`` (one
+        whose ``step`` takes ``params=``, e.g. :class:`xdot.FusedAdamW`) the update is split: the
+        buckets reduced before the last one are stepped while the last all-reduce (the gradient
+        that arrives last in backward) is still on the wire, then the last bucket.  Returns
+        True when the optimizer has stepped."""
         ws = self.comm.world_size
+        split = (optimizer is not None and ws > 1 and len(self._handles) > 1
+                 and not getattr(optimizer, "capturable", False)
+                 and "params" in inspect.signature(optimizer.step).parameters)
         if ws > 1:
             missing = [i for i, done in enumerate(self._launched) if not done]
             if missing and self.unused == "raise":
@@ -181,7 +190,10 @@ class GradSync:
                                    "freeze it, or pass unused='zero')")
             for i in missing:  # bucket index order: the same on every rank
                 self._launch(i)
-        for i, flat, h in self._handles:
+        last = len(self._handles) - 1
+        for k, (i, flat, h) in enumerate(self._handles):
+            if split and k == last:  # everything reduced so far steps under the last all-reduce
+                optimizer.step(params=[p for j, _, _ in self._handles[:last] for p in self.buckets[j]])
             h.wait()
             if self.op == "avg":
                 flat.div_(ws)
@@ -193,7 +205,10 @@ class GradSync:
                 n = p.numel()
                 p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
+        if split:
+            optimizer.step(params=list(self.buckets[self._handles[last][0]]))
         self._reset()
+        return split
 
     def _reset(self):
         self._handles.clear()
