@@ -92,6 +92,7 @@ def main(argv=None, comm=None):
     sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
     # projection's all-reduce overlaps the attention backward
     crit = xdot.MSELoss()  # fused loss + gradient pass (torch.nn.MSELoss semantics)
+    from xdot.ops.loss import unit_grad
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.rand(a.batch, R, a.dim, device=dev, dtype=dt, generator=g)
@@ -108,7 +109,7 @@ def main(argv=None, comm=None):
         opt.zero_grad(set_to_none=True)
         out = model(x, x, x, mask)
         loss = crit(out, y)
-        loss.backward()
+        loss.backward(unit_grad(loss))  # == loss.backward(), minus the seed fill / scaling pass
         # with several ranks the update of the buckets already reduced runs under the last
         # gradient all-reduce (GradSync.wait(optimizer=...)); otherwise one step after the wait
         stepped = sync.wait(optimizer=None if a.no_optim or not a.split_step else opt)

@@ -47,3 +47,36 @@ def test_mse_gpu_deterministic(gpu):
     a = mse_loss(y, t)
     b = mse_loss(y, t)
     assert torch.equal(a, b)
+
+
+def test_unit_grad_seed_matches_default_backward():
+    """loss.backward(unit_grad(loss)) == loss.backward() (CPU: torch path; the seed is exact 1)."""
+    import xdot
+    from xdot.ops.loss import unit_grad
+
+    g = torch.Generator().manual_seed(3)
+    y0, t = torch.randn(4, 33, generator=g), torch.randn(4, 33, generator=g)
+    a = y0.clone().requires_grad_(True)
+    b = y0.clone().requires_grad_(True)
+    xdot.MSELoss()(a, t).backward()
+    lb = xdot.MSELoss()(b, t)
+    lb.backward(unit_grad(lb))
+    assert torch.equal(a.grad, b.grad)
+    assert unit_grad(lb) is unit_grad(lb)
+
+
+@pytest.mark.gpu
+def test_unit_grad_seed_gpu(gpu):
+    """HIP path: the exact-1 seed hands the kernel's saved gradient on unscaled — bitwise equal
+    to the default backward (dy * 1)."""
+    import xdot
+    from xdot.ops.loss import unit_grad
+
+    y0 = torch.randn(1, 3125, 768, device=gpu, dtype=torch.bfloat16)
+    t = torch.randn(1, 3125, 768, device=gpu, dtype=torch.bfloat16)
+    a = y0.clone().requires_grad_(True)
+    b = y0.clone().requires_grad_(True)
+    xdot.MSELoss()(a, t).backward()
+    lb = xdot.MSELoss()(b, t)
+    lb.backward(unit_grad(lb))
+    assert torch.equal(a.grad, b.grad)

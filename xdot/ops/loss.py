@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from .. import _ext
 
-__all__ = ["mse_loss", "MSELoss"]
+__all__ = ["mse_loss", "MSELoss", "unit_grad"]
 
 _DT = (torch.bfloat16, torch.float16, torch.float32)
 
@@ -40,9 +40,26 @@ class _MSE(torch.autograd.Function):
     @_ext.pinned
     def backward(ctx, g):
         (dy,) = ctx.saved_tensors
-        gy = dy * g.to(dy.dtype)
+        # an exact-1 seed (unit_grad) leaves the saved gradient as it is: no scaling pass
+        gy = dy if getattr(g, "_xdot_unit", False) else dy * g.to(dy.dtype)
         gt = -gy if ctx.needs_input_grad[1] else None
         return (gy if ctx.needs_input_grad[0] else None), gt
+
+
+_UNIT = {}
+
+
+def unit_grad(loss: torch.Tensor) -> torch.Tensor:
+    """A cached exact-1 seed for ``loss.backward(unit_grad(loss))``: the same gradient as
+    ``loss.backward()`` without autograd's per-call fill of a ones tensor, and the fused loss
+    hands its saved gradient on without the scaling pass (two small kernels per step).  The
+    returned tensor is shared: do not modify it."""
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    t = _UNIT.get(key)
+    if t is None:
+        t = _UNIT[key] = torch.ones(loss.shape, dtype=loss.dtype, device=loss.device)
+        t._xdot_unit = True
+    return t
 
 
 def mse_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
