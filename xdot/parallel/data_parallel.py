@@ -15,6 +15,7 @@ must be **summed** (not averaged) across ranks.  The reference leaves this to th
 from __future__ import annotations
 
 import contextlib
+import functools
 import inspect
 from typing import Dict, Iterable, List, Optional
 
@@ -84,6 +85,12 @@ def allreduce_gradients(module_or_params, op: str = "sum", comm: Optional[_comm.
 
     for b in _buckets(grads, int(bucket_mb * 2**20)):
         _flat_apply(b, red)
+
+
+@functools.lru_cache(maxsize=None)
+def _takes_params(opt_cls) -> bool:
+    """Does ``opt_cls.step`` accept ``params=`` (a partial step, e.g. :class:`xdot.FusedAdamW`)?"""
+    return "params" in inspect.signature(opt_cls.step).parameters
 
 
 class GradSync:
@@ -178,8 +185,7 @@ class GradSync:
         True when the optimizer has stepped."""
         ws = self.comm.world_size
         split = (optimizer is not None and ws > 1 and len(self._handles) > 1
-                 and not getattr(optimizer, "capturable", False)
-                 and "params" in inspect.signature(optimizer.step).parameters)
+                 and not getattr(optimizer, "capturable", False) and _takes_params(type(optimizer)))
         if ws > 1:
             missing = [i for i, done in enumerate(self._launched) if not done]
             if missing and self.unused == "raise":
