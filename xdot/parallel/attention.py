@@ -332,12 +332,12 @@ def _bwd_overlap(B: int, R: int, H: int) -> bool:
     return -(-R // 128) * B * H >= int(os.environ.get("XDOT_BWD_OVERLAP_TILES", "0") or 0)
 
 
-def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    """Per-device high-priority compute stream of the backward (created once)."""
+def _side_stream(dev: torch.device, priority: int = -1) -> "torch.cuda.Stream":
+    """Per-device compute stream of the backward (created once per priority; -1 = high)."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
-    if i not in _SIDE:
-        _SIDE[i] = torch.cuda.Stream(device=i, priority=-1)
-    return _SIDE[i]
+    if (i, priority) not in _SIDE:
+        _SIDE[(i, priority)] = torch.cuda.Stream(device=i, priority=priority)
+    return _SIDE[(i, priority)]
 
 
 # ----------------------------------------------------------------------------------------
@@ -431,7 +431,9 @@ class SeqParallelAttention(torch.autograd.Function):
             # the GPU first.  Per-chunk kernels (chunk c's reduce-scatter under chunk c+1's
             # kernel) only when the chunks are separate buffers (B > 1).
             cur = torch.cuda.current_stream(do.device)
-            hi = _side_stream(do.device)
+            # high priority so the gathered side (and its reduce-scatter) finishes early;
+            # XDOT_BWD_SIDE_PRIO=0 makes it an ordinary stream (A/B knob)
+            hi = _side_stream(do.device, int(os.environ.get("XDOT_BWD_SIDE_PRIO", "-1")))
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
