@@ -45,6 +45,11 @@
                                when the rank has >= XDOT_BWD_OVERLAP_TILES row tiles of 128 x heads
                                (default 0: always; back to back measured slower at every rank
                                shape, profiles/r2_bwd_overlap.md)
+``XDOT_BWD_SIDE_PRIO``         priority of the fused backward's gathered-side stream (default -1 =
+                               high; 0 measured slower at N=1 and N=8, profiles/r2_bwd_overlap.md)
+``XDOT_WGRAD_PATH``            weight-gradient GEMM: ``auto`` (the 256x256 split-K kernel) or ``128``
+                               (K slabs of the 128x128 kernel, ``XDOT_WGRAD_SPLITS`` slabs);
+                               profiles/r2_wgrad_route.md
 ``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
                                row kernel (default 1: VALU of one sub-tile issues between the
                                next sub-tile's MFMAs; 1.5 % faster kernel)
