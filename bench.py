@@ -23,7 +23,12 @@ import os
 import sys
 import time
 
-import torch
+# kernel arguments in device memory: lower launch latency for the step's ~26 launches (read by
+# the HIP runtime at its initialisation, i.e. before the first GPU call).  Same-box A/B, 3 rounds:
+# N=1 7.90 -> 7.86 ms, emulated N=8 rank 1.339 -> 1.306 ms (profiles/r2_kernarg.md)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+import torch  # noqa: E402
 
 METRIC = "ms/fwd+bwd DistributedDotProductAttn T=25000 d=768 h=8; scaling 1/2/4/8 GPU"
 
