@@ -430,7 +430,8 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const c10::optional<at::Tensor>& bits,
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
                                                               double scale, const c10::optional<at::Tensor>& delta_in,
-                                                              bool fp32_out, bool prescaled) {
+                                                              bool fp32_out, bool prescaled,
+                                                              const c10::optional<at::Tensor>& lse2_in) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
@@ -450,14 +451,24 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   a.dkc = dkv.data_ptr(); a.dvc = static_cast<char*>(dkv.data_ptr()) + g.C * dkv.element_size(); a.ldg = 2 * g.C;
   a.dkv16 = (fp32_out || rows.scalar_type() == at::kFloat) ? 0 : 1;
   a.delta = delta.data_ptr<float>();
-  auto lse2 = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  // lse2 = lse * log2 e: given (from flash_bwd_prep, together with δ), or one prep pass here
+  const bool have_lse2 = have_delta && lse2_in.has_value() && lse2_in->defined();
+  at::Tensor lse2;
+  if (have_lse2) {
+    lse2 = *lse2_in;
+    TORCH_CHECK(lse2.is_contiguous() && lse2.scalar_type() == at::kFloat && lse2.numel() == g.B * H * g.R &&
+                    lse2.device() == rows.device(), "xdot.flash_bwd_cols: lse2");
+  } else {
+    lse2 = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
+  }
   a.lse2 = lse2.data_ptr<float>();
   c10::DeviceGuard guard(rows.device());
   const int dt = dt_code(rows.scalar_type());
   // prep: lse2 (+ δ unless given)
-  TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), have_delta ? nullptr : delta.data_ptr<float>(), dt,
-                                          (int)g.D, cur_stream(rows)) == 0,
-              "xdot.flash_bwd_cols: config");
+  if (!have_lse2)
+    TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), have_delta ? nullptr : delta.data_ptr<float>(), dt,
+                                            (int)g.D, cur_stream(rows)) == 0,
+                "xdot.flash_bwd_cols: config");
   TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, dt, (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
   check_launch(hipGetLastError(), "flash_bwd_cols");
   return {dkv, delta};
@@ -581,6 +592,32 @@ at::Tensor flash_bwd_delta(const at::Tensor& dout, const at::Tensor& out, int64_
               "xdot.flash_bwd_delta: unsupported dtype/head dim");
   check_launch(hipGetLastError(), "flash_bwd_delta");
   return delta;
+}
+
+// δ = rowsum(dO ⊙ O) and lse2 = lse * log2 e, both fp32 (B, H, R), in ONE pass: the fused
+// backward's prep (flash_bwd_cols then takes both and launches no prep of its own)
+std::tuple<at::Tensor, at::Tensor> flash_bwd_prep(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& lse,
+                                                  int64_t H) {
+  Range rr_("xdot.flash_bwd_prep");
+  TORCH_CHECK(dout.is_cuda() && dout.dim() == 3 && dout.is_contiguous() && out.sizes() == dout.sizes() &&
+                  out.is_contiguous() && out.scalar_type() == dout.scalar_type() && out.device() == dout.device(),
+              "xdot.flash_bwd_prep: dout/out must be matching contiguous (B, R, H*D) device tensors");
+  TORCH_CHECK(H > 0 && dout.size(2) % H == 0, "xdot.flash_bwd_prep: H");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat && lse.device() == dout.device() &&
+                  lse.numel() == dout.size(0) * H * dout.size(1), "xdot.flash_bwd_prep: lse (B, H, R) fp32");
+  xdot::fa::BwdArgs a{};
+  a.dout = dout.data_ptr();
+  a.B = (int)dout.size(0); a.R = (int)dout.size(1); a.H = (int)H;
+  auto delta = at::empty({dout.size(0), H, dout.size(1)}, dout.options().dtype(at::kFloat));
+  auto lse2 = at::empty_like(delta);
+  a.lse = lse.data_ptr<float>();
+  a.lse2 = lse2.data_ptr<float>();
+  c10::DeviceGuard guard(dout.device());
+  TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), delta.data_ptr<float>(), dt_code(dout.scalar_type()),
+                                          (int)(dout.size(2) / H), cur_stream(dout)) == 0,
+              "xdot.flash_bwd_prep: unsupported dtype/head dim");
+  check_launch(hipGetLastError(), "flash_bwd_prep");
+  return {delta, lse2};
 }
 
 // row-side grad (this rank's rows), column-split when the row count is small
@@ -848,7 +885,9 @@ TORCH_LIBRARY(xdot, m) {
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
-        "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False) -> (Tensor, Tensor)");
+        "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False, "
+        "Tensor? lse2=None) -> (Tensor, Tensor)");
+  m.def("flash_bwd_prep(Tensor dout, Tensor out, Tensor lse, int H) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
   m.def("flash_splits(int B, int R, int T, int H, bool rows_kernel) -> int");
@@ -903,6 +942,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_bwd_cols", &flash_bwd_cols);
   m.impl("flash_bwd_rows", &flash_bwd_rows);
   m.impl("flash_bwd_delta", &flash_bwd_delta);
+  m.impl("flash_bwd_prep", &flash_bwd_prep);
   m.impl("sum_partials", &sum_partials);
   m.impl("flash_prescale", &flash_prescale);
   m.impl("mse_fwd", &mse_fwd);

@@ -204,16 +204,23 @@ def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
     return _ext.ops().flash_bwd_delta(dout.contiguous(), out.contiguous(), int(H))
 
 
+def bwd_prep(dout: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, H: int):
+    """(δ, lse2): δ = rowsum(dO ⊙ O) and the log2-domain LSE, fp32 (B, H, R), in one launch."""
+    return _ext.ops().flash_bwd_prep(dout.contiguous(), out.contiguous(), lse.contiguous(), int(H))
+
+
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
-             delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False):
+             delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False,
+             lse2: Optional[torch.Tensor] = None):
     """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
-    ``delta`` (from :func:`bwd_delta`) is computed here when not given.  The grads are fp32
+    ``delta`` (from :func:`bwd_delta`) is computed here when not given; with ``lse2`` too (both
+    from :func:`bwd_prep`) no prep pass is launched here.  The grads are fp32
     (``fp32_out``) or rounded once to the input dtype in the kernel epilogue."""
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
-                                     bool(fp32_out), bool(prescaled))
+                                     bool(fp32_out), bool(prescaled), lse2)
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0,

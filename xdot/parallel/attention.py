@@ -438,7 +438,7 @@ class SeqParallelAttention(torch.autograd.Function):
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
             with torch.cuda.stream(hi):
-                delta = flash.bwd_delta(do, o, H)
+                delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
                 ev = torch.cuda.Event()
                 ev.record(hi)
                 dqv = None
@@ -449,7 +449,7 @@ class SeqParallelAttention(torch.autograd.Function):
                 if one:
                     g = bufs[0]
                     dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
+                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2)
                     off = 0
                     for r0, rc in chunks:  # (chunk, rank, row) order: chunk c's ranks are contiguous
                         part = dkv if len(chunks) == 1 else dkv[:, off:off + n * rc]
@@ -462,7 +462,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     for c, (r0, rc) in enumerate(chunks):
                         g = bufs[c]
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[c], H, scale, delta,
-                                                fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled)
+                                                fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2)
                         h, oc = reduce_async(flash.btc_to_rank_major(dkv, n),
                                              None if dqv is None else dqv[:, r0:r0 + rc])
                         handles.append(h)
