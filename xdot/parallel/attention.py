@@ -82,13 +82,14 @@ def _row_chunks(n: int, R: int, hip: bool, nchunks: Optional[int] = None) -> Lis
     """Row chunks (r0, rc) of every rank's shard for the pipelined gather of the fused path:
     with several ranks the gathered side can travel in ``XDOT_GATHER_CHUNKS`` all-gathers so
     chunk c+1 is in flight while the kernels consume chunk c (and, in backward, chunk c's
-    reduce-scatter runs while chunk c+1's gradients are computed).  Default 1: measured on
-    one MI355X with emulated 8-rank shapes, 2 chunks cost ≈0.23 ms more compute per step
-    (per-chunk mask copies, split partials, half-occupied last workgroup rounds), about what
-    the overlap can save over xGMI."""
+    reduce-scatter runs while chunk c+1's gradients are computed).  Default (auto): 2 chunks
+    from 8 ranks on, else 1 — measured on the emulated rank step with a 300 GB/s collective
+    link model: N=8 1.621 -> 1.577 ms with 2 chunks, N=4 2.459 -> 2.471 ms (without any
+    transfer time 2 chunks cost 23 / 55 µs of compute), profiles/r2_gather_chunks.md."""
     if n == 1:
         return [(0, R)]
-    nc = nchunks or (FLAGS.gather_chunks if hip else 1)
+    auto = 2 if n >= 8 else 1
+    nc = nchunks or ((FLAGS.gather_chunks or auto) if hip else 1)
     nc = max(1, min(nc, R if nchunks else R // 64))  # an explicit plan is honoured down to 1-row chunks
     base, extra = divmod(R, nc)
     out, r0 = [], 0

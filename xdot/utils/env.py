@@ -17,10 +17,9 @@
                                the bf16/fp16 compute dtype in the kernel, half the bytes)
 ``XDOT_ROCTX``                 ``1``: roctx ranges around every native op (rocprofv3 markers)
 ``XDOT_GATHER_CHUNKS``         row chunks of the fused attention's all-gather / reduce-scatter
-                               pipeline with several ranks (default 1 = one collective each; 2
-                               overlaps half the gather with the kernels at +0.32 / +0.23 /
-                               +0.10 ms of compute per step at N = 2 / 4 / 8 (emulated, T=25000),
-                               about what it hides over xGMI: worth it on a slower interconnect)
+                               pipeline with several ranks (default auto: 2 from 8 ranks on, else
+                               1; with a 300 GB/s link model 2 chunks save 44 µs per N=8 rank step
+                               and lose 12 µs at N=4, profiles/r2_gather_chunks.md)
 ``XDOT_LOCAL_FIRST``           ``0``: with several ranks the fused forward waits for the whole
                                all-gather, then runs one kernel over all T columns (default 1:
                                the rank's own block runs first, under the gather, then the peer
@@ -97,7 +96,7 @@ class _Flags:
         self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
         self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
-        self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "1") or 1)
+        self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "0") or 0)  # 0: auto
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
