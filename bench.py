@@ -45,7 +45,9 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--impl", default="auto", choices=["auto", "flash", "materialized", "ring"])
     ap.add_argument("--offset", type=int, default=None)
-    ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random"])
+    ap.add_argument("--mask", default="zeros", choices=["zeros", "none", "random", "block-causal"],
+                    help="zeros: the reference example's all-False mask (example.py:29); random: 10 %% masked; "
+                         "block-causal: 1024-wide causal blocks")
     ap.add_argument("--no-optim", action="store_true", help="(diagnostic) skip the optimizer step")
     ap.add_argument("--optim", default="xdot", choices=["xdot", "torch"],
                     help="AdamW implementation: xdot.FusedAdamW (one HIP launch) or torch's fused AdamW")
@@ -56,48 +58,84 @@ def parse(argv=None):
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--no-split-step", dest="split_step", action="store_false",
                     help="(A/B) one optimizer step after every all-reduce instead of splitting it around the last one")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the T=512 numerics check of the N-rank module against the dense fp32 module")
+    ap.add_argument("--fp32-steps", type=int, default=5,
+                    help="also time this many steps of the same step in fp32 (the reference's precision; "
+                         "0 = skip); reported as fp32_ms_per_step")
+    ap.add_argument("--fp32-warmup", type=int, default=2)
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd+bwd+grad sync+AdamW) in a HIP graph and replay it "
                          "(xdot.utils.graphs.GraphedStep; single-GPU / emulated communicators)")
     return ap.parse_args(argv)
 
 
-def main(argv=None, comm=None):
-    """``comm``: optional communicator override (``benchmarks/bench_rank.py`` passes an
-    :class:`xdot.utils.comm.EmulatedComm` to run one rank of an N-GPU step on one GPU)."""
-    a = parse(argv)
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+def numerics_check(a, comm, dev, dt, impl, T: int = 512, tol: float = 3e-2) -> float:
+    """Before timing: a T=512 forward+backward of the module on THIS job's ranks (same
+    communicator, impl and dtype as the timed step, a random 10 % mask) against the dense
+    single-device fp32 module (``distributed=False``) on the full sequence, which every rank
+    recomputes (the reference's test_gradient.py pattern).  Compares this rank's output rows,
+    input gradient and the Sum-all-reduced parameter gradients (relative Frobenius); raises
+    SystemExit(3) on a mismatch.  Returns the worst relative error."""
     import xdot
-    from xdot.utils import comm as C
-    from xdot.parallel import GradSync
+    from xdot.parallel import allreduce_gradients
 
-    emulated = comm is not None
-    comm = comm or C.init(a.backend)
     n, rank = comm.world_size, comm.rank
-    if n != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but world size {n}", file=sys.stderr)
-    dev = torch.device(a.device, C.get_local_rank() % max(1, torch.cuda.device_count())) if a.device == "cuda" \
-        else torch.device("cpu")
-    if dev.type == "cuda":
-        torch.cuda.set_device(dev)
-    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
-    T = a.seq_len
-    if T % n:
-        raise SystemExit(f"seq-len {T} not divisible by world size {n}")
+    T = max(T // n, 1) * n
     R = T // n
+    torch.manual_seed(4321)  # identical weights on every rank
+    m = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, impl=impl, comm=comm).to(dev, dt)
+    ref = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, distributed=False).to(dev, torch.float32)
+    ref.load_state_dict({k: v.float() for k, v in m.state_dict().items()})
+    g = torch.Generator(device=dev).manual_seed(99)  # identical full inputs on every rank
+    xf = torch.rand(1, T, a.dim, device=dev, generator=g)
+    mask = torch.rand(1, T, T, device=dev, generator=g) < 0.1
+    mask[..., 0] = False
+    rows = slice(rank * R, (rank + 1) * R)
+    x = xf[:, rows].to(dt).requires_grad_(True)
+    out = m(x, x, x, mask[:, rows].contiguous())
+    (out.float().square().sum() / (T * a.dim)).backward()
+    allreduce_gradients(m, comm=comm)  # per-rank partial parameter grads -> their sum
+    xr = xf.clone().requires_grad_(True)
+    outr = ref(xr, xr, xr, mask)
+    (outr.square().sum() / (T * a.dim)).backward()
 
+    def rel(u, v):
+        return float((u.detach().float() - v.detach().float()).norm() / v.detach().float().norm().clamp_min(1e-30))
+
+    errs = {"out": rel(out, outr[:, rows]), "dx": rel(x.grad, xr.grad[:, rows])}
+    for (name, p), (_, pr) in zip(m.named_parameters(), ref.named_parameters()):
+        errs["d" + name] = rel(p.grad, pr.grad)
+    worst = max(errs.values())
+    t = torch.tensor([worst], dtype=torch.float64, device=dev if "gloo" not in comm.backend else "cpu")
+    comm.all_reduce(t, op="max")
+    worst = float(t.item())
+    if not worst <= tol:  # NaN fails too
+        raise SystemExit(f"bench numerics check failed on rank {rank} (N={n}, T={T}, {impl}, {dt}): {errs}")
+    return worst
+
+
+def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
+    """Build the model/optimizer for ``dt`` and time ``steps`` training steps after
+    ``warmup`` untimed ones.  Returns (ms_per_step max over ranks, host enqueue ms, loss, impl)."""
+    import xdot
+    from xdot.parallel import GradSync
+    from xdot.ops.loss import unit_grad
+
+    n, rank = comm.world_size, comm.rank
+    T = a.seq_len
+    R = T // n
     torch.manual_seed(1234)  # identical weights on every rank
     model = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, offset=a.offset, impl=a.impl,
                                         comm=comm).to(dev, dt)
     if a.optim == "xdot":
         # one multi-tensor HIP launch per step (device-side step count when graph-captured)
-        opt = xdot.FusedAdamW(model.parameters(), lr=1e-4, capturable=a.graph)
+        opt = xdot.FusedAdamW(model.parameters(), lr=1e-4, capturable=graph)
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
     sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
     # projection's all-reduce overlaps the attention backward
     crit = xdot.MSELoss()  # fused loss + gradient pass (torch.nn.MSELoss semantics)
-    from xdot.ops.loss import unit_grad
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.rand(a.batch, R, a.dim, device=dev, dtype=dt, generator=g)
@@ -106,9 +144,13 @@ def main(argv=None, comm=None):
         mask = None
     elif a.mask == "zeros":
         mask = torch.zeros(a.batch, R, T, dtype=torch.bool, device=dev)
-    else:
+    elif a.mask == "random":
         mask = torch.rand(a.batch, R, T, device=dev, generator=g) < 0.1
         mask[..., 0] = False
+    else:  # block-causal: 1024-wide blocks, each row sees its own block and every earlier one
+        r = torch.arange(R, device=dev) + rank * R
+        c = torch.arange(T, device=dev)
+        mask = ((c[None, :] // 1024) > (r[:, None] // 1024)).unsqueeze(0).expand(a.batch, R, T).contiguous()
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -122,7 +164,7 @@ def main(argv=None, comm=None):
             opt.step()
         return loss
 
-    if a.graph:
+    if graph:
         from xdot.utils.graphs import GraphedStep
 
         def body():
@@ -134,10 +176,10 @@ def main(argv=None, comm=None):
                 opt.step()
             return loss
 
-        step = GraphedStep(body, zero_grad=opt.zero_grad, warmup=max(1, a.warmup))
+        step = GraphedStep(body, zero_grad=opt.zero_grad, warmup=max(1, warmup), optimizer=opt)
         step()  # warmup steps + capture + one replay
     else:
-        for _ in range(a.warmup):
+        for _ in range(warmup):
             step()
     impl = model._pick_impl(x)
 
@@ -147,35 +189,85 @@ def main(argv=None, comm=None):
         comm.barrier()
 
     prof = None
-    if a.profile_dir and rank == 0:
+    if profile_dir and rank == 0:
         prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
                                                   torch.profiler.ProfilerActivity.CUDA])
         prof.__enter__()
     sync_all()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         loss = step()
     th = time.perf_counter()  # host done enqueuing (diagnostic: close to t1 = host-bound step)
     sync_all()
     t1 = time.perf_counter()
     if prof is not None:
         prof.__exit__(None, None, None)
-        os.makedirs(a.profile_dir, exist_ok=True)
-        prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
-        with open(os.path.join(a.profile_dir, "ops.txt"), "w") as f:
+        os.makedirs(profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(profile_dir, "trace.json"))
+        with open(os.path.join(profile_dir, "ops.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
 
-    ms = (t1 - t0) * 1e3 / max(1, a.steps)
-    t = torch.tensor([ms], dtype=torch.float64, device=dev if comm.backend in ("nccl", "emulated") else "cpu")
+    ms = (t1 - t0) * 1e3 / max(1, steps)
+    t = torch.tensor([ms], dtype=torch.float64, device=dev if "gloo" not in comm.backend else "cpu")
     comm.all_reduce(t, op="max")
     ms = float(t.item())
     lossv = float(loss.float().item())
     if not math.isfinite(lossv):
         raise SystemExit(f"non-finite loss {lossv}")
+    del model, opt, sync, x, y, mask
+    return ms, (th - t0) * 1e3 / max(1, steps), lossv, impl
+
+
+def main(argv=None, comm=None):
+    """``comm``: optional communicator override (``benchmarks/bench_rank.py`` passes an
+    :class:`xdot.utils.comm.EmulatedComm` to run one rank of an N-GPU step on one GPU)."""
+    a = parse(argv)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from xdot.utils import comm as C
+    from xdot.utils.env import FLAGS
+
+    emulated = comm is not None
+    comm = comm or C.init(a.backend)
+    n, rank = comm.world_size, comm.rank
+    if n != a.gpus and not emulated:
+        # the job must be the N-rank job it claims to be (reference: utils/comm.py:8-9 asserts
+        # hvd.size() == the MPI world size at init)
+        msg = f"bench.py: --gpus {a.gpus} but the launch has {n} rank(s); start it with torchrun --nproc-per-node {a.gpus}"
+        print(msg, file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    dev = torch.device(a.device, C.get_local_rank() % max(1, torch.cuda.device_count())) if a.device == "cuda" \
+        else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    T = a.seq_len
+    if T % n:
+        raise SystemExit(f"seq-len {T} not divisible by world size {n}")
+    R = T // n
+
+    check_err = None
+    if not emulated and not a.no_check:
+        check_err = numerics_check(a, comm, dev, dt, a.impl)
+    ms, host_ms, lossv, impl = time_step(a, comm, dev, dt, a.steps, a.warmup, graph=a.graph,
+                                         profile_dir=a.profile_dir)
+    fp32 = None
+    if a.fp32_steps > 0 and dt != torch.float32 and dev.type == "cuda":
+        # the reference computes in fp32 only (module.py:60-71): time the same step in fp32 too
+        fp32 = time_step(a, comm, dev, torch.float32, a.fp32_steps, a.fp32_warmup)
     if rank == 0:
         metric = METRIC
         if (T, a.dim, a.heads) != (25000, 768, 8):  # not the headline config: say what was run
             metric = f"ms/fwd+bwd DistributedDotProductAttn T={T} d={a.dim} h={a.heads}"
+        from xdot.parallel.attention import _row_chunks
+
+        backend = comm.backend
+        transport = {"nccl": "rccl", "ipc+nccl": "ipc+rccl"}.get(backend, backend)
+        rccl = None
+        if "nccl" in backend:
+            try:
+                rccl = ".".join(map(str, torch.cuda.nccl.version()))
+            except Exception:  # noqa: BLE001
+                rccl = "unknown"
         rec = {
             "metric": metric,
             "value": round(ms, 4),
@@ -194,9 +286,19 @@ def main(argv=None, comm=None):
                        "step": "fwd+bwd+grad-allreduce+AdamW" if not a.no_optim else "fwd+bwd+grad-allreduce",
                        "launch": "hip-graph" if a.graph else "eager"},
             "tokens_per_s": round(a.batch * T / (ms / 1e3), 1),
-            "host_enqueue_ms_per_step": round((th - t0) * 1e3 / max(1, a.steps), 4),
+            "host_enqueue_ms_per_step": round(host_ms, 4),
             "loss": lossv,
+            "world_size": n,
+            "transport": transport,
+            "rccl_version": rccl,
+            "gather_chunks": len(_row_chunks(n, R, impl == "flash")),
+            "local_first": bool(FLAGS.local_first),
+            "numerics_check_max_rel_err": None if check_err is None else round(check_err, 5),
         }
+        if fp32 is not None:
+            rec["fp32_ms_per_step"] = round(fp32[0], 4)
+            rec["fp32_impl"] = fp32[3]
+            rec["fp32_steps"] = a.fp32_steps
         if emulated:
             link = getattr(comm, "link_gbps", None)
             what = "no transport" if link is None else f"link model {link:g} GB/s collectives, {comm.p2p_gbps:g} GB/s hops"

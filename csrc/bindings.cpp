@@ -529,13 +529,19 @@ at::Tensor flash_prescale(const at::Tensor& x, double scale) {
 // one AdamW step for lists of same-dtype params / grads with fp32 moments (chunks of 32)
 void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_avg, at::TensorList exp_avg_sq,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                const c10::optional<at::Tensor>& step_t) {
+                at::TensorList step_ts, const c10::optional<at::Tensor>& lr_t) {
   Range rr_("xdot.adamw_step");
-  const bool dev_step = step_t.has_value() && step_t->defined();
-  if (dev_step)
-    TORCH_CHECK(step_t->is_cuda() && step_t->scalar_type() == at::kFloat && step_t->numel() == 1,
-                "xdot.adamw_step: step_t must be a one-element fp32 device tensor");
   const size_t n = params.size();
+  const bool dev_state = step_ts.size() > 0;
+  if (dev_state) {
+    TORCH_CHECK(step_ts.size() == n && lr_t.has_value() && lr_t->defined(),
+                "xdot.adamw_step: device state needs one step tensor per parameter and lr_t");
+    for (const auto& t : step_ts)
+      TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() == 1,
+                  "xdot.adamw_step: step tensors must be one-element fp32 device tensors");
+    TORCH_CHECK(lr_t->is_cuda() && lr_t->scalar_type() == at::kFloat && lr_t->numel() == 1,
+                "xdot.adamw_step: lr_t must be a one-element fp32 device tensor");
+  }
   TORCH_CHECK(grads.size() == n && exp_avg.size() == n && exp_avg_sq.size() == n, "xdot.adamw_step: list sizes");
   TORCH_CHECK(step >= 1, "xdot.adamw_step: step counts from 1");
   if (n == 0) return;
@@ -561,6 +567,7 @@ void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_
       a.p[i] = params[k].data_ptr(); a.g[i] = grads[k].data_ptr();
       a.m[i] = exp_avg[k].data_ptr<float>(); a.v[i] = exp_avg_sq[k].data_ptr<float>();
       a.n[i] = params[k].numel();
+      a.step_dev[i] = dev_state ? step_ts[k].data_ptr<float>() : nullptr;
       a.blk0[i] = blk;
       const int64_t nb = (a.n[i] + xdot::ADAM_BLOCK_ELEMS - 1) / xdot::ADAM_BLOCK_ELEMS;
       TORCH_CHECK(blk + nb < (1LL << 31), "xdot.adamw_step: too many elements");
@@ -569,7 +576,8 @@ void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_
     a.blk0[a.nt] = blk;
     a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps; a.wd = (float)weight_decay;
     a.bc1 = bc1; a.bc2_sqrt = std::sqrt(bc2);
-    a.step_dev = dev_step ? step_t->data_ptr<float>() : nullptr;
+    a.dev_state = dev_state ? 1 : 0;
+    a.lr_dev = dev_state ? lr_t->data_ptr<float>() : nullptr;
     TORCH_CHECK(xdot_adamw_launch(&a, dt_code(dtype), cur_stream(params[0])) == 0, "xdot.adamw_step: dtype");
     check_launch(hipGetLastError(), "adamw_step");
   }
@@ -900,7 +908,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_fwd_merge(Tensor(a!) opart, Tensor lpart, Tensor(b!) lrun, int H) -> ()");
   m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
-        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor? step_t=None) -> ()");
+        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts=[], Tensor? lr_t=None) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");

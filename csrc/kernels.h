@@ -99,8 +99,13 @@ struct AdamArgs {
   int blk0[ADAM_MAX_T + 1];  // first block of each tensor (prefix sum)
   int nt;
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
-  const float* step_dev;  // non-null: the step count lives on the device (graph-capturable
-                          // optimizer); bc1 / bc2_sqrt are then computed from it in the kernel
+  // graph-capturable optimizer (dev_state = 1): every tensor's step count lives on the device
+  // (the optimizer's per-parameter state["step"], advanced by a device op before the update)
+  // and so does the learning rate (refreshed from the param group before each replay); bc1 /
+  // bc2_sqrt / lr are then read in the kernel
+  int dev_state;
+  const float* step_dev[ADAM_MAX_T];
+  const float* lr_dev;
 };
 namespace ipc {
 constexpr int MAXR = 8;     // ranks of one node

@@ -22,21 +22,22 @@ template <int DT>
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   using TP = typename dt_traits<DT>::T;
   const int blk = blockIdx.x;
-  int t = 0;
-  while (t + 1 < a.nt && blk >= a.blk0[t + 1]) ++t;  // wave-uniform search over <= 32 entries
-  const int64_t base = (int64_t)(blk - a.blk0[t]) * ADAM_BLOCK_ELEMS + threadIdx.x * 4;
-  const int64_t n = a.n[t];
-  TP* p = reinterpret_cast<TP*>(a.p[t]);
-  const TP* g = reinterpret_cast<const TP*>(a.g[t]);
-  float* m = a.m[t];
-  float* v = a.v[t];
-  float bc1 = a.bc1, bc2_sqrt = a.bc2_sqrt;
-  if (a.step_dev) {  // captured in a HIP graph: the step advances on the device between replays
-    const float t = *a.step_dev;
+  int t_ = 0;
+  while (t_ + 1 < a.nt && blk >= a.blk0[t_ + 1]) ++t_;  // wave-uniform search over <= 32 entries
+  const int64_t base = (int64_t)(blk - a.blk0[t_]) * ADAM_BLOCK_ELEMS + threadIdx.x * 4;
+  const int64_t n = a.n[t_];
+  TP* p = reinterpret_cast<TP*>(a.p[t_]);
+  const TP* g = reinterpret_cast<const TP*>(a.g[t_]);
+  float* m = a.m[t_];
+  float* v = a.v[t_];
+  float bc1 = a.bc1, bc2_sqrt = a.bc2_sqrt, lr = a.lr;
+  if (a.dev_state) {  // captured in a HIP graph: step and lr are read from device memory
+    const float t = *a.step_dev[t_];
     bc1 = 1.f - __builtin_powf(a.beta1, t);
     bc2_sqrt = __builtin_sqrtf(1.f - __builtin_powf(a.beta2, t));
+    lr = *a.lr_dev;
   }
-  const float step_size = a.lr / bc1, decay = 1.f - a.lr * a.wd;
+  const float step_size = lr / bc1, decay = 1.f - lr * a.wd;
   auto upd = [&](float pi, float gi, float& mi, float& vi) {
     mi = a.beta1 * mi + (1.f - a.beta1) * gi;
     vi = a.beta2 * vi + (1.f - a.beta2) * gi * gi;

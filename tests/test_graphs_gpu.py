@@ -53,3 +53,65 @@ def test_graphed_step_matches_eager(gpu):
     # replays keep training: the parameters moved between steps
     _, p1 = _train(gpu, True, steps=4)
     assert any((a - b).abs().max().item() > 0 for a, b in zip(p1, pg))
+
+
+def _adam_run(gpu, steps, resume_at=None, capturable=True):
+    import xdot
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(1000, device=gpu))
+    opt = xdot.FusedAdamW([w], lr=1e-2, capturable=capturable)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    grads = [torch.randn(1000, device=gpu, generator=g) for _ in range(steps)]
+    for i in range(steps):
+        if resume_at is not None and i == resume_at:
+            sd = opt.state_dict()
+            opt = xdot.FusedAdamW([w], lr=1e-2, capturable=capturable)
+            opt.load_state_dict(sd)
+        w.grad = grads[i].clone()
+        opt.step()
+    torch.cuda.synchronize()
+    return w.detach().clone(), opt
+
+
+def test_capturable_adamw_state_round_trips(gpu):
+    """state['step'] of a capturable FusedAdamW lives on the device and survives
+    state_dict/load_state_dict: a resumed run equals a continuous one (no bias-correction
+    restart), and equals the non-capturable optimizer."""
+    a, opt = _adam_run(gpu, 4)
+    b, _ = _adam_run(gpu, 4, resume_at=2)
+    c, _ = _adam_run(gpu, 4, capturable=False)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-6)
+    st = opt.state_dict()["state"][0]["step"]
+    assert torch.is_tensor(st) and float(st) == 4.0
+
+
+def test_graphed_step_follows_lr_changes(gpu):
+    """The captured update reads lr from the device: changing group['lr'] between replays
+    (an LR scheduler) takes effect; lr = 0 freezes the parameters."""
+    import xdot
+    from xdot.utils.graphs import GraphedStep
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(256, device=gpu))
+    opt = xdot.FusedAdamW([w], lr=1e-2, weight_decay=0.0, capturable=True)
+    x = torch.randn(256, device=gpu)
+
+    def body():
+        loss = (w * x).sum()
+        loss.backward()
+        opt.step()
+        return loss
+
+    st = GraphedStep(body, zero_grad=opt.zero_grad, warmup=1, optimizer=opt)
+    st()
+    w1 = w.detach().clone()
+    opt.param_groups[0]["lr"] = 0.0
+    st()
+    torch.cuda.synchronize()
+    assert torch.equal(w.detach(), w1)
+    opt.param_groups[0]["lr"] = 1e-2
+    st()
+    torch.cuda.synchronize()
+    assert not torch.equal(w.detach(), w1)

@@ -23,3 +23,12 @@ def test_fused_adamw_matches_torch_cpu():
     b = _run(torch.optim.AdamW, params, grads, 4, **kw)
     for x, y in zip(a, b):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_graphed_step_rejects_zero_warmup():
+    import pytest
+
+    from xdot.utils.graphs import GraphedStep
+
+    with pytest.raises(ValueError):
+        GraphedStep(lambda: None, warmup=0)

@@ -58,6 +58,19 @@ def test_bench_contract_cpu():
     assert r["value"] > 0 and r["value"] == r["ms_per_step"] and r["higher_is_better"] is False
     assert r["config"]["seq_len"] == 128 and "T=128" in r["metric"]
     assert "synthetic" in r["data"]
+    # launch / transport record and the pre-timing numerics check
+    assert r["world_size"] == 1 and r["transport"] == "local" and r["rccl_version"] is None
+    assert r["gather_chunks"] == 1 and r["local_first"] in (True, False)
+    assert 0 <= r["numerics_check_max_rel_err"] < 1e-3  # fp32 on the CPU: the same math
+
+
+def test_bench_rejects_wrong_world_size():
+    """--gpus 2 under a 1-rank launch exits non-zero instead of timing the wrong job."""
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--seq-len", "64", "--dim", "32",
+                        "--heads", "2", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode != 0 and "rank(s)" in p.stderr, (p.returncode, p.stderr[-2000:])
+    assert not _json_lines(p.stdout)
 
 
 @pytest.mark.parametrize("impl", ["auto", "ring"])
@@ -69,6 +82,27 @@ def test_bench_two_ranks_gloo(impl):
     recs = _json_lines(out)
     assert len(recs) == 1, out
     assert recs[0]["n_gpus"] == 2 and recs[0]["config"]["parallelism"] == "sp2"
+    assert recs[0]["world_size"] == 2 and recs[0]["transport"] == "gloo"
+    assert recs[0]["numerics_check_max_rel_err"] < 1e-3
+
+
+def test_bench_mismatched_collective_knobs_raise():
+    """Ranks launched with different XDOT_GATHER_CHUNKS fail at init (both ranks), not hang."""
+    env = _env()
+    args = [sys.executable, "-c",
+            "import os, sys; os.environ['XDOT_GATHER_CHUNKS'] = str(1 + int(os.environ['RANK'])); "
+            "sys.argv = ['bench.py', '--gpus', '2', '--device', 'cpu', '--backend', 'gloo', '--seq-len', '64', "
+            "'--dim', '32', '--heads', '2', '--steps', '1', '--warmup', '0']; "
+            "import runpy; runpy.run_path('bench.py', run_name='__main__')"]
+    # torchrun needs a script path: write the launcher next to the repo's scripts
+    launcher = os.path.join(ROOT, "build", "knob_mismatch_launcher.py")
+    os.makedirs(os.path.dirname(launcher), exist_ok=True)
+    with open(launcher, "w") as f:
+        f.write(args[2].replace("; ", "\n"))
+    p = subprocess.run([sys.executable] + _torchrun(2) + [launcher], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert "disagree on collective-shaping flags" in p.stderr + p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
 
 
 @pytest.mark.parametrize("mode", ["nt", "all", "tn"])

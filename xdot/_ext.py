@@ -14,7 +14,7 @@ import torch
 from .utils.env import FLAGS
 
 # XDOT_EXT_PATH: load a differently built copy (A/B kernel experiments in one GPU session)
-_LIB = os.environ.get("XDOT_EXT_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
+_LIB = FLAGS.ext_path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
 _lock = threading.Lock()
 _state = {"loaded": False, "error": None}
 

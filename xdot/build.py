@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build", "xdot")
 OUT = os.path.join(ROOT, "xdot", "_C.so")
-ARCH = os.environ.get("XDOT_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X only
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -68,7 +68,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
     # -fno-slp-vectorize: no v_pk_mul/add_f32 beside the MFMAs (packed f32 VALU costs ~13
     # issue cycles per instruction in an MFMA gap vs 4 for each scalar v_fma/v_mul: the
     # softmax / softmax-grad epilogues of the flash kernels are VALU-issue bound)
-    extra = os.environ.get("XDOT_HIPCC_FLAGS", "-fno-slp-vectorize").split()
+    from .utils.env import FLAGS
+
+    extra = (FLAGS.hipcc_flags or "-fno-slp-vectorize").split()
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", CSRC] + extra + [
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
               "-Wno-unused-result", "-Wno-unused-variable"]

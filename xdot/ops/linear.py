@@ -16,7 +16,6 @@ in the caller's ``nn.Linear`` modules (``state_dict`` compatible with the refere
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Optional
 
 import torch
@@ -53,16 +52,14 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
     x = x.contiguous()
     # 256x256 kernel.  K slabs of the 128x128 kernel are faster in isolation at short K (K = 3125:
     # 36 vs 44 µs at 768²) but not inside the step (emulated N=8 rank 1.350 vs 1.343 ms):
-    # profiles/r2_wgrad_route.md.  XDOT_WGRAD_PATH = 128 forces the slab path.
-    path = os.environ.get("XDOT_WGRAD_PATH", "auto")
-    big = path != "128"
-    if big and M % 8 == 0 and N % 8 == 0 and min(M, N) >= 128:
+    # profiles/r2_wgrad_route.md; the slab path serves the shapes the 256x256 kernel does not take.
+    if M % 8 == 0 and N % 8 == 0 and min(M, N) >= 128:
         # 256x256 LDS-DMA kernel: it picks the K split itself (fp32 slices, one vectorised
         # in-order reduction that also casts to the parameter dtype)
         out = torch.empty(M, N, dtype=out_dtype, device=dy.device)
         strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True, path=2)
         return out
-    S = int(os.environ.get("XDOT_WGRAD_SPLITS", "0") or 0) or _splits(M, N, K)
+    S = _splits(M, N, K)
     slab = K // S
     part = torch.empty(S + (1 if K % S else 0), M, N, dtype=torch.float32, device=dy.device)
     if slab > 0:

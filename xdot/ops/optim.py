@@ -8,11 +8,16 @@ every group in one multi-tensor kernel per (group, dtype).  Semantics follow
 parameters and anything the kernel does not take fall back to ``torch.optim.AdamW``'s
 functional update.
 
-``capturable=True`` keeps the step count on the device (one fp32 scalar per parameter group
-and dtype, advanced by a device op before each update, the bias corrections computed in the
-kernel from it), so ``step()`` can be recorded in a HIP graph and replayed
-(:class:`xdot.utils.graphs.GraphedStep`); every parameter of the group must then have a
-gradient at every step.
+``capturable=True`` keeps the optimizer state the update reads on the device, as
+``torch.optim.AdamW(capturable=True)`` does: every parameter's ``state["step"]`` is a 0-d fp32
+device tensor (advanced by one multi-tensor device op before each update, the bias corrections
+computed in the kernel from it; it round-trips through ``state_dict``/``load_state_dict`` and a
+resumed run continues its bias correction), and each param group's learning rate lives in a
+one-element device tensor that :meth:`FusedAdamW.sync_lr` refreshes from ``group["lr"]``.  So
+``step()`` can be recorded in a HIP graph and replayed (:class:`xdot.utils.graphs.GraphedStep`
+calls ``sync_lr`` before every replay, so LR schedulers keep working); every parameter of the
+group must then have a gradient at every step.  ``weight_decay``/``betas``/``eps`` are baked in
+at capture time.
 """
 from __future__ import annotations
 
@@ -32,7 +37,7 @@ class FusedAdamW(torch.optim.Optimizer):
             raise ValueError("invalid AdamW hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.capturable = capturable
-        self._dev_step = {}  # (group index, dtype, device) -> fp32 device step count
+        self._lr_dev = {}  # (group index, device) -> one-element fp32 device tensor (capturable)
 
     @torch.no_grad()
     def step(self, closure=None, params=None):
@@ -56,31 +61,69 @@ class FusedAdamW(torch.optim.Optimizer):
                     continue
                 st = self.state[p]
                 if not st:
-                    st["step"] = 0
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device) if self.capturable else 0
                     st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
-                st["step"] += 1
                 hip = (p.is_cuda and p.dtype in (torch.bfloat16, torch.float16, torch.float32) and p.is_contiguous()
                        and _ext.use_hip(p))
+                if self.capturable:
+                    if not hip:
+                        raise RuntimeError("FusedAdamW(capturable=True) needs contiguous bf16/fp16/fp32 GPU parameters")
+                    st["step"] = self._dev_step_of(st["step"], p.device)
+                    buckets.setdefault((p.dtype, p.device, 0), []).append(p)
+                    continue
+                if torch.is_tensor(st["step"]):  # a state loaded from a capturable optimizer
+                    st["step"] = int(st["step"].item())
+                st["step"] += 1
                 if hip:
-                    buckets.setdefault((p.dtype, p.device, 0 if self.capturable else st["step"]), []).append(p)
-                elif self.capturable:
-                    raise RuntimeError("FusedAdamW(capturable=True) needs contiguous bf16/fp16/fp32 GPU parameters")
+                    buckets.setdefault((p.dtype, p.device, st["step"]), []).append(p)
                 else:
                     self._torch_update(p, st, group, b1, b2)
             for (dt, dev, step), ps in buckets.items():
-                step_t = None
+                steps, lr_t = [], None
                 if self.capturable:
-                    key = (gi, dt, dev)
-                    step_t = self._dev_step.get(key)
-                    if step_t is None:
-                        step_t = self._dev_step[key] = torch.zeros((), dtype=torch.float32, device=dev)
-                    step_t.add_(1.0)  # a device op: advances on every graph replay too
+                    steps = [self.state[p]["step"] for p in ps]
+                    torch._foreach_add_(steps, 1.0)  # device ops: advance on every graph replay too
+                    lr_t = self._lr_tensor(gi, group, dev)
                     step = 1
                 _ext.ops().adamw_step(ps, [p.grad.contiguous() for p in ps], [self.state[p]["exp_avg"] for p in ps],
                                       [self.state[p]["exp_avg_sq"] for p in ps], float(group["lr"]), float(b1),
-                                      float(b2), float(group["eps"]), float(group["weight_decay"]), int(step), step_t)
+                                      float(b2), float(group["eps"]), float(group["weight_decay"]), int(step),
+                                      steps, lr_t)
         return loss
+
+    @staticmethod
+    def _dev_step_of(step, device) -> torch.Tensor:
+        """The parameter's step count as a 0-d fp32 device tensor (seeded from a loaded int or
+        tensor state, so a resumed run continues its bias correction)."""
+        if torch.is_tensor(step):
+            if step.device == device and step.dtype == torch.float32 and step.dim() == 0:
+                return step
+            return step.detach().reshape(()).to(device=device, dtype=torch.float32)
+        return torch.full((), float(step), dtype=torch.float32, device=device)
+
+    def _lr_tensor(self, gi, group, dev) -> torch.Tensor:
+        t = self._lr_dev.get((gi, dev))
+        if t is None:
+            t = self._lr_dev[(gi, dev)] = torch.full((1,), float(group["lr"]), dtype=torch.float32, device=dev)
+        elif not torch.cuda.is_current_stream_capturing():
+            t.fill_(float(group["lr"]))  # eager step: follow the group's current lr
+        return t
+
+    def sync_lr(self) -> None:
+        """Copy every param group's current ``lr`` into its device tensor (capturable mode; call
+        before replaying a captured step so schedulers take effect — GraphedStep does)."""
+        for (gi, _dev), t in self._lr_dev.items():
+            t.fill_(float(self.param_groups[gi]["lr"]))
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self.capturable:  # re-home loaded step counts on the parameters' devices now
+            for group in self.param_groups:
+                for p in group["params"]:
+                    st = self.state.get(p)
+                    if st and "step" in st:
+                        st["step"] = self._dev_step_of(st["step"], p.device)
 
     @staticmethod
     def _torch_update(p, st, group, b1, b2):

@@ -26,7 +26,6 @@ schedule with a torch reference implementation of steps 2-5.
 """
 from __future__ import annotations
 
-import os
 
 from typing import List, Optional, Tuple
 
@@ -325,14 +324,6 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
 _SIDE = {}
 
 
-def _bwd_overlap(B: int, R: int, H: int) -> bool:
-    """Row-side kernel concurrent with the gathered-side kernel (XDOT_BWD_OVERLAP)?"""
-    ov = FLAGS.bwd_overlap
-    if ov != "auto":
-        return ov not in ("0", "false", "off", "no")
-    return -(-R // 128) * B * H >= int(os.environ.get("XDOT_BWD_OVERLAP_TILES", "0") or 0)
-
-
 def _side_stream(dev: torch.device, priority: int = -1) -> "torch.cuda.Stream":
     """Per-device compute stream of the backward (created once per priority; -1 = high)."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -432,9 +423,9 @@ class SeqParallelAttention(torch.autograd.Function):
             # the GPU first.  Per-chunk kernels (chunk c's reduce-scatter under chunk c+1's
             # kernel) only when the chunks are separate buffers (B > 1).
             cur = torch.cuda.current_stream(do.device)
-            # high priority so the gathered side (and its reduce-scatter) finishes early;
-            # XDOT_BWD_SIDE_PRIO=0 makes it an ordinary stream (A/B knob)
-            hi = _side_stream(do.device, int(os.environ.get("XDOT_BWD_SIDE_PRIO", "-1")))
+            # high priority so the gathered side (and its reduce-scatter) finishes early (an
+            # ordinary-priority side stream measured slower at N=1 and N=8: profiles/r2_bwd_overlap.md)
+            hi = _side_stream(do.device, -1)
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
@@ -468,10 +459,9 @@ class SeqParallelAttention(torch.autograd.Function):
                                              None if dqv is None else dqv[:, r0:r0 + rc])
                         handles.append(h)
                         outs.append(oc)
-            if _bwd_overlap(B, R, H):
-                cur.wait_event(ev)
-            else:  # small rank shapes: back to back (measured: concurrency costs more than it fills)
-                cur.wait_stream(hi)
+            # the row-side kernel starts as soon as δ exists: back to back measured slower at
+            # every rank shape (profiles/r2_bwd_overlap.md)
+            cur.wait_event(ev)
             delta.record_stream(cur)
             if one:
                 g = bufs[0]

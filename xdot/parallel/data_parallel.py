@@ -136,6 +136,8 @@ class GradSync:
         self._handles: List = []
         self._hooks = []
         self._muted = False
+        self._rest_key = None
+        self._rest: List[torch.Tensor] = []
         if self.comm.world_size > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -181,8 +183,9 @@ class GradSync:
         """Order the current stream after every bucket's all-reduce.  With ``optimizer`` (one
         whose ``step`` takes ``params=``, e.g. :class:`xdot.FusedAdamW`) the update is split: the
         buckets reduced before the last one are stepped while the last all-reduce (the gradient
-        that arrives last in backward) is still on the wire, then the last bucket.  Returns
-        True when the optimizer has stepped."""
+        that arrives last in backward) is still on the wire, then the last bucket together with
+        every optimizer parameter outside the buckets.  Returns True when the optimizer has
+        stepped (every parameter it holds, exactly once)."""
         ws = self.comm.world_size
         split = (optimizer is not None and ws > 1 and len(self._handles) > 1
                  and not getattr(optimizer, "capturable", False) and _takes_params(type(optimizer)))
@@ -212,9 +215,23 @@ class GradSync:
                 p.grad.copy_(flat[off:off + n].view_as(p.grad))
                 off += n
         if split:
-            optimizer.step(params=list(self.buckets[self._handles[last][0]]))
+            rest = self._outside_params(optimizer)
+            optimizer.step(params=list(self.buckets[self._handles[last][0]]) + rest)
         self._reset()
         return split
+
+    def _outside_params(self, optimizer) -> List[torch.Tensor]:
+        """Parameters the optimizer holds that are not in this GradSync's buckets (a second
+        module, an extra param group, a parameter outside ``module.parameters()``): a split
+        step must update them too, else they would silently never train.  Cached per
+        (optimizer, parameter count)."""
+        key = (id(optimizer), sum(len(g["params"]) for g in optimizer.param_groups))
+        if self._rest_key != key:
+            mine = {id(p) for b in self.buckets for p in b}
+            self._rest = [p for g in optimizer.param_groups for p in g["params"]
+                          if id(p) not in mine and p.requires_grad]
+            self._rest_key = key
+        return self._rest
 
     def _reset(self):
         self._handles.clear()

@@ -35,10 +35,12 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .env import FLAGS
+
 __all__ = [
     "Communicator", "TorchDistComm", "LocalComm", "EmulatedComm", "ThreadComm", "ThreadGroup", "Handle",
     "init", "is_initialized", "get_comm", "use_comm", "get_world_size", "get_rank",
-    "get_local_rank", "is_main_process", "synchronize", "destroy", "resolve_backend",
+    "get_local_rank", "is_main_process", "synchronize", "destroy", "resolve_backend", "check_collective_knobs",
 ]
 
 
@@ -611,14 +613,14 @@ def init(backend: str = "auto", timeout_s: Optional[float] = None, set_device: b
         if set_device and torch.cuda.is_available():
             torch.cuda.set_device(get_local_rank() % max(1, torch.cuda.device_count()))
     kw = {}
-    t = timeout_s if timeout_s is not None else float(os.environ.get("XDOT_COMM_TIMEOUT_S", "600"))
+    t = timeout_s if timeout_s is not None else FLAGS.comm_timeout_s
     kw["timeout"] = datetime.timedelta(seconds=t)
     if be == "nccl" and torch.cuda.is_available():
         kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
     dist.init_process_group(be, **kw)
     _DEFAULT = TorchDistComm()
-    if (_DEFAULT.world_size > 1 and torch.cuda.is_available()
-            and os.environ.get("XDOT_IPC", "0").strip().lower() not in ("", "0", "false", "no", "off")):
+    check_collective_knobs(_DEFAULT)
+    if _DEFAULT.world_size > 1 and torch.cuda.is_available() and FLAGS.ipc:
         # stage 2: xGMI pull all-gather / reduce-scatter (csrc/ipc.hip).  Over gloo too: several
         # ranks sharing one GPU rehearse the device-side collectives (RCCL refuses that layout)
         from .ipc import IpcComm
@@ -626,6 +628,25 @@ def init(backend: str = "auto", timeout_s: Optional[float] = None, set_device: b
             torch.cuda.set_device(get_local_rank() % max(1, torch.cuda.device_count()) if set_device else 0)
         _DEFAULT = IpcComm(_DEFAULT)
     return _DEFAULT
+
+
+def check_collective_knobs(comm: "Communicator") -> None:
+    """Raise on every rank if the ranks disagree on a flag that changes the number or dtype
+    of the collectives an op issues (``xdot.utils.env.COLLECTIVE_KNOBS``: gather chunks,
+    local-first, IPC, ops schedule, ...).  Mismatched ranks would otherwise issue different
+    collective sequences and hang until the timeout.  Called by :func:`init` for multi-rank
+    communicators (the reference asserts its world size at init: ``utils/comm.py:8-9``)."""
+    if comm.world_size == 1:
+        return
+    from .env import collective_knobs
+
+    mine = collective_knobs()
+    everyone = comm.all_gather_object(mine)
+    bad = sorted(k for k in mine if any(o.get(k) != mine[k] for o in everyone))
+    if bad:
+        vals = {k: [o.get(k) for o in everyone] for k in bad}
+        raise RuntimeError(f"xdot: ranks disagree on collective-shaping flags {vals} (per rank); set the same "
+                           "XDOT_* environment on every rank")
 
 
 def is_initialized() -> bool:

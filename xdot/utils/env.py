@@ -1,76 +1,56 @@
-"""Runtime flags (environment variables), read once at import and overridable in code.
+"""Runtime flags (environment variables): the ONE place xdot reads ``XDOT_*`` variables.
 
-=============================  ==========================================================
-``XDOT_DEBUG`` / ``DISTRIBUTED_DOT_DEBUG``  print per-op shapes, HBM delta and synced time
-                                           (reference alias: ``functions.py:21``)
-``XDOT_CHECK``                 all-gather an op fingerprint before every distributed op
-                               and raise on rank divergence (instead of hanging)
-``XDOT_BACKEND``               ``auto`` | ``hip`` | ``torch``: compute backend for GPU tensors
-``XDOT_ALLOW_TORCH_FALLBACK``  ``1`` lets GPU ops fall back to torch when ``_C.so`` is absent
-                               (default: fail loudly)
-``XDOT_COMM_TIMEOUT_S``        collective timeout in seconds (default 600)
-``XDOT_CHUNK_BUDGET_MB``       transient-buffer budget used by the chunk planner (``offset='auto'``)
-                               and by the grouped offset-row gathers of ``nt`` / ``all`` (a
-                               quarter per group; default 256 MB per group)
-``XDOT_GRAD_FP32``             ``1``: the fused attention's gathered-side gradient partials are
-                               kept and reduce-scattered in fp32 (default: rounded once to
-                               the bf16/fp16 compute dtype in the kernel, half the bytes)
-``XDOT_ROCTX``                 ``1``: roctx ranges around every native op (rocprofv3 markers)
-``XDOT_GATHER_CHUNKS``         row chunks of the fused attention's all-gather / reduce-scatter
-                               pipeline with several ranks (default auto: 2 from 8 ranks on, else
-                               1; with a 300 GB/s link model 2 chunks save 44 µs per N=8 rank step
-                               and lose 12 µs at N=4, profiles/r2_gather_chunks.md)
-``XDOT_LOCAL_FIRST``           ``0``: with several ranks the fused forward waits for the whole
-                               all-gather, then runs one kernel over all T columns (default 1:
-                               the rank's own block runs first, under the gather, then the peer
-                               blocks of each chunk as it lands; one log-sum-exp combine)
-``XDOT_MASK_ASYNC``            ``1``: pack the attention mask on a side stream, overlapping the
-                               projection GEMMs (default off: neutral at N=1, 1.7 % slower at the
-                               emulated N=8 rank, profiles/r1_s7_mask_async_ab.md; with several
-                               ranks packing already overlaps the all-gather)
-``XDOT_PRESCALE``              ``0``: flash kernels scale every score by scale*log2 e (default 1:
-                               the row side is pre-multiplied once per forward — one bf16
-                               rounding, the same buffer for forward and backward — and the
-                               score accumulators are seeded with the row max / LSE; forward
-                               2.11 -> 1.98 ms at T=R=25000)
-``XDOT_RING_OVERLAP``          ring attention backward: ``1`` runs each block's gathered-side and
-                               row-side kernels on two streams, ``0`` on one; default ``auto``:
-                               two streams when a block has >= 1024 row tiles of 128 x heads
-                               (measured, 1x MI355X, T=25000: N=1 9.21 -> 8.71 ms with two
-                               streams, emulated N=8 rank 2.46 -> 2.63 ms, i.e. worse)
-``XDOT_BWD_OVERLAP``           fused attention backward: ``1`` runs the row-side kernel concurrently
-                               with the gathered-side kernel (two streams), ``0`` after it (the
-                               reduce-scatter still overlaps it); default ``auto``: concurrent
-                               when the rank has >= XDOT_BWD_OVERLAP_TILES row tiles of 128 x heads
-                               (default 0: always; back to back measured slower at every rank
-                               shape, profiles/r2_bwd_overlap.md)
-``XDOT_BWD_SIDE_PRIO``         priority of the fused backward's gathered-side stream (default -1 =
-                               high; 0 measured slower at N=1 and N=8, profiles/r2_bwd_overlap.md)
-``XDOT_WGRAD_PATH``            weight-gradient GEMM: ``auto`` (the 256x256 split-K kernel) or ``128``
-                               (K slabs of the 128x128 kernel, ``XDOT_WGRAD_SPLITS`` slabs);
-                               profiles/r2_wgrad_route.md
-``XDOT_ROWS_PIPE``             ``0``: plain (not software-pipelined) body of the flash backward
-                               row kernel (default 1: VALU of one sub-tile issues between the
-                               next sub-tile's MFMAs; 1.5 % faster kernel)
-``XDOT_ROWS_NSPLIT``           column splits of the flash backward row kernel (default: the
-                               occupancy model; 1 measured 7 % / 32 % slower at N = 1 / 8 ranks)
-``XDOT_OPS_SCHEDULE``          ``ring``: the distributed products (``nt`` / ``all`` / ``tn`` and the
-                               autograd ops / materialised path built on them) move the shards
-                               rank to rank over point-to-point send/recv instead of all-gather /
-                               reduce-scatter (default ``gather``: faster over xGMI's full mesh;
-                               the ring holds two shards instead of the gathered side)
-``XDOT_IPC``                   ``1``: with RCCL and several ranks, all-gathers and reduce-scatters
-                               run as native xGMI pull kernels over HIP IPC
-                               (``xdot/utils/ipc.py``, ``csrc/ipc.hip``; default 0 = RCCL).
-                               ``XDOT_IPC_MB`` staging MiB per slot (512), ``XDOT_IPC_TIMEOUT_S``
-                               bound of every device-side wait (30),
-                               ``XDOT_IPC_WGS`` workgroups (byte ranges) per collective (128)
-``XDOT_WGRAD_SIDE``            ``0``: the packed [q|v] projection's weight gradient runs on the
-                               main stream after the attention backward (default 1: on the
-                               backward's priority stream as soon as the gathered-side gradient
-                               lands, overlapping the row-side kernel)
-``XDOT_EXT_PATH``              load this build of the extension instead of ``xdot/_C.so``
-=============================  ==========================================================
+Read once at import (``FLAGS.reload()`` re-reads them) and overridable in code; the native
+extension reads the three marked (C++) itself, at its first use.  The reference has a single
+flag (``DISTRIBUTED_DOT_DEBUG``, ``multiplication/functions.py:21``); everything else here is a
+documented default of this MI355X build, mostly with the measurement that chose it.
+
+==========================  ========  ===========================================================
+variable                    default   effect
+==========================  ========  ===========================================================
+``XDOT_DEBUG`` /            0         print per-op shapes, HBM delta and synced time (reference
+``DISTRIBUTED_DOT_DEBUG``             alias)
+``XDOT_CHECK``              0         all-gather an op fingerprint before every distributed op and
+                                      raise on rank divergence instead of hanging  [collective]
+``XDOT_BACKEND``            auto      ``auto`` | ``hip`` | ``torch``: compute backend of GPU tensors
+``XDOT_ALLOW_TORCH_FALLBACK`` 0       let GPU ops fall back to torch when ``_C.so`` is absent
+                                      (default: fail loudly)
+``XDOT_EXT_PATH``           (in-tree) load this build of the extension instead of ``xdot/_C.so``
+``XDOT_COMM_TIMEOUT_S``     600       bound of every collective (process group timeout; also the
+                                      default bound of the IPC kernels' device-side waits)
+``XDOT_CHUNK_BUDGET_MB``    0 (auto)  transient-buffer budget of the chunk planner and of the
+                                      grouped offset gathers of ``nt`` / ``all``  [collective]
+``XDOT_OPS_SCHEDULE``       gather    ``ring``: the distributed products move shards rank to rank
+                                      (send/recv) instead of all-gather / reduce-scatter  [collective]
+``XDOT_GATHER_CHUNKS``      0 (auto)  row chunks of the fused attention's gather / reduce-scatter
+                                      pipeline (auto: 2 from 8 ranks on, else 1;
+                                      profiles/r2_gather_chunks.md)  [collective]
+``XDOT_LOCAL_FIRST``        1         fused forward: the rank's own block runs under the gather
+                                      (0: wait for the whole gather)  [collective]
+``XDOT_GRAD_FP32``          0         reduce-scatter the gathered-side gradient partials in fp32
+                                      (default: rounded once to bf16/fp16 in the kernel)  [collective]
+``XDOT_IPC``                0         all-gathers / reduce-scatters as native xGMI pull kernels over
+                                      HIP IPC (``csrc/ipc.hip``)  [collective]
+``XDOT_IPC_MB``             512       IPC staging MiB per slot
+``XDOT_IPC_WGS``            64        workgroups (byte ranges) per IPC collective
+``XDOT_IPC_TIMEOUT_S``      (comm)    bound of every IPC device-side wait
+``XDOT_PRESCALE``           1         pre-multiply the row side by scale·log2 e once per forward
+                                      (seeded score accumulators; forward 2.11 -> 1.98 ms)
+``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
+                                      1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
+``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
+                                      stream as soon as the gathered-side gradient lands
+``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
+                                      tiles of 128 x heads)
+``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
+``XDOT_GEMM_LIB`` (C++)     see doc   plain large products on hipBLASLt instead of the hand-written
+                                      MFMA GEMM (``csrc/bindings.cpp``)
+``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
+==========================  ========  ===========================================================
+
+Variables marked [collective] change how many collectives an op issues (or their dtype):
+ranks that disagree would hang, so :func:`collective_knobs` is cross-checked by
+``xdot.utils.comm.init`` when it creates a multi-rank communicator.
 """
 from __future__ import annotations
 
@@ -85,6 +65,17 @@ def _flag(*names: str, default: str = "0") -> bool:
     return default not in ("0", "")
 
 
+def _str(name: str, default: str) -> str:
+    return (os.environ.get(name, default) or default).strip().lower()
+
+
+def _num(name: str, default, typ=float):
+    v = os.environ.get(name)
+    if v is None or not v.strip():
+        return default
+    return typ(v)
+
+
 class _Flags:
     def __init__(self):
         self.reload()
@@ -92,18 +83,33 @@ class _Flags:
     def reload(self):
         self.debug = _flag("XDOT_DEBUG", "DISTRIBUTED_DOT_DEBUG")
         self.check = _flag("XDOT_CHECK")
-        self.backend = os.environ.get("XDOT_BACKEND", "auto").lower()
+        self.backend = _str("XDOT_BACKEND", "auto")
         self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
-        self.chunk_budget_mb = float(os.environ.get("XDOT_CHUNK_BUDGET_MB", "0") or 0)
+        self.ext_path = os.environ.get("XDOT_EXT_PATH") or None
+        self.comm_timeout_s = _num("XDOT_COMM_TIMEOUT_S", 600.0)
+        self.chunk_budget_mb = _num("XDOT_CHUNK_BUDGET_MB", 0.0)
+        self.ops_schedule = _str("XDOT_OPS_SCHEDULE", "gather")
+        self.gather_chunks = _num("XDOT_GATHER_CHUNKS", 0, int)  # 0: auto
+        self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
-        self.gather_chunks = int(os.environ.get("XDOT_GATHER_CHUNKS", "0") or 0)  # 0: auto
+        self.ipc = _flag("XDOT_IPC")
+        self.ipc_mb = _num("XDOT_IPC_MB", 512.0)
+        self.ipc_wgs = _num("XDOT_IPC_WGS", 64, int)
+        self.ipc_timeout_s = _num("XDOT_IPC_TIMEOUT_S", self.comm_timeout_s)
+        self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
-        self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
-        self.prescale = _flag("XDOT_PRESCALE", default="1")
-        self.ring_overlap = os.environ.get("XDOT_RING_OVERLAP", "auto").strip().lower() or "auto"
-        self.bwd_overlap = os.environ.get("XDOT_BWD_OVERLAP", "auto").strip().lower() or "auto"
-        self.ops_schedule = os.environ.get("XDOT_OPS_SCHEDULE", "gather").strip().lower() or "gather"
+        self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
+        self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
 
 
 FLAGS = _Flags()
+
+# flags that change the number (or dtype) of the collectives an op issues
+COLLECTIVE_KNOBS = ("check", "chunk_budget_mb", "ops_schedule", "gather_chunks", "local_first", "grad_fp32",
+                    "ipc", "ipc_wgs")
+
+
+def collective_knobs() -> dict:
+    """This process's values of the [collective] flags (every rank must agree on them)."""
+    return {k: getattr(FLAGS, k) for k in COLLECTIVE_KNOBS}

@@ -27,14 +27,19 @@ __all__ = ["GraphedStep"]
 
 
 class GraphedStep:
-    """``GraphedStep(step_fn, zero_grad=opt.zero_grad)``: ``step_fn()`` runs one training step and
+    """``GraphedStep(step_fn, zero_grad=opt.zero_grad, optimizer=opt)``: ``step_fn()`` runs one training step and
     returns the loss tensor.  The first call runs ``warmup`` eager steps on a side stream,
     captures one step and replays it (``warmup + 1`` training steps); every later call replays
     it once.  Returns the (static) loss tensor of the step just run."""
 
     def __init__(self, step_fn: Callable[[], torch.Tensor], zero_grad: Optional[Callable[..., None]] = None,
-                 warmup: int = 3, device: Optional[torch.device] = None):
+                 warmup: int = 3, device: Optional[torch.device] = None, optimizer=None):
+        if warmup < 1:
+            # the optimizer's lazy state (moments, device step counts) must exist before the
+            # capture, else every replay would re-create it and train as step 1 forever
+            raise ValueError("GraphedStep needs warmup >= 1 (optimizer state is created by the eager steps)")
         self.step_fn = step_fn
+        self.optimizer = optimizer
         self.zero_grad = zero_grad
         self.warmup = warmup
         self.device = device
@@ -54,6 +59,8 @@ class GraphedStep:
                 self._zero()
                 self.step_fn()
         torch.cuda.current_stream(dev).wait_stream(side)
+        if self.optimizer is not None and getattr(self.optimizer, "capturable", None) is False:
+            raise ValueError("GraphedStep: the optimizer must be capturable (e.g. FusedAdamW(capturable=True))")
         self._zero()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="relaxed"):
@@ -63,5 +70,7 @@ class GraphedStep:
     def __call__(self) -> torch.Tensor:
         if self.graph is None:
             self.capture()  # the warmup steps + the captured step are real training steps
+        if self.optimizer is not None and hasattr(self.optimizer, "sync_lr"):
+            self.optimizer.sync_lr()  # lr schedulers: the captured update reads lr from the device
         self.graph.replay()
         return self.loss

@@ -36,6 +36,7 @@ import torch
 
 from .. import _ext
 from .comm import Communicator, Handle, _check_gather
+from .env import FLAGS
 
 __all__ = ["IpcComm", "ipc_available"]
 
@@ -63,12 +64,12 @@ class IpcComm(Communicator):
         if not 2 <= self.world_size <= max_ranks:
             raise IpcError(f"IpcComm: world size {self.world_size} outside 2..{max_ranks} (one node)")
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-        cap = float(capacity_mb if capacity_mb is not None else os.environ.get("XDOT_IPC_MB", "512"))
+        cap = float(capacity_mb if capacity_mb is not None else FLAGS.ipc_mb)
         self.capacity = (int(cap * 2**20) + 255) // 256 * 256
-        t = float(timeout_s if timeout_s is not None else os.environ.get("XDOT_IPC_TIMEOUT_S", "30"))
+        t = float(timeout_s if timeout_s is not None else FLAGS.ipc_timeout_s)
         self.ticks = int(t * khz * 1000) if khz > 0 else int(t * 1e8)
         self.max_wgs = int(max_wgs)
-        w = int(nwg if nwg is not None else os.environ.get("XDOT_IPC_WGS", "128"))
+        w = int(nwg if nwg is not None else FLAGS.ipc_wgs)
         self.nwg = max(1, min(self.max_wgs, w))  # byte ranges = workgroups per collective
         self.epoch = 0
         with torch.cuda.device(self.device):
