@@ -908,7 +908,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_fwd_merge(Tensor(a!) opart, Tensor lpart, Tensor(b!) lrun, int H) -> ()");
   m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
-        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts=[], Tensor? lr_t=None) -> ()");
+        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");

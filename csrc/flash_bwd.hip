@@ -26,24 +26,6 @@
 
 #include <type_traits>
 
-// Compile-time scheduling knobs (A/B'd with scripts/build_variant.sh + scripts/so_ab.sh,
-// profiles/r2_sched_variants.md); -1 disables an iglp hint.
-#ifndef XDOT_A0_AHEAD
-#define XDOT_A0_AHEAD 2   // rows kernel, phase A0: operand reads ahead of the MFMAs (3/4: no gain)
-#endif
-#ifndef XDOT_A0_IGLP
-#define XDOT_A0_IGLP 1    // rows kernel, phase A0: LLVM iglp_opt(1) MFMA/DS interleave (-2 % at N=1)
-#endif
-#ifndef XDOT_COLS_IGLP
-#define XDOT_COLS_IGLP 0  // cols kernel tile body: iglp_opt(0) (-1 %; iglp_opt(1) +0.6 %)
-#endif
-#ifndef XDOT_ROWS_PIN
-#define XDOT_ROWS_PIN 1   // rows kernel, phases A1 / K0: MFMA + VALU order pinned by sched_barrier
-#endif
-#ifndef XDOT_ROWS_PHASE_IGLP
-#define XDOT_ROWS_PHASE_IGLP -1  // rows kernel, phases A1 / K0: iglp_opt hint
-#endif
-
 namespace xdot {
 namespace fa {
 
@@ -80,8 +62,20 @@ __global__ __launch_bounds__(256) void flash_bwd_prep_kernel(BwdArgs a, const vo
 // ---------------------------------------------------------------------------------------
 // grad of the row side.  4 waves x 32 rows; 64-column tiles of Q_cols / V_cols arrive by
 // LDS-DMA into the same ring as the forward's (RowsCfg).
-template <int DT, int D, int WPS = 2, bool PS = false, bool PIPE = false>
-__global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
+//
+// Software-pipelined tile body.  Per 64-column tile the wave runs
+//   A0: Sᵀ/dPᵀ chains of sub-tile 0 (12 MFMAs, operand reads two ahead)
+//   A1 ∥ V0: the chains of sub-tile 1, each MFMA followed by its share of sub-tile 0's
+//            softmax gradient (v_exp, multiply)
+//   K0 ∥ V1: dk += Q·dSᵀ of sub-tile 0, each MFMA followed by a share of sub-tile 1's VALU
+//   K1:      dk of sub-tile 1
+// so nearly all the VALU work issues between this wave's own MFMAs (a plain S/dP -> VALU -> dk
+// body leaves the matrix pipe to the partner wave during the VALU block: 1.5 % slower).
+// Masks never reach the VALU: a masked (or past-T) column seeds its Sᵀ accumulator with -inf
+// (pre-scaled: P = 2^acc = 0; otherwise P = 2^(acc·c2 - lse2) = 0), so masked and unmasked
+// tiles run the same body and only the seeds differ.
+template <int DT, int D, bool PS = false>
+__global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
   constexpr int IMG = CF::IMG, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
@@ -167,23 +161,18 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
   for (int i = 0; i < DB; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[i][r] = 0.f;
-  // PIPE: software-pipelined tile body.  Per 64-column tile the wave runs
-  //   A0: Sᵀ/dPᵀ chains of sub-tile 0 (12 MFMAs, operand reads two ahead)
-  //   A1 ∥ V0: the chains of sub-tile 1, each MFMA followed by its share of sub-tile 0's
-  //            softmax gradient (FMA, v_exp, multiply)
-  //   K0 ∥ V1: dk += Q·dSᵀ of sub-tile 0, each MFMA followed by a share of sub-tile 1's VALU
-  //   K1:      dk of sub-tile 1
-  // so nearly all the VALU work issues between this wave's own MFMAs (the plain body runs
-  // S/dP -> VALU -> dk back to back and leaves the matrix pipe to the partner wave during
-  // the VALU block).  Costs 32 more live accumulator registers.
-  auto pipe_body = [&](auto chkc, const char* qs, const char* vs, uint64_t w) {
-    constexpr bool CHK = decltype(chkc)::value;
+  // seed of sub-tile tt with the masked columns (bits of w, MFMA C/D order) at -inf
+  auto masked_seed = [&](uint64_t w, int tt) {
+    f32x16 sd = sseed;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) sd[r] = NEG_INF;
+    return sd;
+  };
+  auto pipe_body = [&](const char* qs, const char* vs, const f32x16& sd0, const f32x16& sd1) __attribute__((always_inline)) {
     constexpr int NA = 2 * KS, NK = 2 * DB;
-    auto elem = [&](f32x16& sc, const f32x16& dc, int tt, int r) {
-      float x = PS ? sc[r] : __builtin_fmaf(sc[r], c2, -lse2);
-      if constexpr (CHK) {
-        if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
-      }
+    auto elem = [&](f32x16& sc, const f32x16& dc, int r) {
+      const float x = PS ? sc[r] : __builtin_fmaf(sc[r], c2, -lse2);
       float y = fast_exp2(x) * dc[r];  // -dSᵀ (unscaled)
       asm volatile("" : "+v"(y));      // keeps it in this MFMA gap (LLVM would sink it to its use)
       sc[r] = y;
@@ -192,30 +181,20 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     auto opnd = [&](int tt, int i) { return (i & 1) ? row_frag<D>(vs, tt * 32, i >> 1, L) : row_frag<D>(qs, tt * 32, i >> 1, L); };
     f32x16 s0, d0, s1, d1;
     {
-      // A0: operand reads XDOT_A0_AHEAD MFMAs ahead (s1/d1 are not live yet, so the window
-      // can be deeper here than in the later phases)
-      constexpr int AH = XDOT_A0_AHEAD;
+      // A0: operand reads two MFMAs ahead (s1/d1 are not live yet)
       u32x4 ow[NA];
-#pragma unroll
-      for (int i = 0; i < AH && i < NA; ++i) ow[i] = opnd(0, i);
-#if XDOT_A0_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(XDOT_A0_IGLP);
-#endif
+      ow[0] = opnd(0, 0);
+      ow[1] = opnd(0, 1);
+      __builtin_amdgcn_iglp_opt(1);  // MFMA / DS interleave (-2 % at N=1)
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        if (i + AH < NA) ow[i + AH] = opnd(0, i + AH);
+        if (i + 2 < NA) ow[i + 2] = opnd(0, i + 2);
         const int ks = i >> 1;
         if (i & 1) d0 = mfma32<DT>::run(ow[i], df[ks], ks == 0 ? dseed : d0);
-        else s0 = mfma32<DT>::run(ow[i], kf[ks], ks == 0 ? sseed : s0);
-#ifdef XDOT_A0_PIN
-        __builtin_amdgcn_sched_barrier(0);
-#endif
+        else s0 = mfma32<DT>::run(ow[i], kf[ks], ks == 0 ? sd0 : s0);
       }
     }
     {
-#if XDOT_ROWS_PHASE_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(XDOT_ROWS_PHASE_IGLP);
-#endif
       u32x4 o0 = opnd(1, 0), o1 = opnd(1, 1);
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -223,21 +202,16 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         if (i + 2 < NA) o2 = opnd(1, i + 2);
         const int ks = i >> 1;
         if (i & 1) d1 = mfma32<DT>::run(o0, df[ks], ks == 0 ? dseed : d1);
-        else s1 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sseed : s1);
+        else s1 = mfma32<DT>::run(o0, kf[ks], ks == 0 ? sd1 : s1);
 #pragma unroll
-        for (int j = (i * 16) / NA; j < ((i + 1) * 16) / NA; ++j) elem(s0, d0, 0, j);
-#if XDOT_ROWS_PIN
-        __builtin_amdgcn_sched_barrier(0);
-#endif
+        for (int j = (i * 16) / NA; j < ((i + 1) * 16) / NA; ++j) elem(s0, d0, j);
+        __builtin_amdgcn_sched_barrier(0);  // pins the MFMA / VALU issue order
         o0 = o1;
         o1 = o2;
       }
     }
     const u32x4 p00 = acc_to_frag<DT>(s0, 0), p01 = acc_to_frag<DT>(s0, 1);
     {
-#if XDOT_ROWS_PHASE_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(XDOT_ROWS_PHASE_IGLP);
-#endif
       u32x4 t0 = tr_frag<D>(qs, 0, 0, L), t1 = tr_frag<D>(qs, 16, 0, L);
 #pragma unroll
       for (int i = 0; i < NK; ++i) {
@@ -245,10 +219,8 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
         if (i + 2 < NK) t2 = tr_frag<D>(qs, ((i + 2) & 1) * 16, ((i + 2) >> 1) * 32, L);
         dk[i >> 1] = mfma32<DT>::run(t0, (i & 1) ? p01 : p00, dk[i >> 1]);
 #pragma unroll
-        for (int j = (i * 16) / NK; j < ((i + 1) * 16) / NK; ++j) elem(s1, d1, 1, j);
-#if XDOT_ROWS_PIN
+        for (int j = (i * 16) / NK; j < ((i + 1) * 16) / NK; ++j) elem(s1, d1, j);
         __builtin_amdgcn_sched_barrier(0);
-#endif
         t0 = t1;
         t1 = t2;
       }
@@ -268,46 +240,13 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_rows_kernel(BwdArgs a) {
     const char* vs = qs + IMG;
     const int flag = r0 >= a.R ? 1 : (fwg ? staged_flag(qs + CF::OFF_F, wave, kt & 3) : 0);
     const bool tail = (kt + 1) * 64 > a.T;
-    if (PIPE && flag != 1 && r0 < a.R) {
+    if (flag != 1) {
       if (flag == 2 || tail) {
         const uint64_t w = tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
                                      a.T - kt * 64, hf);
-        pipe_body(std::true_type{}, qs, vs, w);
+        pipe_body(qs, vs, masked_seed(w, 0), masked_seed(w, 1));
       } else {
-        pipe_body(std::false_type{}, qs, vs, 0ull);
-      }
-    } else if (flag != 1 && r0 < a.R) {
-      const bool chk = flag == 2 || tail;
-      const uint64_t w = chk ? tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
-                                         a.T - kt * 64, hf)
-                             : 0ull;
-      // one 32-column sub-tile at a time keeps the live score registers at 2 x 16
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        f32x16 s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, 0, L), kf[0], sseed);
-        f32x16 dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, 0, L), df[0], dseed);
-#pragma unroll
-        for (int ks = 1; ks < KS; ++ks) {
-          s = mfma32<DT>::run(row_frag<D>(qs, tt * 32, ks, L), kf[ks], s);
-          dp = mfma32<DT>::run(row_frag<D>(vs, tt * 32, ks, L), df[ks], dp);
-        }
-        if (chk) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float x = PS ? s[r] : __builtin_fmaf(s[r], c2, -lse2);
-            if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) x = NEG_INF;
-            s[r] = fast_exp2(x) * dp[r];  // -dSᵀ (unscaled)
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s[r] = fast_exp2(PS ? s[r] : __builtin_fmaf(s[r], c2, -lse2)) * dp[r];
-        }
-        const u32x4 f0 = acc_to_frag<DT>(s, 0), f1 = acc_to_frag<DT>(s, 1);
-#pragma unroll
-        for (int db = 0; db < DB; ++db) {
-          dk[db] = mfma32<DT>::run(tr_frag<D>(qs, tt * 32, db * 32, L), f0, dk[db]);
-          dk[db] = mfma32<DT>::run(tr_frag<D>(qs, tt * 32 + 16, db * 32, L), f1, dk[db]);
-        }
+        pipe_body(qs, vs, sseed, sseed);
       }
     }
     if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
@@ -530,9 +469,7 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
       flag = __builtin_amdgcn_readfirstlane((f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2));
     }
     if (flag != 1 && c0 < a.T) {
-#if XDOT_COLS_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(XDOT_COLS_IGLP);
-#endif
+      __builtin_amdgcn_iglp_opt(0);  // -1 % (iglp_opt(1): +0.6 %)
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         f32x16 s = mfma32<DT>::run(row_frag<D>(ks, tt * 32, 0, L), qf[0], PS ? lse_seed(ls, tt) : f32x16{});
@@ -623,45 +560,27 @@ static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hi
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
 }
 
-// Ring depth of the column kernel: 2 stages (default) keeps it under the 256-register budget
-// of 2 waves/SIMD at D = 96 (the 3-stage ring spilled 9 VGPRs to scratch inside the tile
-// loop, and every scratch reload's vmcnt drained the DMA prefetch): 4.36 vs 4.62 ms at
-// T = R = 25000, 0.60 vs 0.64 ms at R = 3125 on MI355X.  XDOT_COLS_NBUF=3 restores 3 stages.
-inline int cols_nbuf() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_COLS_NBUF");
-    return (e && e[0] == '3') ? 3 : 2;
-  }();
-  return v;
-}
-
-// Software-pipelined row kernel body (default; XDOT_ROWS_PIPE=0 selects the plain body, read
-// once); see pipe_body.  MI355X, T = R = 25000, D = 96: 2.63 -> 2.59 ms (1.10 PFLOP/s), headline
-// step 8.70 -> 8.63 ms, emulated N=8 rank step 1.460 -> 1.449 ms (3 alternating runs each).
-inline bool rows_pipe() {
+// software-pipelined column kernel (csrc/flash_cols.hip) for pre-scaled D <= 96; XDOT_COLS_PIPE=0
+// selects the plain kernel below (A/B, read once)
+inline bool cols_pipe() {
   static const bool v = [] {
-    const char* e = std::getenv("XDOT_ROWS_PIPE");
+    const char* e = std::getenv("XDOT_COLS_PIPE");
     return !(e && e[0] == '0');
   }();
   return v;
 }
 
+// The plain column kernel runs 2 ring stages: 3 stages spilled 9 VGPRs inside the tile loop at
+// D = 96 (every scratch reload's vmcnt drained the DMA prefetch): 4.36 vs 4.62 ms at T = R =
+// 25000, 0.60 vs 0.64 ms at R = 3125 on MI355X.
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
+  if (D <= 96 && a.prescaled && cols_pipe() && xdot_flash_bwd_cols2_launch(&a, DT, D, st) == 0) return;
   const int ncb = (a.T + 127) / 128;
-  constexpr int LDS = ColsCfg<D>::NBUF * ColsCfg<D>::STAGE;
   constexpr int LDS2 = 2 * ColsCfg<D, 2>::STAGE;
   const dim3 grid(ncb * a.B * a.H);
-  if (a.prescaled) {
-    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1, 0, true>), grid, dim3(256), LDS, st, a);
-    else if (cols_nbuf() == 2) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2, true>), grid, dim3(256), LDS2, st, a);
-    else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 0, true>), grid, dim3(256), LDS, st, a);
-    return;
-  }
-  if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
-  else if (cols_nbuf() == 2)
-    hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), grid, dim3(256), LDS2, st, a);
-  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
+  if (a.prescaled) hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2, true>), grid, dim3(256), LDS2, st, a);
+  else hipLaunchKernelGGL((flash_bwd_cols_kernel<DT, D, 2, 2>), grid, dim3(256), LDS2, st, a);
 }
 
 template <int DT, int D>
@@ -675,15 +594,8 @@ static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   const int nrb = (a.R + 127) / 128;
   constexpr int LDS = RowsCfg<D>::NBUF * RowsCfg<D>::STAGE;
   const dim3 grid(nrb * a.B * a.H * a.nsplit);
-  if (a.prescaled) {
-    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1, true>), grid, dim3(256), LDS, st, a);
-    else if (rows_pipe()) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true, true>), grid, dim3(256), LDS, st, a);
-    else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, true>), grid, dim3(256), LDS, st, a);
-  } else {
-    if (fa_wps() == 1) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
-    else if (rows_pipe()) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2, false, true>), grid, dim3(256), LDS, st, a);
-    else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
-  }
+  if (a.prescaled) hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, true>), grid, dim3(256), LDS, st, a);
+  else hipLaunchKernelGGL((flash_bwd_rows_kernel<DT, D, false>), grid, dim3(256), LDS, st, a);
   if (a.nsplit > 1 && !a.force_partial) launch_rows_sum<DT, D>(a, st);
 }
 

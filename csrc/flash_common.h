@@ -17,16 +17,6 @@
 namespace xdot {
 namespace fa {
 
-// Occupancy variant of the flash kernels (XDOT_FA_WPS = waves per SIMD: 2 -> 256 VGPRs per
-// wave, 1 -> the whole 512-entry register file); read once per process.
-inline int fa_wps() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_FA_WPS");
-    return (e && e[0] == '1') ? 1 : 2;
-  }();
-  return v;
-}
-
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 

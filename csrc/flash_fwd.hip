@@ -28,27 +28,15 @@
 
 #include <type_traits>
 
-// scheduling knobs (A/B: scripts/build_variant.sh + scripts/so_ab.sh, profiles/r2_sched_variants.md)
-#ifndef XDOT_FWD_PIN
-#define XDOT_FWD_PIN 1    // blocks A / B: MFMA + VALU issue order pinned by sched_barrier
-#endif
-#ifndef XDOT_FWD_IGLP
-#define XDOT_FWD_IGLP -1  // blocks A / B: iglp_opt hint (-1: none)
-#endif
-#ifndef XDOT_FWD_MASKLESS
-#define XDOT_FWD_MASKLESS 0  // 1: a mask-less instantiation issues no placeholder DMAs per tile
-#endif
-#ifndef XDOT_FWD_MSUM
-#define XDOT_FWD_MSUM 0   // 1: row sums of P on the matrix pipe (ones · Pᵀ MFMAs) instead of VALU adds
-#endif
-
 namespace xdot {
 namespace fa {
 
-// MK: the launch may carry a packed mask.  MK = false (no mask, XDOT_FWD_MASKLESS) drops the two
-// per-tile mask DMAs instead of issuing placeholders of the same count.
-template <int DT, int D, int WPS = 2, bool PS = false, bool MK = true>
-__global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
+// The launch may carry a packed mask; without one every wave still issues the two per-tile mask
+// DMAs as placeholders (a mask-less instantiation without them measured 5 % slower:
+// profiles/r2_fwd_issue_budget.md).
+template <int DT, int D, bool PS = false>
+__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
+  constexpr bool MK = true;
   using T16 = typename dt_traits<DT>::T;
   using CF = RowsCfg<D>;
   constexpr int IMG = CF::IMG;  // ring of 3 stages (the pipelined loop reads two of them)
@@ -137,13 +125,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) mseed[r] = 0.f;
   float m_seed = 0.f;
-  // MSUM: l accumulates like O, as Σ_t 1 · Pᵀ[t][row] on the matrix pipe (every entry of the
-  // accumulator holds the lane's row sum); the row sums then come from the same bf16 P as O
-  f32x16 lacc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) lacc[r] = 0.f;
-  constexpr uint32_t ONE2 = DT == DT_F16 ? 0x3C003C00u : 0x3F803F80u;
-  const u32x4 ones = {ONE2, ONE2, ONE2, ONE2};
   f32x16 o[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i)
@@ -213,10 +194,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       for (int i = 0; i < DB; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-      if constexpr (XDOT_FWD_MSUM != 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
-      }
       m_run = m_new;
       if constexpr (PS) {
         const float mu = (m_run == NEG_INF) ? 0.f : m_run;
@@ -253,9 +230,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       constexpr int NA = 2 * KS, NB = 4 * DB;
       u32x4 pf[4];
       {
-#if XDOT_FWD_IGLP >= 0
-        __builtin_amdgcn_iglp_opt(XDOT_FWD_IGLP);
-#endif
         u32x4 q0 = row_frag<D>(nxt, 0, 0, L), q1 = row_frag<D>(nxt, (1 / KS) * 32, 1 % KS, L);
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
@@ -268,9 +242,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
             sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
             if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
           }
-#if XDOT_FWD_PIN
           __builtin_amdgcn_sched_barrier(0);
-#endif
           q0 = q1;
           q1 = q2;
         }
@@ -278,9 +250,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
       // ---- block B: P(kt)·V(kt) MFMAs, each followed by its share of the row sums ----
       float ls = 0.f;
       {
-#if XDOT_FWD_IGLP >= 0
-        __builtin_amdgcn_iglp_opt(XDOT_FWD_IGLP);
-#endif
         u32x4 v0 = tr_frag<D>(cur + IMG, 0, 0, L), v1 = tr_frag<D>(cur + IMG, 16, 0, L);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
@@ -288,18 +257,10 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
           u32x4 v2 = v1;
           if (i + 2 < NB) v2 = tr_frag<D>(cur + IMG, ((i + 2) & 3) * 16, ((i + 2) >> 2) * 32, L);
           o[db] = mfma32<DT>::run(v0, pf[k4], o[db]);
-          if constexpr (XDOT_FWD_MSUM != 0) {
-            // one row-sum MFMA after every DB-th PV MFMA: its chain stays DB MFMAs apart
-            if ((i + 1) % DB == 0) lacc = mfma32<DT>::run(ones, pf[(i + 1) / DB - 1], lacc);
-          } else {
 #pragma unroll
-            for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
-            asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
-          }
-
-#if XDOT_FWD_PIN
+          for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
+          asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
           __builtin_amdgcn_sched_barrier(0);
-#endif
           v0 = v1;
           v1 = v2;
         }
@@ -350,7 +311,7 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
   }
 
   // ---- epilogue ----
-  const float l_tot = XDOT_FWD_MSUM != 0 ? lacc[0] : pair_sum(l_run);
+  const float l_tot = pair_sum(l_run);
   const float inv = 1.f / l_tot;
   if (row_ok && a.nsplit == 1 && !a.force_partial) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
@@ -375,222 +336,6 @@ __global__ __launch_bounds__(256, WPS) void flash_fwd_kernel(FwdArgs a) {
         *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
       }
     if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// 64 rows per wave (two 32-row sub-blocks u = 0, 1): every Q_cols / V_cols operand fragment
-// read from LDS feeds two MFMAs and every staged tile serves 256 rows, which halves both the
-// LDS read traffic and the HBM->LDS DMA traffic per FLOP of the 32-row kernel above.  Not
-// software-pipelined (the two sub-blocks already give the scheduler two independent chains).
-// Ring of 3 stages = {Q(t), V(t), mask words of 256 rows, flags of 8 row blocks}.
-template <int D> struct Fwd64Cfg {
-  static constexpr int IMG = Img<D>::BYTES;
-  static constexpr int OFF_W = 2 * IMG, OFF_F = OFF_W + 256 * 8, OFF_X = OFF_F + 256;
-  static constexpr int STAGE = OFF_X + 256;
-  static constexpr int NG = 2 * ImgDma<D>::IPW + 3;  // DMAs per wave per tile: images, 2 word pieces, flags
-};
-
-template <int DT, int D>
-__global__ __launch_bounds__(256, 2) void flash_fwd64_kernel(FwdArgs a) {
-  using T16 = typename dt_traits<DT>::T;
-  using CF = Fwd64Cfg<D>;
-  constexpr int IMG = CF::IMG, NG = CF::NG, NBUF = 3, PF = 2;
-  constexpr int KS = D / 16, DB = D / 32;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Lanes L = make_lanes<D>(lane);
-  const int nrb = (a.R + 255) / 256;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb = lin % nrb, bhs = lin / nrb;
-  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
-  const int b = bh / a.H, h = bh % a.H;
-  const int C = a.H * D;
-  const int NKT = (a.T + 63) / 64;
-  const int kt_beg = (int)((int64_t)sp * NKT / a.nsplit), kt_end = (int)((int64_t)(sp + 1) * NKT / a.nsplit);
-  const int r0 = rb * 256 + wave * 64;  // sub-block u covers rows r0 + 32u ..
-  const bool sub_ok[2] = {r0 < a.R, r0 + 32 < a.R};
-
-  u32x4 kf[2][KS];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = r0 + 32 * u + (lane & 31);
-    const T16* p = reinterpret_cast<const T16*>(a.rows) + ((int64_t)b * a.R + row) * C + h * D + 8 * hf;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) kf[u][s] = row < a.R ? *reinterpret_cast<const u32x4*>(p + 16 * s) : u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(kf[u][s]));  // retire before the first DMA
-  }
-
-  const int ldb = a.ldkv * 2;
-  ImgDma<D> dma;
-  dma.init(wave, lane, ldb);
-  const char* kcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.kc) + h * D + (int64_t)b * a.T * a.ldkv);
-  const char* vcb = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.vc) + h * D + (int64_t)b * a.T * a.ldkv);
-  const int NKT4 = (NKT + 3) & ~3;
-  const int NRB32 = (a.R + 31) / 32;
-  const uint64_t* mwg = a.mbits ? a.mbits + (int64_t)b * NKT * a.R + rb * 256 : nullptr;  // + kt * R per tile
-  const uint8_t* fwg = a.mflags ? a.mflags + ((int64_t)b * NRB32 + rb * 8) * NKT4 : nullptr;
-  const int nfr = min(8, NRB32 - rb * 8);
-  // words: [dword][256 rows]; wave w moves rows 64w + lane, both dwords (2 DMAs)
-  const uint32_t moff = (uint32_t)(min(wave * 64 + lane, a.R - 1 - rb * 256) * 8);
-  auto issue = [&](int kt) {
-    char* st = smem + ((kt - kt_beg) % NBUF) * CF::STAGE;
-    const int64_t t0 = (int64_t)kt * 64;
-    const int rmax = a.T - 1 - (int)t0;  // columns past T re-read column T-1 (masked in compute)
-    dma.issue(kcb + t0 * ldb, ldb, rmax, st, wave);
-    dma.issue(vcb + t0 * ldb, ldb, rmax, st + IMG, wave);
-    if (mwg) {
-      glds4(mwg + (int64_t)kt * a.R, moff, st + CF::OFF_W + wave * 256);
-      glds4(mwg + (int64_t)kt * a.R, moff + 4, st + CF::OFF_W + 1024 + wave * 256);
-      glds_flags(fwg, NKT4, nfr, kt >> 2, st + CF::OFF_F);
-    } else {  // same DMA count with or without a mask
-      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
-      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
-      glds4(kcb, (uint32_t)lane * 4, st + CF::OFF_X);
-    }
-  };
-
-  const float c2 = a.scale * LOG2E;
-  const float NEG_INF = -__builtin_inff();
-  constexpr float RESCALE_LOG2 = 8.f;  // deferred max (see flash_fwd_kernel)
-  float m_run[2] = {NEG_INF, NEG_INF}, l_run[2] = {0.f, 0.f};
-  f32x16 o[2][DB];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int i = 0; i < DB; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[u][i][r] = 0.f;
-
-  auto tile = [&](auto bufc, int kt) {
-    constexpr int BUF = decltype(bufc)::value;
-    if (kt + PF < kt_end) issue(kt + PF);
-    const char* qs = smem + BUF * CF::STAGE;
-    const char* vs = qs + IMG;
-    int fl[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      fl[u] = !sub_ok[u] ? 1 : (fwg ? staged_flag(qs + CF::OFF_F, 2 * wave + u, kt & 3) : 0);
-    if (fl[0] != 1 || fl[1] != 1) {
-      // ---- Sᵀ for both sub-blocks: one Q fragment read, two MFMAs ----
-      f32x16 s[2][2];
-      {
-        u32x4 qa = row_frag<D>(qs, 0, 0, L);
-#pragma unroll
-        for (int i = 0; i < 2 * KS; ++i) {
-          const int tt = i / KS, ks = i % KS;
-          u32x4 qn = qa;
-          if (i + 1 < 2 * KS) qn = row_frag<D>(qs, ((i + 1) / KS) * 32, (i + 1) % KS, L);
-#pragma unroll
-          for (int u = 0; u < 2; ++u) s[u][tt] = mfma32<DT>::run(qa, kf[u][ks], ks == 0 ? f32x16{} : s[u][tt]);
-          qa = qn;
-        }
-      }
-      const bool tail = (kt + 1) * 64 > a.T;
-      u32x4 pf[2][4];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (fl[u] != 0 || tail) {
-          const uint64_t w = tile_bits(fl[u] == 2 ? staged_word<256>(qs + CF::OFF_W, wave * 64 + 32 * u + (lane & 31)) : 0ull,
-                                       fl[u] == 1 ? 0 : a.T - kt * 64, hf);
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) s[u][tt][r] = NEG_INF;
-        }
-        float mx = NEG_INF;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[u][tt][r]);
-        mx = pair_max(mx) * c2;
-        const float m_new = fmaxf(m_run[u], mx);
-        if (__any(m_new > m_run[u] + RESCALE_LOG2)) {
-          const float alpha = fast_exp2(m_run[u] - ((m_new == NEG_INF) ? 0.f : m_new));
-          l_run[u] *= alpha;
-#pragma unroll
-          for (int i = 0; i < DB; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[u][i][r] *= alpha;
-          m_run[u] = m_new;
-        }
-        const float m_use = (m_run[u] == NEG_INF) ? 0.f : m_run[u];
-        float ls = 0.f;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = fast_exp2(__builtin_fmaf(s[u][tt][r], c2, -m_use));
-            s[u][tt][r] = p;
-            ls += p;
-          }
-#pragma unroll
-          for (int sh = 0; sh < 2; ++sh) pf[u][tt * 2 + sh] = acc_to_frag<DT>(s[u][tt], sh);
-        }
-        l_run[u] += ls;
-      }
-      // ---- Oᵀ += V_colsᵀ · Pᵀ for both sub-blocks: one V fragment read, two MFMAs ----
-      u32x4 va = tr_frag<D>(vs, 0, 0, L);
-#pragma unroll
-      for (int i = 0; i < 4 * DB; ++i) {
-        const int db = i >> 2, k4 = i & 3;
-        u32x4 vn = va;
-        if (i + 1 < 4 * DB) vn = tr_frag<D>(vs, ((i + 1) & 3) * 16, ((i + 1) >> 2) * 32, L);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) o[u][db] = mfma32<DT>::run(va, pf[u][k4], o[u][db]);
-        va = vn;
-      }
-    }
-    if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
-    else wait_vm<0>();
-    raw_barrier();
-  };
-
-#pragma unroll
-  for (int t = 0; t < PF; ++t)
-    if (kt_beg + t < kt_end) issue(kt_beg + t);
-  if (kt_beg + 1 < kt_end) wait_vm<NG * (PF - 1)>();
-  else wait_vm<0>();
-  raw_barrier();
-  for (int kt = kt_beg; kt < kt_end; kt += NBUF) {
-    tile(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < kt_end) tile(std::integral_constant<int, 1>{}, kt + 1);
-    if (kt + 2 < kt_end) tile(std::integral_constant<int, 2>{}, kt + 2);
-  }
-
-  // ---- epilogue (per sub-block, as flash_fwd_kernel) ----
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = r0 + 32 * u + (lane & 31);
-    const float l_tot = pair_sum(l_run[u]);
-    const float inv = 1.f / l_tot;
-    if (row < a.R && a.nsplit == 1 && !a.force_partial) {
-      T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
-#pragma unroll
-      for (int db = 0; db < DB; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u32x2 w;
-          w[0] = pack2<DT>(o[u][db][4 * g + 0] * inv, o[u][db][4 * g + 1] * inv);
-          w[1] = pack2<DT>(o[u][db][4 * g + 2] * inv, o[u][db][4 * g + 3] * inv);
-          *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = w;
-        }
-      if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run[u] + __log2f(l_tot)) * LN2;
-    } else if (row < a.R) {
-      float* op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
-#pragma unroll
-      for (int db = 0; db < DB; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 v = {o[u][db][4 * g] * inv, o[u][db][4 * g + 1] * inv, o[u][db][4 * g + 2] * inv, o[u][db][4 * g + 3] * inv};
-          *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
-        }
-      if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = (m_run[u] + __log2f(l_tot)) * LN2;
-    }
   }
 }
 
@@ -645,37 +390,16 @@ static void launch_combine(const FwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((flash_fwd_combine<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
 }
 
-// rows per wave of the forward kernel: 32 (flash_fwd_kernel, default) or 64
-// (flash_fwd64_kernel, XDOT_FWD_ROWS=64; read once per process).  Measured on MI355X at the
-// headline shapes: 64 rows/wave is 2 % faster at R = 25000 but 6 % slower at R = 3125 (256-row
-// blocks leave more of the last block empty), so the 32-row pipelined kernel is the default.
-inline int fwd_rows_per_wave() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_FWD_ROWS");
-    return (e && e[0] == '6') ? 64 : 32;
-  }();
-  return v;
-}
-
+// 32 rows per wave: a 64-row-per-wave variant (two sub-blocks sharing every operand read)
+// measured 2 % faster at R = 25000 and 6 % slower at R = 3125 (256-row blocks leave more of
+// the last block empty), so the pipelined 32-row kernel is the one kept.
 template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
-  if (fwd_rows_per_wave() == 64 && !a.prescaled) {  // the 64-row kernel has no pre-scaled form
-    constexpr int LDS = 3 * Fwd64Cfg<D>::STAGE;
-    const int nrb = (a.R + 255) / 256;
-    hipLaunchKernelGGL((flash_fwd64_kernel<DT, D>), dim3(nrb * a.B * a.H * a.nsplit), dim3(256), LDS, st, a);
-  } else {
-    constexpr int LDS = 3 * RowsCfg<D>::STAGE;
-    const int nrb = (a.R + 127) / 128;
-    const dim3 grid(nrb * a.B * a.H * a.nsplit);
-    if (a.prescaled) {
-      if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1, true>), grid, dim3(256), LDS, st, a);
-      else if (XDOT_FWD_MASKLESS && !a.mbits && !a.mflags) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2, true, false>), grid, dim3(256), LDS, st, a);
-      else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2, true>), grid, dim3(256), LDS, st, a);
-    } else {
-      if (fa_wps() == 1) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 1>), grid, dim3(256), LDS, st, a);
-      else hipLaunchKernelGGL((flash_fwd_kernel<DT, D, 2>), grid, dim3(256), LDS, st, a);
-    }
-  }
+  constexpr int LDS = 3 * RowsCfg<D>::STAGE;
+  const int nrb = (a.R + 127) / 128;
+  const dim3 grid(nrb * a.B * a.H * a.nsplit);
+  if (a.prescaled) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, true>), grid, dim3(256), LDS, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), grid, dim3(256), LDS, st, a);
   if (a.nsplit > 1 && !a.force_partial) launch_combine<DT, D>(a, st);
 }
 
@@ -683,7 +407,7 @@ static void launch_fwd(const FwdArgs& a, hipStream_t st) {
 }  // namespace xdot
 
 // rows per workgroup of the forward kernel (grid / split planning on the host)
-extern "C" int xdot_flash_fwd_rows_per_wg() { return 4 * xdot::fa::fwd_rows_per_wave(); }
+extern "C" int xdot_flash_fwd_rows_per_wg() { return 128; }
 
 // merge a->nsplit partial slots of opart/lpart into out/lse
 extern "C" int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st) {

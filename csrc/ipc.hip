@@ -44,20 +44,35 @@ __device__ inline void st_flag(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// thread 0 spins until *p >= want (or the budget expires: error word set, returns)
-__device__ inline void wait_ge(const uint32_t* p, uint32_t want, const Args& a) {
+// thread 0 spins until *p >= want (or the budget expires: error word set); returns true for
+// every thread of the workgroup when the wait EXPIRED (the caller then poisons its output
+// range with NaN instead of reading the peer's stale bytes)
+__device__ inline bool wait_ge(const uint32_t* p, uint32_t want, const Args& a) {
+  __shared__ int expired;
   if (threadIdx.x == 0) {
+    int ex = 0;
     const uint64_t t0 = wall_clock64();
     while ((int32_t)(ld_flag(p) - want) < 0) {
       if ((int64_t)(wall_clock64() - t0) > a.timeout_ticks) {
         st_flag(a.status, 1u);
+        ex = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    expired = ex;
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  const bool ex = expired != 0;
+  __syncthreads();  // `expired` is reused by the next wait
+  return ex;
+}
+
+// dst[v] = all-ones (NaN in fp32 / bf16 / fp16) for 16-byte units v in [v0, v1)
+__device__ inline void poison_units(char* dst, int64_t v0, int64_t v1) {
+  u32x4_ua* d = reinterpret_cast<u32x4_ua*>(dst);
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) d[v] = u32x4{~0u, ~0u, ~0u, ~0u};
 }
 
 // publish: this workgroup's stores are in memory before the flag lands at the peer
@@ -95,7 +110,8 @@ __global__ __launch_bounds__(256) void all_gather_kernel(Args a) {
   uint32_t* done = a.sig[a.rank] + MAXR * MAXG;
   int64_t v0, v1;
   range_of(a, w, v0, v1);
-  // 1. our slot is free once every peer finished reading it two collectives ago
+  // 1. our slot is free once every peer finished reading it two collectives ago (an expired
+  //    wait here only delays the peer that stopped; the error word is set)
   if (a.epoch > 2)
     for (int p = 0; p < a.n; ++p)
       if (p != a.rank) wait_ge(done + p * MAXG + w, (uint32_t)(a.epoch - 2), a);
@@ -105,10 +121,13 @@ __global__ __launch_bounds__(256) void all_gather_kernel(Args a) {
   release_all();
   if (threadIdx.x < a.n && threadIdx.x != a.rank)
     st_flag(a.sig[threadIdx.x] + a.rank * MAXG + w, (uint32_t)a.epoch);
-  // 3. pull range w of every peer
+  // 3. pull range w of every peer (NaN if the peer never arrived)
   for (int q = 0; q < a.n - 1; ++q) {
     const int p = peer_at(a, w, q);
-    wait_ge(arrive + p * MAXG + w, (uint32_t)a.epoch, a);
+    if (wait_ge(arrive + p * MAXG + w, (uint32_t)a.epoch, a)) {
+      poison_units(a.out + p * a.shard, v0, v1);
+      continue;
+    }
     copy_units(a.out + p * a.shard, a.stage[p], v0, v1);
     release_all();  // the loads have returned (their data is stored) before the peer may refill
     if (threadIdx.x == 0) st_flag(a.sig[p] + MAXR * MAXG + a.rank * MAXG + w, (uint32_t)a.epoch);
@@ -159,10 +178,15 @@ __global__ __launch_bounds__(256) void reduce_scatter_kernel(Args a) {
   release_all();
   if (threadIdx.x < a.n && threadIdx.x != a.rank)
     st_flag(a.sig[threadIdx.x] + a.rank * MAXG + w, (uint32_t)a.epoch);
-  for (int q = 0; q < a.n - 1; ++q) wait_ge(arrive + peer_at(a, w, q) * MAXG + w, (uint32_t)a.epoch, a);
+  bool lost = false;
+  for (int q = 0; q < a.n - 1; ++q) lost |= wait_ge(arrive + peer_at(a, w, q) * MAXG + w, (uint32_t)a.epoch, a);
   // fixed summation order 0..N-1 on every rank (deterministic, fp32)
   const u32x4_ua* own = reinterpret_cast<const u32x4_ua*>(a.src + a.rank * a.shard);
   u32x4_ua* o = reinterpret_cast<u32x4_ua*>(a.out);
+  if (lost) {  // a peer's partial is missing: the whole range is invalid
+    poison_units(a.out, v0, v1);
+    v1 = v0;
+  }
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < a.n; ++p) {

@@ -144,12 +144,14 @@ int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const void* out, flo
 // gathered-side grads; a->delta must hold δ
 int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
+// software-pipelined column kernel (csrc/flash_cols.hip): pre-scaled 16-bit, D <= 96; -1 = not taken
+int xdot_flash_bwd_cols2_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 // out (n elements, dtype dto) = Σ_s part[s] (fp32 partials, n % 4 == 0)
 int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int dto, hipStream_t st);
 // out = (16-bit) (x * (scale * log2 e)) elementwise, n % 8 == 0: the pre-scaled row side of the
 // flash kernels (the factor is formed in fp32 exactly as the kernels form it)
 int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, int dt, hipStream_t st);
-// rows per workgroup of the forward kernel (depends on XDOT_FWD_ROWS)
+// rows per workgroup of the forward kernel (128)
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
 int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);

@@ -141,8 +141,11 @@ def _timeout_case(rank, ws):
     torch.cuda.synchronize()
     comm.check()
     if rank == 0:  # rank 1 never joins this one: every wait of rank 0 expires, the grid drains
+        out.zero_()
         comm.all_gather_into(out, x)
         torch.cuda.synchronize()
+        # the missing peer's block is NaN (never stale or zero), our own block is intact
+        assert torch.isnan(out[1].float()).all() and torch.equal(out[0], x)
         with pytest.raises(IpcError):
             comm.check()
     C.get_comm().barrier()
@@ -150,3 +153,38 @@ def _timeout_case(rank, ws):
 
 def test_ipc_peer_timeout_raises(gpu):
     run_gloo(_timeout_case, 2, timeout=120)
+
+
+def _async_case(rank, ws):
+    """async_op=True returns before the pull completes: the kernel runs on the communication
+    stream, the handle's event is pending while the peer has not arrived, and wait() orders
+    the caller's stream after it (the data is then exact)."""
+    import time
+
+    import xdot.utils.comm as C
+    from xdot.utils.ipc import IpcComm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = IpcComm(C.get_comm(), capacity_mb=8, timeout_s=60)
+    x = torch.full((8192,), float(rank + 1), dtype=torch.bfloat16, device=dev)
+    out = torch.empty(ws, 8192, dtype=torch.bfloat16, device=dev)
+    C.get_comm().barrier()
+    if rank == 1:
+        time.sleep(3.0)  # rank 0's kernel must still be waiting for us
+    h = comm.all_gather_into(out, x, async_op=True)
+    if rank == 0:
+        time.sleep(0.5)
+        assert not h._work.is_completed(), "the pull finished before the peer arrived"
+        # the caller's stream is free meanwhile: this runs while the pull kernel waits
+        y = (x.float() * 2).sum()
+        torch.cuda.current_stream().synchronize()
+        assert float(y) == 2.0 * 8192
+    got = h.wait()
+    torch.cuda.synchronize()
+    assert got is out and torch.equal(out[0], torch.full_like(x, 1.0)) and torch.equal(out[1], torch.full_like(x, 2.0))
+    comm.close()
+
+
+def test_ipc_async_handle_overlaps(gpu):
+    run_gloo(_async_case, 2, timeout=120)

@@ -170,3 +170,15 @@ def test_packaging_metadata():
     src = open(os.path.join(root, "setup.py")).read()
     assert '"_C.so"' in src and "build_py" in src
     assert os.path.exists(os.path.join(root, "pyproject.toml"))
+
+
+def test_extension_schema_loads_on_cpu():
+    """The built xdot/_C.so registers its op schemas at load time (no GPU needed): a schema
+    error aborts the process, so load it in a subprocess and expect a clean exit."""
+    so = os.path.join(ROOT, "xdot", "_C.so")
+    if not os.path.exists(so):
+        pytest.skip("xdot/_C.so not built")
+    p = subprocess.run([sys.executable, "-c", f"import torch; torch.ops.load_library({so!r}); "
+                        "print(len([n for n in dir(torch.ops.xdot) if not n.startswith('_')]))"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]

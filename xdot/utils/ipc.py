@@ -19,9 +19,15 @@ beyond the staging capacity, CPU tensors) goes to the wrapped communicator.  Tho
 depend only on shapes and dtypes, so every rank takes the same route.
 
 Synchronisation is device-side (per (peer, byte-range) epoch flags in uncached signal pages);
-the host never blocks.  Every device wait is bounded (``XDOT_IPC_TIMEOUT_S``, default 30 s):
-a rank that stops participating makes its peers' kernels drain, set a host-mapped error word,
-and the next collective on the host raises instead of hanging the GPU.
+the host never blocks.  The pull kernels run on a dedicated high-priority communication
+stream (ordered after the caller's stream for their inputs) and ``async_op=True`` returns an
+event-backed :class:`~xdot.utils.comm.Handle`: the caller's stream keeps computing (e.g. the
+attention's local block) while the pull runs, and ``Handle.wait()`` orders it after the kernel.
+Every device wait is bounded (``XDOT_IPC_TIMEOUT_S``, default: the process-group timeout
+``XDOT_COMM_TIMEOUT_S``, 600 s, so a peer busy with host work such as checkpointing is not
+mistaken for a dead one): on expiry the kernel writes NaN over the output range that peer
+should have supplied (the result is unusable, never silently stale), sets a host-mapped error
+word and drains; the host raises at the next collective (and ``Handle.wait()`` checks too).
 
 Enable with ``XDOT_IPC=1`` (``xdot.utils.comm.init`` wraps its RCCL communicator) or build one
 explicitly: ``IpcComm(comm)``.  The staging buffers hold ``XDOT_IPC_MB`` MiB per slot (two
@@ -49,6 +55,21 @@ class IpcError(RuntimeError):
     pass
 
 
+class _EventWork:
+    """``wait()`` orders the caller's current stream after a recorded event (device-side)."""
+
+    __slots__ = ("ev",)
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+
 class IpcComm(Communicator):
     """Pull-based all-gather / reduce-scatter over IPC-mapped peer memory; the rest delegates
     to ``base`` (which also exchanges the IPC handles)."""
@@ -72,6 +93,7 @@ class IpcComm(Communicator):
         w = int(nwg if nwg is not None else FLAGS.ipc_wgs)
         self.nwg = max(1, min(self.max_wgs, w))  # byte ranges = workgroups per collective
         self.epoch = 0
+        self._stream = None  # high-priority communication stream (created on first use)
         with torch.cuda.device(self.device):
             self._stage = ops.ipc_alloc(2 * self.capacity, False)
             self._sig = ops.ipc_alloc(int(sig_bytes), True)
@@ -121,20 +143,40 @@ class IpcComm(Communicator):
         off = (self.epoch & 1) * self.capacity
         return [p + off for p in self.stage_ptrs]
 
+    def _launch(self, fn, out, tensors, async_op):
+        """Run ``fn()`` (one pull kernel) on the communication stream, ordered after the
+        caller's stream; returns an event-backed Handle (async) or orders the caller's stream
+        after the kernel (sync; the host never blocks either way)."""
+        cur = torch.cuda.current_stream(self.device)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=self.device, priority=-1)
+        cs = self._stream
+        cs.wait_stream(cur)
+        with torch.cuda.stream(cs):
+            fn()
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        for t in tensors:  # the caching allocator must not recycle them while the kernel runs
+            t.record_stream(cs)
+        if async_op:
+            return Handle(work=_EventWork(ev), out=out, post=self.check)
+        cur.wait_event(ev)
+        return None
+
     # -- pull collectives ---------------------------------------------------------------
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
         nb = inp.numel() * inp.element_size()
         if not (self._pullable(out, inp, stage_bytes=nb) and nb % 16 == 0):
             return self.base.all_gather_into(out, inp, async_op)
-        o = out if out.is_contiguous() else torch.empty_like(out, memory_format=torch.contiguous_format)
+        if not out.is_contiguous():  # same on every rank (layout follows the shapes)
+            return self.base.all_gather_into(out, inp, async_op)
         i = inp.contiguous()
         stage = self._next()
-        torch.ops.xdot.ipc_all_gather(i, o.view(-1), stage, self.sig_ptrs, self._status, self.rank, self.epoch,
-                                      self.ticks, self._wgs(nb))
-        if o is not out:
-            out.copy_(o)
-        return Handle(out=out) if async_op else None
+        ep, wgs = self.epoch, self._wgs(nb)
+        return self._launch(lambda: torch.ops.xdot.ipc_all_gather(i, out.view(-1), stage, self.sig_ptrs, self._status,
+                                                                  self.rank, ep, self.ticks, wgs),
+                            out, (i, out), async_op)
 
     def reduce_scatter(self, out, inp, async_op=False):
         if inp.numel() != out.numel() * self.world_size:
@@ -144,14 +186,14 @@ class IpcComm(Communicator):
               and nb % 16 == 0 and self._pullable(out, inp, stage_bytes=nb * self.world_size))
         if not ok:
             return self.base.reduce_scatter(out, inp, async_op)
-        o = out if out.is_contiguous() else torch.empty_like(out, memory_format=torch.contiguous_format)
+        if not out.is_contiguous():
+            return self.base.reduce_scatter(out, inp, async_op)
         i = inp.contiguous()
         stage = self._next()
-        torch.ops.xdot.ipc_reduce_scatter(i, o.view(-1), stage, self.sig_ptrs, self._status, self.rank, self.epoch,
-                                          self.ticks, self._wgs(nb))
-        if o is not out:
-            out.copy_(o)
-        return Handle(out=out) if async_op else None
+        ep, wgs = self.epoch, self._wgs(nb)
+        return self._launch(lambda: torch.ops.xdot.ipc_reduce_scatter(i, out.view(-1), stage, self.sig_ptrs,
+                                                                      self._status, self.rank, ep, self.ticks, wgs),
+                            out, (i, out), async_op)
 
     # -- delegated ----------------------------------------------------------------------
     def all_reduce(self, t, op="sum", async_op=False):
