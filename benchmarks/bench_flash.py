@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="all", choices=["all", "fwd", "bwd_cols", "bwd_rows", "mask"])
     ap.add_argument("--mask", action="store_true", help="pass an all-False (B, R, T) mask")
+    ap.add_argument("--mask-density", type=float, default=0.0,
+                    help="with --mask: fraction of randomly masked entries (0: all-False)")
     ap.add_argument("--nsplit", type=int, default=0)
     ap.add_argument("--no-prescale", action="store_true",
                     help="kernels scale every score (default: pre-scaled rows + seeded accumulators, the module's path)")
@@ -63,7 +65,10 @@ def main():
     qv = torch.randn(B, T, 2 * C, device=dev, dtype=torch.bfloat16, generator=g)
     kc, vc = qv[..., :C], qv[..., C:]
     do = torch.randn(B, R, C, device=dev, dtype=torch.bfloat16, generator=g)
-    mask = torch.zeros(B, R, T, dtype=torch.bool, device=dev) if a.mask else None
+    mask = None
+    if a.mask:
+        mask = torch.rand(B, R, T, device=dev, generator=g) < a.mask_density
+        mask[..., 0] = False
     mk = flash.prepare_mask(mask, B, R, T)
     scale = 1.0 / math.sqrt(D)
     ps = not a.no_prescale

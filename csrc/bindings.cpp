@@ -372,6 +372,20 @@ int pick_split(int64_t blocks, int64_t T, int64_t slots, int64_t req) {
   return best;
 }
 
+// Column splits of the row-side backward kernel.  It runs concurrently with the gathered-side
+// kernel (which has stream priority and owns the GPU while it runs): splitting the row kernel's
+// column sweep until its workgroups are no longer than the column kernel's (36 vs 48 MFMAs per
+// 64-tile step; R/64 tiles per column workgroup) lets it pack into that kernel's tail instead of
+// running a long tail of its own.  Measured at the N = 8 rank shape (R = 3125, T = 25000, one
+// MI355X, cols||rows): 2 splits 0.989, 3: 0.943, 4: 0.911, 6: 0.888 ms (profiles/r3_masked.md).
+int rows_split(int64_t B, int64_t R, int64_t T, int64_t H) {
+  const int64_t nkt = (T + 63) / 64, nrt = (R + 63) / 64;
+  const int base = pick_split(((R + 127) / 128) * B * H, T, 512, 0);
+  int64_t conc = (nkt * 36 + nrt * 48 - 1) / (nrt * 48);
+  conc = std::min<int64_t>(8, std::max<int64_t>(1, std::min<int64_t>(conc, nkt / 8)));
+  return std::max(base, (int)conc);
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
                                              int64_t H, double scale, int64_t nsplit, bool prescaled) {
@@ -639,7 +653,7 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
               "xdot.flash_bwd_rows: delta");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   auto drows = at::empty_like(rows);
-  const int ns = pick_split(((g.R + 127) / 128) * g.B * H, g.T, 512, nsplit);
+  const int ns = nsplit > 0 ? pick_split(1, g.T, 1, nsplit) : rows_split(g.B, g.R, g.T, H);
   at::Tensor dpart;
   if (ns > 1) dpart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
   a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
@@ -656,8 +670,8 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
 // column splits the row-block kernels would use for (R rows, T columns) — the caller sizes the
 // partial buffers with it
 int64_t flash_splits(int64_t B, int64_t R, int64_t T, int64_t H, bool rows_kernel) {
-  const int rpw = rows_kernel ? 128 : xdot_flash_fwd_rows_per_wg();
-  return pick_split(((R + rpw - 1) / rpw) * B * H, T, 512, 0);
+  if (rows_kernel) return rows_split(B, R, T, H);
+  return pick_split(((R + 127) / 128) * B * H, T, 512, 0);
 }
 
 void check_part(const at::Tensor& t, int64_t slots_needed, int64_t per_slot, const char* what) {

@@ -164,12 +164,10 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   // seed of sub-tile tt with the masked columns (bits of w, MFMA C/D order) at -inf
   auto masked_seed = [&](uint64_t w, int tt) {
     f32x16 sd = sseed;
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) sd[r] = NEG_INF;
+    sel_bits16(sd, (uint32_t)(w >> (32 * tt)), NINF_BITS);
     return sd;
   };
-  auto pipe_body = [&](const char* qs, const char* vs, const f32x16& sd0, const f32x16& sd1) __attribute__((always_inline)) {
+  auto pipe_body = [&](const char* qs, const char* vs, const f32x16& sd0, bool masked, uint64_t w) __attribute__((always_inline)) {
     constexpr int NA = 2 * KS, NK = 2 * DB;
     auto elem = [&](f32x16& sc, const f32x16& dc, int r) {
       const float x = PS ? sc[r] : __builtin_fmaf(sc[r], c2, -lse2);
@@ -180,6 +178,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
     // operand i of a sub-tile's interleaved S (even i) / dP (odd i) chains
     auto opnd = [&](int tt, int i) { return (i & 1) ? row_frag<D>(vs, tt * 32, i >> 1, L) : row_frag<D>(qs, tt * 32, i >> 1, L); };
     f32x16 s0, d0, s1, d1;
+    // sub-tile 1's seed, built under A0's MFMAs
+    const f32x16 sd1 = masked ? masked_seed(w, 1) : sseed;
     {
       // A0: operand reads two MFMAs ahead (s1/d1 are not live yet)
       u32x4 ow[NA];
@@ -244,9 +244,9 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
       if (flag == 2 || tail) {
         const uint64_t w = tile_bits(flag == 2 ? staged_word(qs + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
                                      a.T - kt * 64, hf);
-        pipe_body(qs, vs, masked_seed(w, 0), masked_seed(w, 1));
+        pipe_body(qs, vs, masked_seed(w, 0), true, w);
       } else {
-        pipe_body(qs, vs, sseed, sseed);
+        pipe_body(qs, vs, sseed, false, 0ull);
       }
     }
     if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();

@@ -136,9 +136,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
   // accumulator ends at +inf and P = 2^-acc = 0 with no per-element test in the pipelined body
   auto seed_masked = [&](const float* c, int tt, uint32_t hw) {
     f32x16 d = seed(c, tt);
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if ((hw >> (8 * (r >> 2) + (r & 3))) & 1u) d[r] = __builtin_inff();
+    sel_bits16(d, hw, PINF_BITS);
     return d;
   };
 
@@ -170,9 +168,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
         a0 = a1; b0 = b1;
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    // half 1's seeds are built under A0's MFMAs (no barrier between: the mask select VALU fills
+    // A0's gaps instead of stalling A1's first MFMA)
     s1 = masked ? seed_masked(ls, 1, (uint32_t)(cw >> 32)) : seed(ls, 1);
     d1 = seed(dls, 1);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- A1 || E0 ----
     {
       u32x4 a0 = opa(1, 0), b0 = opb(0);

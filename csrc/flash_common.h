@@ -13,6 +13,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <utility>
 
 namespace xdot {
 namespace fa {
@@ -247,6 +248,28 @@ __device__ __forceinline__ uint64_t tile_bits(uint64_t w, int valid, int hf) {
 __device__ __forceinline__ bool bit_at(uint64_t w, int j) {
   return j < 32 ? ((uint32_t)w >> j) & 1u : ((uint32_t)(w >> 32) >> (j - 32)) & 1u;
 }
+
+// Masked-entry select in two VALU ops: (bit B of w) ? y : x with y given as raw bits
+// (v_bfe_i32 -> 0 / -1, v_bfi_b32 -> (m & y) | (~m & x)).  hipcc turns the plain C form into
+// four (shift, compare, v_cndmask, and-or); a 10 % random mask makes EVERY tile partial, so
+// this select runs on every score of every head (profiles/r3_masked.md).
+template <int B>
+__device__ __forceinline__ float sel_bit(uint32_t w, float x, uint32_t ybits) {
+  uint32_t m, r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "n"(B));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(ybits), "v"(__builtin_bit_cast(uint32_t, x)));
+  return __builtin_bit_cast(float, r);
+}
+// d[r] = (bit (r & 3) + 8 (r >> 2) of w) ? y : d[r] for the 16 registers of a 32x32 accumulator
+// (the MFMA C/D row order of one lane half)
+template <int... R>
+__device__ __forceinline__ void sel_bits16_(f32x16& d, uint32_t w, uint32_t ybits, std::integer_sequence<int, R...>) {
+  ((d[R] = sel_bit<(R & 3) + 8 * (R >> 2)>(w, d[R], ybits)), ...);
+}
+__device__ __forceinline__ void sel_bits16(f32x16& d, uint32_t w, uint32_t ybits) {
+  sel_bits16_(d, w, ybits, std::make_integer_sequence<int, 16>{});
+}
+constexpr uint32_t PINF_BITS = 0x7F800000u, NINF_BITS = 0xFF800000u;
 
 // v_exp_f32 directly (exp2f would add a denormal-range fix-up of ~3 VALU ops per call;
 // arguments here are <= 0 and results below 2^-126 are irrelevant to a softmax)

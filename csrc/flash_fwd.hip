@@ -170,11 +170,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     }
     const uint64_t w = tile_bits(flag == 2 ? staged_word(st + CF::OFF_W, wave * 32 + (lane & 31)) : 0ull,
                                  a.T - kt * 64, hf);
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (bit_at(w, tt * 32 + (r & 3) + 8 * (r >> 2))) s[tt][r] = NEG_INF;
+    sel_bits16(s[0], (uint32_t)w, NINF_BITS);
+    sel_bits16(s[1], (uint32_t)(w >> 32), NINF_BITS);
   };
   auto row_max = [&](const f32x16 (&s)[2]) {
     float mx = NEG_INF;
