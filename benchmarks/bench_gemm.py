@@ -1,4 +1,4 @@
-"""GEMM micro-benchmark: xdot.gemm (v1 128x128 / v2 256x256 LDS-DMA, pick with XDOT_GEMM) vs
+"""GEMM micro-benchmark: xdot.gemm (v1 128x128 / v2 256x256 LDS-DMA, pick with --path) vs
 torch.matmul (hipBLASLt) on the distributed-product shapes (nt, all, tn) of the reference's
 T=75000 / D=768 benchmarks.  Prints one JSON line per case."""
 import argparse
@@ -31,13 +31,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cases", default="nt,all,tn,nt_small,all3,tn3")
+    ap.add_argument("--path", default="auto", choices=["auto", "v1", "v2"],
+                    help="xdot kernel: auto (library route for plain large products), v1 128x128, v2 256x256")
     a = ap.parse_args()
     from xdot.ops.gemm import strided_gemm
 
     dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    path = os.environ.get("XDOT_GEMM", "auto")
+    path = a.path
+    pc = {"auto": 0, "v1": 1, "v2": 2}[path]
     for case in a.cases.split(","):
         if case in ("nt", "nt_small"):
             M = N = 75000 if case == "nt" else 25000
@@ -45,7 +48,7 @@ def main():
             A = torch.randn(M, K, device=dev, dtype=dt)
             B = torch.randn(N, K, device=dev, dtype=dt)
             C = torch.empty(M, N, device=dev, dtype=dt)
-            ours = lambda: strided_gemm(A, B, C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N)
+            ours = lambda: strided_gemm(A, B, C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, path=pc)
             ref = lambda: torch.matmul(A, B.t(), out=C)
             flops = 2 * M * N * K
         elif case in ("all", "all3"):
@@ -56,7 +59,7 @@ def main():
             B = torch.randn(n, R, D, device=dev, dtype=dt)
             C = torch.empty(R, D, device=dev, dtype=dt)
             ours = lambda: strided_gemm(A, B, C, M=R, N=D, K=R, nseg=n, lda=T, ldb=D, ldc=D, sAseg=R,
-                                        sBseg=R * D, a_mc=False, b_mc=True)
+                                        sBseg=R * D, a_mc=False, b_mc=True, path=pc)
             Bf = B.view(n * R, D)
             ref = lambda: torch.matmul(A, Bf, out=C)
             flops = 2 * R * D * T
@@ -68,7 +71,7 @@ def main():
             B = torch.randn(R, D, device=dev, dtype=dt)
             C = torch.empty(n, R, D, device=dev, dtype=dt)
             ours = lambda: strided_gemm(A, B, C, M=R, N=D, K=R, nb2=n, lda=T, ldb=D, ldc=D, sA2=R, sC2=R * D,
-                                        a_mc=True, b_mc=True)
+                                        a_mc=True, b_mc=True, path=pc)
             ref = lambda: torch.matmul(A.view(R, n, R).permute(1, 2, 0), B, out=C)
             flops = 2 * n * R * R * D
         else:

@@ -37,17 +37,10 @@ def main():
             x = torch.randn(K, N, device=dev, dtype=torch.bfloat16)
             t_x = timeit(lambda: weight_grad(dy, x))
             t_b = timeit(lambda: torch.mm(dy.t(), x))
-            slab = {}
-            os.environ["XDOT_WGRAD_PATH"] = "128"
-            for S in (0, 8, 16, 32):  # the 128x128 slab path, auto / fixed K splits
-                os.environ["XDOT_WGRAD_SPLITS"] = str(S)
-                slab[f"slab128_S{S or 'auto'}_us"] = round(timeit(lambda: weight_grad(dy, x)), 1)
-            os.environ.pop("XDOT_WGRAD_PATH")
-            os.environ.pop("XDOT_WGRAD_SPLITS")
             ref = dy.float().t() @ x.float()
             err = (weight_grad(dy, x).float() - ref).abs().max().item() / ref.abs().max().item()
             print(json.dumps({"K": K, "M": M, "N": N, "xdot_us": round(t_x, 1), "hipblaslt_us": round(t_b, 1),
-                              "xdot_rel_err": err, **slab}), flush=True)
+                              "xdot_rel_err": err}), flush=True)
 
 
 if __name__ == "__main__":

@@ -64,18 +64,6 @@ int64_t avail_elems(const at::Tensor& t) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// XDOT_GEMM: 0 = auto (default), 1 = always the 128x128 v1 kernel, 2 = v2 whenever legal
-int gemm_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_GEMM");
-    if (!e) return 0;
-    if (e[0] == 'v' && e[1] == '1') return 1;
-    if (e[0] == 'v' && e[1] == '2') return 2;
-    return 0;
-  }();
-  return v;
-}
-
 // XDOT_GEMM_LIB: 1 (default) = plain GEMMs (one uniform batch level, K segments contiguous,
 // output dtype = input dtype) that fill >= 2 rounds of 256x256 tiles go to the library GEMM
 // (at::baddbmm -> hipBLASLt) on in-place strided views; 0 = always the xdot kernels
@@ -190,9 +178,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   c10::DeviceGuard guard(A.device());
   // v2 (256x256 tiles, LDS-DMA, csrc/gemm2.hip) for 16-bit operands whose layout meets its
   // alignment rules and whose output fills 256-wide tiles; split-K when the tiles alone would
-  // leave CUs idle.  XDOT_GEMM=v1|v2 forces a path (v2 still needs the layout rules).
-  // path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call; XDOT_GEMM overrides auto)
-  const int mode = path ? (int)path : gemm_mode();
+  // leave CUs idle.  path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call)
+  const int mode = (int)path;
   if (mode == 0 && gemm_lib() &&
       gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
                    b_mc, alpha, beta))

@@ -171,6 +171,39 @@ __device__ __forceinline__ void glds4(const void* base, uint32_t off, const char
 }
 
 
+// IPW consecutive 1-KiB pieces of one wave (LDS destinations lds, lds + 1 KiB, ...) in ONE asm
+// block: M0 is saved / restored once and stepped with s_add between pieces (per piece 1 SALU + 1
+// wait state instead of 3 SALU + 2 wait states: 12 pieces per forward tile per wave)
+template <int N> struct GldsRun;
+template <> struct GldsRun<1> {
+  static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(o[0]), "s"(lds), "s"(base) : "memory");
+  }
+};
+template <> struct GldsRun<3> {
+  static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "v"(o[2]), "s"(lds), "s"(base) : "memory", "scc");
+  }
+};
+template <> struct GldsRun<5> {
+  static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %7\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %7\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %7\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %7\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %7\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "s"(lds), "s"(base)
+                 : "memory", "scc");
+  }
+};
+
 // Per-lane DMA sources of one 64-row swizzled image, filled by the 4 waves of a workgroup in
 // IPW 1-KiB pieces each: image position p holds chunk ((p % ROW) / 16) ^ ((row >> 2) & 3) of
 // tile row p / ROW (padding positions of D = 64/128 images load chunk 0: any valid address).
@@ -191,14 +224,15 @@ template <int D> struct ImgDma {
   // 32-bit VGPR offset (no per-DMA address arithmetic), rows past rmax (tail tile) re-read
   // row rmax (callers mask them)
   __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int wave) const {
+    uint32_t o[IPW];
     if (rmax >= 63) {
 #pragma unroll
-      for (int i = 0; i < IPW; ++i) glds16(base, (uint32_t)off[i], img + (wave * IPW + i) * 1024);
+      for (int i = 0; i < IPW; ++i) o[i] = (uint32_t)off[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < IPW; ++i)
-        glds16(base, (uint32_t)(off[i] - (row[i] - min(row[i], rmax)) * stride_bytes), img + (wave * IPW + i) * 1024);
+      for (int i = 0; i < IPW; ++i) o[i] = (uint32_t)(off[i] - (row[i] - min(row[i], rmax)) * stride_bytes);
     }
+    GldsRun<IPW>::run(base, o, lds_addr(img + wave * IPW * 1024));
   }
 };
 
@@ -249,10 +283,12 @@ __device__ __forceinline__ bool bit_at(uint64_t w, int j) {
   return j < 32 ? ((uint32_t)w >> j) & 1u : ((uint32_t)(w >> 32) >> (j - 32)) & 1u;
 }
 
-// Masked-entry select in two VALU ops: (bit B of w) ? y : x with y given as raw bits
-// (v_bfe_i32 -> 0 / -1, v_bfi_b32 -> (m & y) | (~m & x)).  hipcc turns the plain C form into
-// four (shift, compare, v_cndmask, and-or); a 10 % random mask makes EVERY tile partial, so
-// this select runs on every score of every head (profiles/r3_masked.md).
+// Masked-entry select: d[r] = (bit (r & 3) + 8 (r >> 2) of w) ? y : d[r] for the 16 registers of
+// a 32x32 accumulator (the MFMA C/D row order of one lane half), y given as raw bits.  Per score
+// v_bfe_i32 (bit -> 0 / -1) + v_bfi_b32 ((m & y) | (~m & x)), one asm statement each (hipcc
+// turns plain C into a compare + v_cndmask form that measured +0.14 ms on the forward with a
+// 10 % random mask; a single asm block over all 16 registers gave intermittently wrong
+// results).  A random mask makes EVERY tile partial, so this runs on every score of every head.
 template <int B>
 __device__ __forceinline__ float sel_bit(uint32_t w, float x, uint32_t ybits) {
   uint32_t m, r;
@@ -260,8 +296,6 @@ __device__ __forceinline__ float sel_bit(uint32_t w, float x, uint32_t ybits) {
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(ybits), "v"(__builtin_bit_cast(uint32_t, x)));
   return __builtin_bit_cast(float, r);
 }
-// d[r] = (bit (r & 3) + 8 (r >> 2) of w) ? y : d[r] for the 16 registers of a 32x32 accumulator
-// (the MFMA C/D row order of one lane half)
 template <int... R>
 __device__ __forceinline__ void sel_bits16_(f32x16& d, uint32_t w, uint32_t ybits, std::integer_sequence<int, R...>) {
   ((d[R] = sel_bit<(R & 3) + 8 * (R >> 2)>(w, d[R], ybits)), ...);

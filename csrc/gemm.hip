@@ -289,11 +289,11 @@ static void launch_t(const GemmArgs& a, int batches, hipStream_t st) {
 
 template <int DTI, int DTO>
 static void launch_d(const GemmArgs& a, int batches, bool amc, bool bmc, bool vec, hipStream_t st) {
-#define XDOT_G(AM, BM_, V) \
+#define G1_CASE(AM, BM_, V) \
   if (amc == AM && bmc == BM_ && vec == V) return launch_t<DTI, DTO, AM, BM_, V>(a, batches, st);
-  XDOT_G(false, false, true) XDOT_G(false, true, true) XDOT_G(true, false, true) XDOT_G(true, true, true)
-  XDOT_G(false, false, false) XDOT_G(false, true, false) XDOT_G(true, false, false) XDOT_G(true, true, false)
-#undef XDOT_G
+  G1_CASE(false, false, true) G1_CASE(false, true, true) G1_CASE(true, false, true) G1_CASE(true, true, true)
+  G1_CASE(false, false, false) G1_CASE(false, true, false) G1_CASE(true, false, false) G1_CASE(true, true, false)
+#undef G1_CASE
 }
 
 }  // namespace xdot
@@ -306,10 +306,10 @@ extern "C" int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in,
   g.tiles_m = (g.M + gemm::BM - 1) / gemm::BM;
   g.tiles_n = (g.N + gemm::BN - 1) / gemm::BN;
   if (g.tiles_m == 0 || g.tiles_n == 0 || batches == 0) return 0;
-#define XDOT_D(I, O) \
+#define G1_DT(I, O) \
   if (dt_in == I && dt_out == O) { launch_d<I, O>(g, batches, a_mc, b_mc, vec, st); return 0; }
-  XDOT_D(DT_BF16, DT_BF16) XDOT_D(DT_BF16, DT_F32) XDOT_D(DT_F16, DT_F16) XDOT_D(DT_F16, DT_F32)
-  XDOT_D(DT_F32, DT_F32) XDOT_D(DT_F32, DT_BF16)
-#undef XDOT_D
+  G1_DT(DT_BF16, DT_BF16) G1_DT(DT_BF16, DT_F32) G1_DT(DT_F16, DT_F16) G1_DT(DT_F16, DT_F32)
+  G1_DT(DT_F32, DT_F32) G1_DT(DT_F32, DT_BF16)
+#undef G1_DT
   return -1;
 }

@@ -466,22 +466,8 @@ inline int num_cus() {
   return v;
 }
 
-inline int gemm2_iss() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_GEMM2_ISS");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
-}
-
-// XDOT_GEMM2_PERSIST_KT: largest k-tile count per item that still runs persistent (default 32)
-inline int gemm2_persist_kt() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_GEMM2_PERSIST_KT");
-    return e ? std::atoi(e) : 32;
-  }();
-  return v;
-}
+// largest k-tile count per item that still runs persistent
+constexpr int GEMM2_PERSIST_KT = 32;
 
 // 4 consecutive columns per thread (N % 4 == 0, ldc % 4 == 0, C 16-byte aligned)
 template <int DTO>
@@ -509,20 +495,15 @@ static void launch2_t(const GemmArgs& a, int batches, int splits, float* ws, hip
   // persistent (one workgroup per CU) when items are short (the per-item prologue/epilogue is
   // then a large share that the ring overlaps); one workgroup per item for long K
   const int kt_item = ((a.K + 63) / 64) * a.nseg / splits;
-  const int G = (W > num_cus() && kt_item <= gemm2_persist_kt()) ? num_cus() : W;
+  const int G = (W > num_cus() && kt_item <= GEMM2_PERSIST_KT) ? num_cus() : W;
   constexpr int LDS = g2::Cfg<64, 2>::LDS + 32768;  // ring + epilogue strips = 160 KiB
   const bool pst = G < W;
-#define XDOT_G2L(ISS, PST, LDSB)                                                                                   \
-  hipLaunchKernelGGL((gemm2_kernel<DTI, DTO, AMC, BMC, ISS, PST>), dim3(G), dim3(g2::NT), LDSB, st, a,          \
+#define G2LAUNCH(PST, LDSB)                                                                                        \
+  hipLaunchKernelGGL((gemm2_kernel<DTI, DTO, AMC, BMC, 1, PST>), dim3(G), dim3(g2::NT), LDSB, st, a,            \
                      splits > 1 ? ws : nullptr, W, batches, splits)
-  if (gemm2_iss() == 1) {
-    if (pst) XDOT_G2L(1, true, LDS);
-    else XDOT_G2L(1, false, LDS - 32768);
-  } else {
-    if (pst) XDOT_G2L(0, true, LDS);
-    else XDOT_G2L(0, false, LDS - 32768);
-  }
-#undef XDOT_G2L
+  if (pst) G2LAUNCH(true, LDS);
+  else G2LAUNCH(false, LDS - 32768);
+#undef G2LAUNCH
   if (splits > 1) {
     const int64_t n = (int64_t)a.M * a.N * batches;
     const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && a.sC1 % 4 == 0 && a.sC2 % 4 == 0 &&
@@ -555,9 +536,9 @@ extern "C" int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in
   g.tiles_n = (g.N + g2::BN - 1) / g2::BN;
   if (g.tiles_m == 0 || g.tiles_n == 0 || batches == 0) return 0;
   if (splits < 1 || (splits > 1 && !ws)) return -2;
-#define XDOT_D2(I, O) \
+#define G2_DT(I, O) \
   if (dt_in == I && dt_out == O) { launch2_d<I, O>(g, batches, a_mc, b_mc, splits, ws, st); return 0; }
-  XDOT_D2(DT_BF16, DT_BF16) XDOT_D2(DT_BF16, DT_F32) XDOT_D2(DT_F16, DT_F16) XDOT_D2(DT_F16, DT_F32)
-#undef XDOT_D2
+  G2_DT(DT_BF16, DT_BF16) G2_DT(DT_BF16, DT_F32) G2_DT(DT_F16, DT_F16) G2_DT(DT_F16, DT_F32)
+#undef G2_DT
   return -1;
 }

@@ -12,9 +12,6 @@
 
 #include <type_traits>
 
-#ifndef XDOT_ADAM_VEC
-#define XDOT_ADAM_VEC 1  // vector loads / stores for full aligned 4-element groups
-#endif
 
 namespace xdot {
 
@@ -46,7 +43,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   // full, aligned 4-element group: one vector load / store per operand (the tensors start at
   // allocator-aligned addresses; the check is wave-uniform per tensor)
   constexpr int PB = 4 * (int)sizeof(TP);
-  if (XDOT_ADAM_VEC && base + 3 < n && ((uintptr_t)p | (uintptr_t)g) % PB == 0 && ((uintptr_t)m | (uintptr_t)v) % 16 == 0) {
+  if (base + 3 < n && ((uintptr_t)p | (uintptr_t)g) % PB == 0 && ((uintptr_t)m | (uintptr_t)v) % 16 == 0) {
     using PV = typename std::conditional<PB == 16, u32x4, u32x2>::type;
     union { PV u; TP e[4]; } pp, gg;
     pp.u = *reinterpret_cast<const PV*>(p + base);

@@ -94,14 +94,14 @@ extern "C" int xdot_mse_fwd_launch(const void* y, const void* t, void* dy, float
   const u32x4* ti = reinterpret_cast<const u32x4*>(t);
   u32x4* o = reinterpret_cast<u32x4*>(dy);
   const float g2 = 2.f / (float)n, inv_n = 1.f / (float)n;
-#define XDOT_MSE(D)                                                                                          \
+#define MSE_CASE(D)                                                                                          \
   hipLaunchKernelGGL(mse_fwd_kernel<D>, dim3(nparts), dim3(256), 0, st, yi, ti, o, part, nv, g2);            \
   hipLaunchKernelGGL(mse_final_kernel<D>, dim3(1), dim3(256), 0, st, part, nparts, loss, inv_n);
-  if (dt == DT_BF16) { XDOT_MSE(DT_BF16) }
-  else if (dt == DT_F16) { XDOT_MSE(DT_F16) }
-  else if (dt == DT_F32) { XDOT_MSE(DT_F32) }
+  if (dt == DT_BF16) { MSE_CASE(DT_BF16) }
+  else if (dt == DT_F16) { MSE_CASE(DT_F16) }
+  else if (dt == DT_F32) { MSE_CASE(DT_F32) }
   else return -1;
-#undef XDOT_MSE
+#undef MSE_CASE
   return 0;
 }
 
