@@ -81,7 +81,6 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
   constexpr int IMG = CF::IMG, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
   constexpr int KS = D / 16, DB = D / 32;
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
   const Lanes L = make_lanes<D>(lane);
@@ -320,7 +319,6 @@ __global__ __launch_bounds__(256, WPS) void flash_bwd_cols_kernel(BwdArgs a) {
   constexpr int ROW = Img<D>::ROW, IMG = CF::IMG, IPW = CF::IPW, NG = CF::NG, PF = CF::PF, NBUF = CF::NBUF;
   constexpr int KS = D / 16, DB = D / 32;
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Lanes L = make_lanes<D>(lane);

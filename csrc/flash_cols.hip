@@ -51,7 +51,6 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
   constexpr int KS = D / 16, DB = D / 32;
   static_assert(D <= 96, "cols2: two workgroups per CU need D <= 96");
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Lanes L = make_lanes<D>(lane);

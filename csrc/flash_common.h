@@ -156,8 +156,12 @@ __device__ __forceinline__ void raw_barrier() {
 // Inline asm on purpose: for the builtin, hipcc inserts `s_waitcnt vmcnt(0)` in front of every
 // ds_read_b64_tr_b16 while any DMA is pending (it cannot prove they do not alias), which
 // would drain the prefetch ring every tile.  The kernel counts these DMAs itself (wait_vm).
+// The dynamic LDS of the flash kernels: ONE symbol for all of them, so LDS-DMA destinations are
+// its LDS address + a byte offset the compiler folds to a constant (converting an arbitrary
+// generic pointer back to an LDS address costs ~8 SALU of null checks per DMA call).
+extern __shared__ __attribute__((aligned(16))) char smem[];
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(const char*)p;
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem + (uint32_t)((const char*)p - smem);
 }
 __device__ __forceinline__ void glds16(const void* base, uint32_t off, const char* lds_wave_base) {
   uint32_t keep;

@@ -322,6 +322,8 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
 
 
 _SIDE = {}
+# diagnostics (A/B of HIP-graph replay): run the fused backward's two halves on the caller's stream
+ONE_STREAM_BACKWARD = False
 
 
 def _side_stream(dev: torch.device, priority: int = -1) -> "torch.cuda.Stream":
@@ -425,7 +427,7 @@ class SeqParallelAttention(torch.autograd.Function):
             cur = torch.cuda.current_stream(do.device)
             # high priority so the gathered side (and its reduce-scatter) finishes early (an
             # ordinary-priority side stream measured slower at N=1 and N=8: profiles/r2_bwd_overlap.md)
-            hi = _side_stream(do.device, -1)
+            hi = cur if ONE_STREAM_BACKWARD else _side_stream(do.device, -1)
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
