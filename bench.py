@@ -250,10 +250,17 @@ def main(argv=None, comm=None):
         check_err = numerics_check(a, comm, dev, dt, a.impl)
     ms, host_ms, lossv, impl = time_step(a, comm, dev, dt, a.steps, a.warmup, graph=a.graph,
                                          profile_dir=a.profile_dir)
-    fp32 = None
+    fp32 = {}
     if a.fp32_steps > 0 and dt != torch.float32 and dev.type == "cuda":
-        # the reference computes in fp32 only (module.py:60-71): time the same step in fp32 too
-        fp32 = time_step(a, comm, dev, torch.float32, a.fp32_steps, a.fp32_warmup)
+        # the reference computes in fp32 only (module.py:60-71): time the same step in fp32 too,
+        # under both fp32 kernel families (XDOT_FP32_MODE: split-bf16 default, exact fp32 MFMA)
+        default_mode = FLAGS.fp32_mode
+        try:
+            for mode in [default_mode] + [m for m in ("split", "exact") if m != default_mode]:
+                FLAGS.fp32_mode = mode
+                fp32[mode] = time_step(a, comm, dev, torch.float32, a.fp32_steps, a.fp32_warmup)
+        finally:
+            FLAGS.fp32_mode = default_mode
     if rank == 0:
         metric = METRIC
         if (T, a.dim, a.heads) != (25000, 768, 8):  # not the headline config: say what was run
@@ -295,9 +302,12 @@ def main(argv=None, comm=None):
             "local_first": bool(FLAGS.local_first),
             "numerics_check_max_rel_err": None if check_err is None else round(check_err, 5),
         }
-        if fp32 is not None:
-            rec["fp32_ms_per_step"] = round(fp32[0], 4)
-            rec["fp32_impl"] = fp32[3]
+        if fp32:
+            first = next(iter(fp32))
+            rec["fp32_ms_per_step"] = round(fp32[first][0], 4)
+            rec["fp32_impl"] = f"{fp32[first][3]}/{first}"
+            for mode, r in fp32.items():
+                rec[f"fp32_{mode}_ms_per_step"] = round(r[0], 4)
             rec["fp32_steps"] = a.fp32_steps
         if emulated:
             link = getattr(comm, "link_gbps", None)

@@ -1,5 +1,6 @@
-"""HIP-graph replay vs eager, with the fused backward on two streams (default) or one
-(``xdot.parallel.attention.ONE_STREAM_BACKWARD``), at N=1 and the emulated N=8 rank shape.
+"""HIP-graph replay vs eager, with the fused backward on the default stream rule (None), forced
+two streams (False) or forced one stream (True) (``xdot.parallel.attention.ONE_STREAM_BACKWARD``),
+at N=1 and emulated per-rank shapes.
 Prints bench.py's JSON lines tagged with the variant.
 
     python benchmarks/graph_ab.py --world 1 8 --steps 10 --warmup 3
@@ -25,7 +26,7 @@ def main():
     from xdot.utils.comm import EmulatedComm
 
     for n in a.world:
-        for one in (False, True):
+        for one in (None, False, True):
             for graph in (False, True):
                 A.ONE_STREAM_BACKWARD = one
                 args = ["--gpus", str(n), "--steps", str(a.steps), "--warmup", str(a.warmup), "--fp32-steps", "0",

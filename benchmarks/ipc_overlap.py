@@ -42,10 +42,10 @@ def main():
         if rank == 1:
             time.sleep(0.02)
         h = comm.all_gather_into(out, qv, async_op=True)
-        e0 = torch.cuda.Event()
+        e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
         o, lse = flash.fwd(rows, qv[..., :C_], qv[..., C_:], None, H, scale)  # own block, no comm needed
-        e1 = torch.cuda.Event()
+        e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         e1.synchronize()
         pending = not h._work.is_completed() if hasattr(h, "_work") else None
@@ -53,8 +53,7 @@ def main():
         torch.cuda.synchronize()
         res.append({"iter": it, "own_block_ms": round(e0.elapsed_time(e1), 3), "gather_pending_after_own_block": pending})
     comm.close()
-    if rank == 0:
-        print(json.dumps({"rank": rank, "results": res}), flush=True)
+    print(json.dumps({"rank": rank, "pid": os.getpid(), "results": res}), flush=True)
     C.destroy()
 
 

@@ -375,7 +375,7 @@ int rows_split(int64_t B, int64_t R, int64_t T, int64_t H) {
 
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
-                                             int64_t H, double scale, int64_t nsplit, bool prescaled) {
+                                             int64_t H, double scale, int64_t nsplit, bool prescaled, int64_t fp32_mode) {
   Range rr_("xdot.flash_fwd");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   auto out = at::empty_like(rows);
@@ -399,6 +399,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   a.opart = ns > 1 ? opart.data_ptr<float>() : nullptr;
   a.lpart = ns > 1 ? lpart.data_ptr<float>() : nullptr;
   a.prescaled = prescaled ? 1 : 0;
+  a.fp32_mode = (int)fp32_mode;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0, "xdot.flash_fwd: config");
   check_launch(hipGetLastError(), "flash_fwd");
@@ -432,13 +433,15 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               const c10::optional<at::Tensor>& flags, int64_t H,
                                                               double scale, const c10::optional<at::Tensor>& delta_in,
                                                               bool fp32_out, bool prescaled,
-                                                              const c10::optional<at::Tensor>& lse2_in) {
+                                                              const c10::optional<at::Tensor>& lse2_in,
+                                                              int64_t fp32_mode) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   a.prescaled = prescaled ? 1 : 0;
+  a.fp32_mode = (int)fp32_mode;
   auto dkv = at::empty({g.B, g.T, 2 * g.C}, fp32_out ? kc.options().dtype(at::kFloat) : kc.options());
   const bool have_delta = delta_in.has_value() && delta_in->defined();
   at::Tensor delta;
@@ -633,7 +636,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_prep(const at::Tensor& dout, const 
 at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                           const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                           const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit,
-                          bool prescaled) {
+                          bool prescaled, int64_t fp32_mode) {
   Range rr_("xdot.flash_bwd_rows");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
@@ -646,6 +649,7 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();
   a.nsplit = ns; a.dpart = ns > 1 ? dpart.data_ptr<float>() : nullptr;
   a.prescaled = prescaled ? 1 : 0;
+  a.fp32_mode = (int)fp32_mode;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows: config");
@@ -671,7 +675,7 @@ void check_part(const at::Tensor& t, int64_t slots_needed, int64_t per_slot, con
 void flash_fwd_partial(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                        const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags, int64_t H,
                        double scale, at::Tensor& opart, at::Tensor& lpart, int64_t sp0, int64_t nsplit,
-                       bool prescaled) {
+                       bool prescaled, int64_t fp32_mode) {
   Range rr_("xdot.flash_fwd_partial");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(sp0 >= 0 && nsplit >= 1, "xdot.flash_fwd_partial: slots");
@@ -688,6 +692,7 @@ void flash_fwd_partial(const at::Tensor& rows, const at::Tensor& kc, const at::T
   a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1;
   a.opart = opart.data_ptr<float>(); a.lpart = lpart.data_ptr<float>();
   a.prescaled = prescaled ? 1 : 0;
+  a.fp32_mode = (int)fp32_mode;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_fwd_partial: config");
@@ -761,7 +766,7 @@ void sum_partials_into(const at::Tensor& part, at::Tensor& out) {
 void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                             const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                             const c10::optional<at::Tensor>& flags, int64_t H, double scale, at::Tensor& dpart,
-                            int64_t sp0, int64_t nsplit, bool prescaled) {
+                            int64_t sp0, int64_t nsplit, bool prescaled, int64_t fp32_mode) {
   Range rr_("xdot.flash_bwd_rows_partial");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
@@ -773,6 +778,7 @@ void flash_bwd_rows_partial(const at::Tensor& dout, const at::Tensor& rows, cons
   a.delta = delta.data_ptr<float>();
   a.nsplit = ns; a.sp0 = (int)sp0; a.force_partial = 1; a.dpart = dpart.data_ptr<float>();
   a.prescaled = prescaled ? 1 : 0;
+  a.fp32_mode = (int)fp32_mode;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows_partial: config");
@@ -892,26 +898,26 @@ TORCH_LIBRARY(xdot, m) {
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
-  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> (Tensor, Tensor)");
+  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False, "
-        "Tensor? lse2=None) -> (Tensor, Tensor)");
+        "Tensor? lse2=None, int fp32_mode=0) -> (Tensor, Tensor)");
   m.def("flash_bwd_prep(Tensor dout, Tensor out, Tensor lse, int H) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
   m.def("flash_splits(int B, int R, int T, int H, bool rows_kernel) -> int");
   m.def("flash_fwd_partial(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, "
-        "Tensor(a!) opart, Tensor(b!) lpart, int sp0, int nsplit, bool prescaled=False) -> ()");
+        "Tensor(a!) opart, Tensor(b!) lpart, int sp0, int nsplit, bool prescaled=False, int fp32_mode=0) -> ()");
   m.def("flash_fwd_combine(Tensor opart, Tensor lpart, int H, Tensor like) -> (Tensor, Tensor)");
   m.def("flash_bwd_rows_partial(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit, bool prescaled=False) -> ()");
+        "Tensor? flags, int H, float scale, Tensor(a!) dpart, int sp0, int nsplit, bool prescaled=False, int fp32_mode=0) -> ()");
   m.def("flash_bwd_rows_sum(Tensor dpart, int H, Tensor like) -> Tensor");
   m.def("flash_fwd_merge(Tensor(a!) opart, Tensor lpart, Tensor(b!) lrun, int H) -> ()");
   m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False) -> Tensor");
+        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
   m.def("ipc_info() -> int[]");

@@ -558,22 +558,14 @@ static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hi
   hipLaunchKernelGGL((flash_bwd_prep_kernel<DT, D>), dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, st, a, out, delta);
 }
 
-// software-pipelined column kernel (csrc/flash_cols.hip) for pre-scaled D <= 96; XDOT_COLS_PIPE=0
-// selects the plain kernel below (A/B, read once)
-inline bool cols_pipe() {
-  static const bool v = [] {
-    const char* e = std::getenv("XDOT_COLS_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
+// Pre-scaled D <= 96 runs the software-pipelined column kernel (csrc/flash_cols.hip: 7 % faster
+// standalone, profiles/r3_cols_pipe.md); D = 128 and non-pre-scaled inputs run the plain kernel below.
 // The plain column kernel runs 2 ring stages: 3 stages spilled 9 VGPRs inside the tile loop at
 // D = 96 (every scratch reload's vmcnt drained the DMA prefetch): 4.36 vs 4.62 ms at T = R =
 // 25000, 0.60 vs 0.64 ms at R = 3125 on MI355X.
 template <int DT, int D>
 static void launch_bwd_cols(const BwdArgs& a, hipStream_t st) {
-  if (D <= 96 && a.prescaled && cols_pipe() && xdot_flash_bwd_cols2_launch(&a, DT, D, st) == 0) return;
+  if (D <= 96 && a.prescaled && xdot_flash_bwd_cols2_launch(&a, DT, D, st) == 0) return;
   const int ncb = (a.T + 127) / 128;
   constexpr int LDS2 = 2 * ColsCfg<D, 2>::STAGE;
   const dim3 grid(ncb * a.B * a.H);
@@ -626,7 +618,7 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
-  if (dt == DT_F32) return xdot_flash_bwd_cols_f32_launch(a, D, st);
+  if (dt == DT_F32) return a->fp32_mode ? xdot_flash_bwd_cols_x3_launch(a, D, st) : xdot_flash_bwd_cols_f32_launch(a, D, st);
 #define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
 #undef XC
@@ -648,7 +640,7 @@ extern "C" int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (dt == DT_F32) {
-    const int rc = xdot_flash_bwd_rows_f32_launch(a, D, st);
+    const int rc = a->fp32_mode ? xdot_flash_bwd_rows_x3_launch(a, D, st) : xdot_flash_bwd_rows_f32_launch(a, D, st);
     if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_rows_sum_f32_launch(a, D, st);
     return rc;
   }

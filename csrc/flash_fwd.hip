@@ -423,7 +423,7 @@ extern "C" int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, 
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
   if (dt == DT_F32) {
-    const int rc = xdot_flash_fwd_f32_launch(a, D, st);
+    const int rc = a->fp32_mode ? xdot_flash_fwd_x3_launch(a, D, st) : xdot_flash_fwd_f32_launch(a, D, st);
     if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_combine_f32_launch(a, D, st);
     return rc;
   }

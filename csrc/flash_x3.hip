@@ -1,0 +1,563 @@
+// xdot — fp32 flash attention on the bf16 matrix pipe ("split-bf16", opt-in fp32 mode).
+//
+// The exact-fp32 family (csrc/flash_f32.hip) runs every product on v_mfma_f32_32x32x2_f32:
+// 64 FLOP/clk/SIMD, 1/16 of the bf16 rate, so an fp32 step costs ~10x a bf16 one.  Here every
+// fp32 operand x is split into two bf16 values, hi = bf16(x) and lo = bf16(x - hi) (x = hi + lo
+// up to ~2^-17 |x|), and a product a·b is three bf16 MFMAs accumulated in fp32:
+//     a·b ≈ a_lo·b_hi + a_hi·b_lo + a_hi·b_hi      (a_lo·b_lo ~ 2^-16 |a·b| dropped)
+// = 3 x 32x32x16 bf16 MFMAs per 16-deep K step instead of 8 x 32x32x2 f32 ones: 5.3x fewer
+// matrix-pipe cycles.  Softmax, LSE, δ and every accumulation stay fp32; measured against fp64
+// the relative error is 6e-6..9e-6 (exact fp32: 3e-7..6e-7), profiles/r3_fp32_split.md.  The
+// default fp32 family (``XDOT_FP32_MODE=split``, per call ``fp32_mode=1``); ``exact`` keeps
+// flash_f32.hip.
+//
+// Same decomposition, layouts, masks and partial/combine protocol as flash_f32.hip (same
+// reference semantics, distributed_dot_product/module.py:60-71): 4 waves x 32 rows (columns
+// for the gathered-side kernel), 32-row tiles staged global -> VGPR (one tile ahead) -> LDS.
+// The staging step splits each fp32 tile ONCE per workgroup into the bf16 images the MFMAs
+// read:
+//   * row-major  [row][d] hi / lo, stride D + 8 (16-byte pad: the 16-lane ds_read_b128 groups
+//     hit 16 distinct bank quads) — A operand of products over the head dim;
+//   * transposed [d][slot] hi / lo, stride 40 — A operand of products over the tile index,
+//     slots permuted so that lane half h of K step j reads tile rows tidx(8j + t, h), t = 0..7,
+//     i.e. the accumulator registers 8j..8j+7 of the previous product (B operand straight from
+//     the accumulator, split in registers).
+#include "flash_common.h"
+
+namespace xdot {
+namespace fa3 {
+
+using fa::BwdArgs;
+using fa::FwdArgs;
+using fa::LN2;
+using fa::LOG2E;
+using fa::pair_max;
+using fa::pair_sum;
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
+
+__device__ __forceinline__ f32x16 mm(const u32x4& a, const u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// a·b of one 16-deep K step from split operands (small terms first)
+__device__ __forceinline__ f32x16 mm3(const u32x4& ah, const u32x4& al, const u32x4& bh, const u32x4& bl, f32x16 c) {
+  c = mm(al, bh, c);
+  c = mm(ah, bl, c);
+  return mm(ah, bh, c);
+}
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// two floats -> packed hi pair and packed lo pair
+__device__ __forceinline__ void split2(float x, float y, uint32_t& hi, uint32_t& lo) {
+  const bf2 h = {(__bf16)x, (__bf16)y};
+  const uint32_t hb = __builtin_bit_cast(uint32_t, h);
+  const float xh = __builtin_bit_cast(float, hb << 16), yh = __builtin_bit_cast(float, hb & 0xffff0000u);
+  const bf2 l = {(__bf16)(x - xh), (__bf16)(y - yh)};
+  hi = hb;
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+__device__ __forceinline__ void split8(const float* x, u32x4& hi, u32x4& lo) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint32_t h, l;
+    split2(x[2 * t], x[2 * t + 1], h, l);
+    hi[t] = h;
+    lo[t] = l;
+  }
+}
+
+template <int D> struct Cfg {
+  static constexpr int PR = D + 8;          // row-major image stride (bf16)
+  static constexpr int RM = 32 * PR * 2;    // bytes of one row-major image (hi or lo)
+  static constexpr int PT = 40;             // transposed image stride (bf16): 32 slots + pad
+  static constexpr int TR = D * PT * 2;     // bytes of one transposed image
+  static constexpr int KS = D / 16;         // 16-deep K steps over the head dim
+  static constexpr int DB = D / 32;         // 32-wide output blocks
+  static constexpr int NC = D / 32;         // f32x4 per thread per 32-row fp32 tile (256 threads)
+};
+
+// one staged image: row-major hi/lo (RMF) and/or transposed hi/lo (TRF)
+template <int D, bool RMF, bool TRF> struct Img {
+  using CF = Cfg<D>;
+  static constexpr int RMH = 0, RML = CF::RM;
+  static constexpr int TRH = RMF ? 2 * CF::RM : 0, TRL = TRH + CF::TR;
+  static constexpr int BYTES = (RMF ? 2 * CF::RM : 0) + (TRF ? 2 * CF::TR : 0);
+};
+
+// tile row c (0..31) -> slot of the transposed image (inverse of K step j, half h, t = 0..7
+// <-> row tidx(8j + t, h) = (t & 3) + 16j + 8(t >> 2) + 4h)
+__device__ __forceinline__ int slot_of(int c) { return 16 * (c >> 4) + 8 * ((c >> 2) & 1) + (c & 3) + 4 * ((c >> 3) & 1); }
+__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
+
+// one 32-row fp32 tile global -> registers (rows row0.., clamped to row0 + rmax) -> split images
+template <int D> struct Tile {
+  using CF = Cfg<D>;
+  f32x4 r[CF::NC];
+  __device__ __forceinline__ void load(const float* base, int64_t ld, int64_t row0, int rmax, int tid) {
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      r[i] = *reinterpret_cast<const f32x4*>(base + (row0 + min(row, rmax)) * ld + 4 * c);
+    }
+  }
+  template <bool RMF, bool TRF>
+  __device__ __forceinline__ void store(char* img, int tid) const {
+    using IL = Img<D, RMF, TRF>;
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      uint32_t h0, l0, h1, l1;
+      split2(r[i][0], r[i][1], h0, l0);
+      split2(r[i][2], r[i][3], h1, l1);
+      if constexpr (RMF) {
+        const int o = (row * CF::PR + 4 * c) * 2;
+        *reinterpret_cast<u32x2*>(img + IL::RMH + o) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(img + IL::RML + o) = u32x2{l0, l1};
+      }
+      if constexpr (TRF) {
+        const int o = ((4 * c) * CF::PT + slot_of(row)) * 2;
+        const uint32_t hs[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+        const uint32_t ls[4] = {l0 & 0xffffu, l0 >> 16, l1 & 0xffffu, l1 >> 16};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          *reinterpret_cast<uint16_t*>(img + IL::TRH + o + e * CF::PT * 2) = (uint16_t)hs[e];
+          *reinterpret_cast<uint16_t*>(img + IL::TRL + o + e * CF::PT * 2) = (uint16_t)ls[e];
+        }
+      }
+    }
+  }
+};
+
+// register-resident split fragments of one 32-row block (B operand of row products):
+// fh/fl[m] = X[row][16m + 8h .. +7]; p points at X[row][8h]
+template <int D>
+__device__ __forceinline__ void load_frag(u32x4 (&fh)[D / 16], u32x4 (&fl)[D / 16], const float* p, bool ok) {
+#pragma unroll
+  for (int m = 0; m < D / 16; ++m) {
+    float x[8];
+    const f32x4 a = ok ? *reinterpret_cast<const f32x4*>(p + 16 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 b = ok ? *reinterpret_cast<const f32x4*>(p + 16 * m + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x[t] = a[t];
+      x[4 + t] = b[t];
+    }
+    split8(x, fh[m], fl[m]);
+  }
+}
+
+// acc[c][j] += Σ_d img[c][d] · frag[j][d]  (c = tile row: register, j = frag row: lane)
+template <int D, bool RMF, bool TRF>
+__device__ __forceinline__ f32x16 rowprod(const char* img, const u32x4 (&fh)[D / 16], const u32x4 (&fl)[D / 16],
+                                          f32x16 acc, int lane) {
+  using IL = Img<D, RMF, TRF>;
+  const char* p = img + ((lane & 31) * Cfg<D>::PR + 8 * (lane >> 5)) * 2;
+#pragma unroll
+  for (int m = 0; m < D / 16; ++m) {
+    const u32x4 ah = *reinterpret_cast<const u32x4*>(p + IL::RMH + 32 * m);
+    const u32x4 al = *reinterpret_cast<const u32x4*>(p + IL::RML + 32 * m);
+    acc = mm3(ah, al, fh[m], fl[m], acc);
+  }
+  return acc;
+}
+
+// out[db][d][j] += Σ_c img[c][d] · x[c][j]  (x: an accumulator tile, c its register rows)
+template <int D, bool RMF, bool TRF>
+__device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 (&out)[D / 32], int lane) {
+  using CF = Cfg<D>;
+  using IL = Img<D, RMF, TRF>;
+  u32x4 bh[2], bl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = x[8 * j + t];
+    split8(v, bh[j], bl[j]);
+  }
+  const char* p = img + ((lane & 31) * CF::PT + 8 * (lane >> 5)) * 2;
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = db * 32 * CF::PT * 2 + 32 * j;
+      const u32x4 ah = *reinterpret_cast<const u32x4*>(p + IL::TRH + o);
+      const u32x4 al = *reinterpret_cast<const u32x4*>(p + IL::TRL + o);
+      out[db] = mm3(ah, al, bh[j], bl[j], out[db]);
+    }
+}
+
+__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
+  return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
+}
+
+// ------------------------------------------------------------------------------------------
+// forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
+template <int D> struct FwdL {
+  using Q = Img<D, true, false>;
+  using V = Img<D, false, true>;
+  static constexpr int STAGE = Q::BYTES + V::BYTES;
+  static constexpr int LDS = 2 * STAGE;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
+  using CF = Cfg<D>;
+  using FL = FwdL<D>;
+  constexpr int DB = CF::DB;
+  using fa::smem;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+
+  u32x4 kh[CF::KS], kl[CF::KS];
+  load_frag<D>(kh, kl, reinterpret_cast<const float*>(a.rows) + ((int64_t)b * a.R + (row_ok ? row : 0)) * C + h * D + 8 * hf,
+               row_ok);
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* vb = reinterpret_cast<const float*>(a.vc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  float m_run = NEG_INF, l_run = 0.f;
+  f32x16 o[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) o[i] = f32x16{};
+
+  Tile<D> tq, tv;
+  if (kt_beg < kt_end) {
+    tq.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    tv.load(vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    tq.template store<true, false>(smem, tid);
+    tv.template store<false, true>(smem + FL::Q::BYTES, tid);
+    __syncthreads();
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (more) {
+      tq.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+      tv.load(vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    }
+    const char* qi = smem + ((kt - kt_beg) & 1) * FL::STAGE;
+    const char* vi = qi + FL::Q::BYTES;
+    int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D, true, false>(qi, kh, kl, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
+      const int valid = a.T - kt * 32;
+      if (flag == 2 || valid < 32) {
+        uint32_t w = 0;
+        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = tidx(r, hf);
+          if (((w >> c) & 1u) || c >= valid) s[r] = NEG_INF;
+        }
+      }
+      float mx = NEG_INF;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+      mx = pair_max(mx) * c2;
+      const float m_new = fmaxf(m_run, mx);
+      if (m_new > m_run) {
+        const float alpha = ex2(m_run - m_new);  // m_run = -inf: 0
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < DB; ++i) o[i] *= alpha;
+        m_run = m_new;
+      }
+      const float m_use = m_run == NEG_INF ? 0.f : m_run;
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = ex2(__builtin_fmaf(s[r], c2, -m_use));
+        ls += s[r];
+      }
+      l_run += ls;
+      trprod<D, false, true>(vi, s, o, lane);  // Oᵀ += Vᵀ · Pᵀ
+    }
+    if (more) {
+      char* nx = smem + ((kt + 1 - kt_beg) & 1) * FL::STAGE;
+      tq.template store<true, false>(nx, tid);
+      tv.template store<false, true>(nx + FL::Q::BYTES, tid);
+    }
+    __syncthreads();
+  }
+
+  const float l_tot = pair_sum(l_run);
+  const float inv = 1.f / l_tot;
+  if (!row_ok) return;
+  const float lse = (m_run + __log2f(l_tot)) * LN2;
+  float* op;
+  if (a.nsplit == 1 && !a.force_partial) {
+    op = reinterpret_cast<float*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
+    if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = lse;
+  } else {
+    op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
+    if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = lse;
+  }
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, row side: dK = scale · Σ_cols dS · Q_cols.  4 waves x 32 rows, column split.
+// One LDS stage (the next tile waits in registers).
+template <int D> struct RowsL {
+  using Q = Img<D, true, true>;
+  using V = Img<D, true, false>;
+  static constexpr int STAGE = Q::BYTES + V::BYTES;
+  static constexpr int LDS = STAGE;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  using RL = RowsL<D>;
+  constexpr int DB = CF::DB;
+  using fa::smem;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+
+  u32x4 kh[CF::KS], kl[CF::KS], dh[CF::KS], dl[CF::KS];
+  {
+    const int64_t off = ((int64_t)b * a.R + (row_ok ? row : 0)) * C + h * D + 8 * hf;
+    load_frag<D>(kh, kl, reinterpret_cast<const float*>(a.rows) + off, row_ok);
+    load_frag<D>(dh, dl, reinterpret_cast<const float*>(a.dout) + off, row_ok);
+  }
+  const int64_t li = ((int64_t)b * a.H + h) * a.R + (row_ok ? row : 0);
+  const float lse2 = row_ok ? a.lse[li] * LOG2E : 0.f, dlt = row_ok ? a.delta[li] : 0.f;
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* vb = reinterpret_cast<const float*>(a.vc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+
+  const char* qi = smem;
+  const char* vi = smem + RL::Q::BYTES;
+  Tile<D> tq, tv;
+  if (kt_beg < kt_end) {
+    tq.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    tv.load(vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    tq.template store<true, true>(smem, tid);
+    tv.template store<true, false>(smem + RL::Q::BYTES, tid);
+    __syncthreads();
+    if (kt + 1 < kt_end) {
+      tq.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+      tv.load(vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    }
+    int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D, true, true>(qi, kh, kl, f32x16{}, lane);    // Sᵀ  (col x row)
+      f32x16 dp = rowprod<D, true, false>(vi, dh, dl, f32x16{}, lane);  // dPᵀ (col x row)
+      const int valid = a.T - kt * 32;
+      uint32_t w = 0;
+      const bool chk = flag == 2 || valid < 32;
+      if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = __builtin_fmaf(s[r], c2, -lse2);
+        if (chk) {
+          const int c = tidx(r, hf);
+          if (((w >> c) & 1u) || c >= valid) x = NEG_INF;
+        }
+        s[r] = ex2(x) * (dp[r] - dlt);  // dSᵀ / scale
+      }
+      trprod<D, true, true>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+    }
+    __syncthreads();
+  }
+  if (!row_ok) return;
+  float* op = (a.nsplit > 1 || a.force_partial) ? a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D
+                                                : reinterpret_cast<float*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dk[db][4 * g] * sc, dk[db][4 * g + 1] * sc, dk[db][4 * g + 2] * sc, dk[db][4 * g + 3] * sc};
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, gathered side: dQ_cols = scale · Σ_rows dSᵀ · K_rows, dV_cols = Σ_rows Pᵀ · dO.
+// 4 waves x 32 columns of one (b, h); sweeps 32-row tiles of K_rows / dO + their lse2 / δ.
+template <int D> struct ColsL {
+  using K = Img<D, true, true>;
+  static constexpr int AUX = 256;  // lse2[32], δ[32] (fp32)
+  static constexpr int STAGE = 2 * K::BYTES + AUX;
+  static constexpr int LDS = 2 * STAGE;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  using KL = ColsL<D>;
+  constexpr int DB = CF::DB;
+  using fa::smem;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = (a.T + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = lin % ncb, bh = lin / ncb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
+  const bool col_ok = col < a.T;
+  const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
+  const int NRT = (a.R + 31) / 32;
+
+  u32x4 qh[CF::KS], ql[CF::KS], vh[CF::KS], vl[CF::KS];
+  {
+    const int64_t off = ((int64_t)b * a.T + (col_ok ? col : 0)) * a.ldkv + h * D + 8 * hf;
+    load_frag<D>(qh, ql, reinterpret_cast<const float*>(a.kc) + off, col_ok);
+    load_frag<D>(vh, vl, reinterpret_cast<const float*>(a.vc) + off, col_ok);
+  }
+  const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
+  const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
+  const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
+  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dq[DB], dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) {
+    dq[i] = f32x16{};
+    dv[i] = f32x16{};
+  }
+
+  // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
+  auto aux_load = [&](int rt) -> float {
+    const int rr = rt * 32 + (tid & 31);
+    if (tid < 32) return rr < a.R ? lse2[rr] : __builtin_inff();
+    if (tid < 64) return rr < a.R ? dlt[rr] : 0.f;
+    return 0.f;
+  };
+  auto put = [&](char* st, const Tile<D>& tk, const Tile<D>& td, float ax) {
+    tk.template store<true, true>(st, tid);
+    td.template store<true, true>(st + KL::K::BYTES, tid);
+    if (tid < 64) reinterpret_cast<float*>(st + 2 * KL::K::BYTES)[tid] = ax;
+  };
+  Tile<D> tk, td;
+  float ax = 0.f;
+  if (NRT > 0) {
+    tk.load(kb, C, 0, a.R - 1, tid);
+    td.load(db_, C, 0, a.R - 1, tid);
+    ax = aux_load(0);
+    put(smem, tk, td, ax);
+    __syncthreads();
+  }
+  for (int rt = 0; rt < NRT; ++rt) {
+    const bool more = rt + 1 < NRT;
+    if (more) {
+      tk.load(kb, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      td.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      ax = aux_load(rt + 1);
+    }
+    const char* ki = smem + (rt & 1) * KL::STAGE;
+    const char* di = ki + KL::K::BYTES;
+    const float* ls = reinterpret_cast<const float*>(ki + 2 * KL::K::BYTES);  // lse2[32], δ[32]
+    int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      f32x16 s = rowprod<D, true, true>(ki, qh, ql, f32x16{}, lane);   // S  (row x col)
+      f32x16 dp = rowprod<D, true, true>(di, vh, vl, f32x16{}, lane);  // dP (row x col)
+      uint32_t w = 0;
+      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = tidx(r, hf);
+        float x = __builtin_fmaf(s[r], c2, -ls[i]);
+        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
+        const float p = ex2(x);
+        s[r] = p;
+        dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
+      }
+      trprod<D, true, true>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
+      trprod<D, true, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+    }
+    if (more) put(smem + ((rt + 1) & 1) * KL::STAGE, tk, td, ax);
+    __syncthreads();
+  }
+  if (!col_ok) return;
+  float* pq = reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dq[db][4 * g] * sc, dq[db][4 * g + 1] * sc, dq[db][4 * g + 2] * sc, dq[db][4 * g + 3] * sc};
+      *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+    }
+}
+
+}  // namespace fa3
+}  // namespace xdot
+
+#define X3_DISPATCH(CALL)              \
+  switch (D) {                         \
+    case 32: CALL(32); return 0;       \
+    case 64: CALL(64); return 0;       \
+    case 96: CALL(96); return 0;       \
+    case 128: CALL(128); return 0;     \
+    default: return -1;                \
+  }
+
+extern "C" int xdot_flash_fwd_x3_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa3;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
+  const dim3 grid(((a->R + 127) / 128) * a->B * a->H * a->nsplit);
+#define L(DV) hipLaunchKernelGGL(fwd_kernel<DV>, grid, dim3(256), FwdL<DV>::LDS, st, *a)
+  X3_DISPATCH(L)
+#undef L
+}
+
+extern "C" int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa3;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (a->prescaled) return -1;
+  const dim3 grid(((a->R + 127) / 128) * a->B * a->H * a->nsplit);
+#define L(DV) hipLaunchKernelGGL(bwd_rows_kernel<DV>, grid, dim3(256), RowsL<DV>::LDS, st, *a)
+  X3_DISPATCH(L)
+#undef L
+}
+
+extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
+  using namespace xdot::fa3;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (a->prescaled || a->dkv16) return -1;
+  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+#define L(DV) hipLaunchKernelGGL(bwd_cols_kernel<DV>, grid, dim3(256), ColsL<DV>::LDS, st, *a)
+  X3_DISPATCH(L)
+#undef L
+}

@@ -55,6 +55,7 @@ struct FwdArgs {
   int prescaled;           // 1: rows hold K * scale * log2(e) (xdot_prescale_rows_launch)
   float* out32;            // combine only: non-null -> write the merged O in fp32 here (fully
                            // masked rows: 0 with lse -inf), a running partial for the ring
+  int fp32_mode;           // fp32 inputs: 0 exact (flash_f32.hip), 1 split-bf16 (flash_x3.hip)
 };
 
 struct BwdArgs {
@@ -80,6 +81,7 @@ struct BwdArgs {
   int sp0;                 // first partial slot of this launch (chunked launches)
   int force_partial;       // 1: write partials even with nsplit == 1 (summed separately)
   int prescaled;           // 1: rows hold K * scale * log2(e) (same buffer as the forward's)
+  int fp32_mode;           // fp32 inputs: 0 exact (flash_f32.hip), 1 split-bf16 (flash_x3.hip)
 };
 
 }  // namespace fa
@@ -168,6 +170,10 @@ int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, 
 int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+// split-bf16 fp32 family (csrc/flash_x3.hip, fp32_mode = 1); prep / combine / sum are shared
+int xdot_flash_fwd_x3_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st);
+int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 // native xGMI pull collectives (csrc/ipc.hip)
 int xdot_ipc_sig_bytes();
 int xdot_ipc_max_ranks();

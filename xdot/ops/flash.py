@@ -14,6 +14,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import _ext
+from ..utils.env import FLAGS
 
 
 class PackedMask:
@@ -188,15 +189,33 @@ def prescale(rows: torch.Tensor, scale: float) -> torch.Tensor:
     return _ext.ops().flash_prescale(rows.contiguous(), float(scale))
 
 
+FP32_MODES = {"exact": 0, "split": 1}
+
+
+def fp32_code(dtype: torch.dtype, mode: Optional[str] = None) -> int:
+    """Kernel family of fp32 operands: 1 split-bf16 (``csrc/flash_x3.hip``, default: 3 bf16 MFMAs
+    per product, <= 9e-6 relative error vs fp64), 0 exact fp32 (``csrc/flash_f32.hip``, ~5e-7;
+    profiles/r3_fp32_split.md).  ``mode`` None: ``XDOT_FP32_MODE``.  0 for 16-bit dtypes."""
+    if dtype != torch.float32:
+        return 0
+    mode = FLAGS.fp32_mode if mode is None else mode
+    if mode not in FP32_MODES:
+        raise ValueError(f"fp32 mode must be one of {sorted(FP32_MODES)}, got {mode!r}")
+    return FP32_MODES[mode]
+
+
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
-        scale: float, nsplit: int = 0, prescaled: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        scale: float, nsplit: int = 0, prescaled: bool = False,
+        fp32_mode: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """-> (out (B, R, H*D) in rows.dtype, lse (B, H, R) fp32 natural log).
 
     ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU).
-    ``prescaled``: ``rows`` is :func:`prescale` output."""
+    ``prescaled``: ``rows`` is :func:`prescale` output.  ``fp32_mode``: :func:`fp32_code`
+    (None: from ``XDOT_FP32_MODE``)."""
     bits, flags = _mask_args(mk)
+    fm = fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode)
     return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit),
-                                bool(prescaled))
+                                bool(prescaled), fm)
 
 
 def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
@@ -211,7 +230,7 @@ def bwd_prep(dout: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, H: int):
 
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
              delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False,
-             lse2: Optional[torch.Tensor] = None):
+             lse2: Optional[torch.Tensor] = None, fp32_mode: Optional[int] = None):
     """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
     ``delta`` (from :func:`bwd_delta`) is computed here when not given; with ``lse2`` too (both
@@ -220,26 +239,29 @@ def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, sca
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
-                                     bool(fp32_out), bool(prescaled), lse2)
+                                     bool(fp32_out), bool(prescaled), lse2,
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode))
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0,
-             prescaled: bool = False):
+             prescaled: bool = False, fp32_mode: Optional[int] = None):
     """Row-side grad (B, R, H*D) in rows.dtype.  ``nsplit`` 0: the launcher's occupancy model
     (column splits so the row kernel fills the GPU; 1 measured 7 % / 32 % slower at N = 1 / 8)."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
-                                     int(nsplit), bool(prescaled))
+                                     int(nsplit), bool(prescaled),
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode))
 
 
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,
-        lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float, prescaled: bool = False):
+        lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float, prescaled: bool = False,
+        fp32_mode: Optional[int] = None):
     """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads).
 
     ``prescaled``: ``rows`` is :func:`prescale` output (the buffer the forward read); d_rows is
     still the gradient of the unscaled rows."""
-    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale, prescaled=prescaled)
-    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale, prescaled=prescaled)
+    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode)
+    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode)
     C = rows.shape[-1]
     return drows, dkv[..., :C], dkv[..., C:]

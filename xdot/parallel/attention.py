@@ -262,7 +262,7 @@ def _mask_cols(B: int, R: int, n: int, j0: int, j1: int, r0: int, rc: int):
     return lambda m: m.reshape(B, R, n, R)[..., j0:j1, r0:r0 + rc].reshape(B, R, (j1 - j0) * rc)
 
 
-def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled):
+def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled, fp32_mode=0):
     """Forward of a multi-rank step as column segments merged by one log-sum-exp combine:
     the rank's OWN [q|v] block first (it needs no communication, so its partial runs while the
     all-gather is in flight), then each gathered chunk's peer blocks as soon as that chunk
@@ -287,7 +287,7 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
             bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
             nsi = ns[slot[1]]
             ops.flash_fwd_partial(k, flash._kv(kc), flash._kv(vc), bits, flags, int(H), float(scale), opart, lpart,
-                                  slot[0], nsi, prescaled)
+                                  slot[0], nsi, prescaled, fp32_mode)
             slot[0] += nsi
             slot[1] += 1
 
@@ -322,8 +322,20 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
 
 
 _SIDE = {}
-# diagnostics (A/B of HIP-graph replay): run the fused backward's two halves on the caller's stream
-ONE_STREAM_BACKWARD = False
+# The fused backward runs its gathered-side half on a high-priority side stream so the row-side
+# kernel fills the column kernel's last, mostly empty workgroup round.  Eager, on one MI355X
+# (benchmarks/graph_ab.py, profiles/r3_graph.md), two streams vs one: N=1 8.18 vs 8.60 ms, N=2
+# rank 4.38 vs 4.59, N=4 rank 2.40 vs 2.46, N=8 rank 1.39 vs 1.43 (an earlier box: 1.43 vs 1.40,
+# within box noise).  Under HIP-graph capture the side stream's priority is lost and two streams
+# replay 19-32 % slower at N=1/2, so a captured backward uses one stream.
+# ONE_STREAM_BACKWARD: None = that rule, True / False = force (A/B diagnostics).
+ONE_STREAM_BACKWARD = None
+
+
+def _two_stream_backward(R: int) -> bool:
+    if ONE_STREAM_BACKWARD is not None:
+        return not ONE_STREAM_BACKWARD
+    return not torch.cuda.is_current_stream_capturing()
 
 
 def _side_stream(dev: torch.device, priority: int = -1) -> "torch.cuda.Stream":
@@ -353,10 +365,12 @@ class SeqParallelAttention(torch.autograd.Function):
             pending = _PendingGather(comm, qv, _row_chunks(n, qv.shape[1], use_hip))
         chunks = pending.chunks
         prescaled = False
+        fm = 0  # fp32 kernel family (XDOT_FP32_MODE), fixed at forward for the backward too
         packed_full = None  # the whole-row packed mask, when the caller packed it ahead
         if use_hip:
             from ..ops import flash
 
+            fm = flash.fp32_code(k.dtype)
             # the row side pre-multiplied by scale*log2 e once (XDOT_PRESCALE, default on): the
             # forward and both backward kernels read this same buffer and seed their score
             # accumulators instead of scaling every score (saved in place of k for backward)
@@ -373,18 +387,18 @@ class SeqParallelAttention(torch.autograd.Function):
             if use_hip:
                 mk = packed_full if packed_full is not None else flash.prepare_mask_cached(mask, B, R, n * R)
                 qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
-                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mk, H, scale, prescaled=prescaled)
+                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mk, H, scale, prescaled=prescaled, fp32_mode=fm)
                 bufs, mks = [qvg], [mk]
             else:
                 qvg = pending.wait(0)                            # (N, B, R, 2C)
                 o, lse = _ref_fwd(k, qvg[..., :C], qvg[..., C:], mask, H, scale)
                 bufs, mks = [qvg], [mask]
         else:
-            o, lse, bufs = _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled)
+            o, lse, bufs = _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled, fm)
             mks = [packed_full] if packed_full is not None else None  # backward packs its own (cached)
         ctx.save_for_backward(k, o, lse, *bufs)
         ctx.mks, ctx.mask, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, mask, chunks, H, scale, comm, use_hip
-        ctx.prescaled = prescaled
+        ctx.prescaled, ctx.fp32_mode = prescaled, fm
         return o
 
     @staticmethod
@@ -427,7 +441,7 @@ class SeqParallelAttention(torch.autograd.Function):
             cur = torch.cuda.current_stream(do.device)
             # high priority so the gathered side (and its reduce-scatter) finishes early (an
             # ordinary-priority side stream measured slower at N=1 and N=8: profiles/r2_bwd_overlap.md)
-            hi = cur if ONE_STREAM_BACKWARD else _side_stream(do.device, -1)
+            hi = _side_stream(do.device, -1) if _two_stream_backward(R) else cur
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
@@ -443,7 +457,8 @@ class SeqParallelAttention(torch.autograd.Function):
                 if one:
                     g = bufs[0]
                     dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2)
+                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
+                                            fp32_mode=ctx.fp32_mode)
                     off = 0
                     for r0, rc in chunks:  # (chunk, rank, row) order: chunk c's ranks are contiguous
                         part = dkv if len(chunks) == 1 else dkv[:, off:off + n * rc]
@@ -456,7 +471,8 @@ class SeqParallelAttention(torch.autograd.Function):
                     for c, (r0, rc) in enumerate(chunks):
                         g = bufs[c]
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[c], H, scale, delta,
-                                                fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2)
+                                                fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
+                                            fp32_mode=ctx.fp32_mode)
                         h, oc = reduce_async(flash.btc_to_rank_major(dkv, n),
                                              None if dqv is None else dqv[:, r0:r0 + rc])
                         handles.append(h)
@@ -468,7 +484,7 @@ class SeqParallelAttention(torch.autograd.Function):
             if one:
                 g = bufs[0]
                 dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
-                                    prescaled=ctx.prescaled)
+                                    prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
             else:
                 ops = _ext.ops()
                 ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))
@@ -478,7 +494,8 @@ class SeqParallelAttention(torch.autograd.Function):
                     mk = mks[c]
                     bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                     ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                               flags, int(H), float(scale), dpart, c * ns, ns, ctx.prescaled)
+                                               flags, int(H), float(scale), dpart, c * ns, ns, ctx.prescaled,
+                                               ctx.fp32_mode)
                 dk = ops.flash_bwd_rows_sum(dpart, int(H), k)
             with torch.cuda.stream(hi):  # the gathered-side grads complete on the priority stream
                 for h in handles:

@@ -127,10 +127,12 @@ class RingAttention(torch.autograd.Function):
         ring = _Ring(comm, qv)
         mks: List = []
         prescaled = False
+        fm = 0
         if use_hip:
             from ..ops import flash
 
             ops = _ext.ops()
+            fm = flash.fp32_code(k.dtype)
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
             kk = flash.prescale(k, scale) if prescaled else k.contiguous()
             ns = int(ops.flash_splits(B, R, R, H, False))
@@ -150,7 +152,7 @@ class RingAttention(torch.autograd.Function):
                 bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                 g = ring.cur
                 ops.flash_fwd_partial(kk, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                      float(scale), opart, lpart, 1, ns, prescaled)
+                                      float(scale), opart, lpart, 1, ns, prescaled, fm)
                 if s < n - 1:
                     ops.flash_fwd_merge(opart, lpart, lrun, int(H))
                     lpart[0].copy_(lrun)
@@ -178,6 +180,7 @@ class RingAttention(torch.autograd.Function):
             o = acc.transpose(1, 2).reshape(B, R, -1).to(k.dtype)
             ctx.save_for_backward(k, qv, o, lse)
         ctx.mks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip, ctx.prescaled = mks, H, scale, comm, use_hip, prescaled
+        ctx.fp32_mode = fm
         return o
 
     @staticmethod
@@ -223,10 +226,11 @@ class RingAttention(torch.autograd.Function):
                 hi.wait_stream(cur)
                 with torch.cuda.stream(hi):
                     contrib, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mk, H, scale, delta,
-                                                fp32_out=True, prescaled=ctx.prescaled)
+                                                fp32_out=True, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
                 bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                 ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                           flags, int(H), float(scale), dpart, 1, nsr, ctx.prescaled)
+                                           flags, int(H), float(scale), dpart, 1, nsr, ctx.prescaled,
+                                           ctx.fp32_mode)
                 if s < n - 1:
                     ops.sum_partials_into(dpart, dpart[0])
                 cur.wait_stream(hi)

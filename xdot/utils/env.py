@@ -36,6 +36,9 @@ variable                    default   effect
 ``XDOT_IPC_TIMEOUT_S``      (comm)    bound of every IPC device-side wait
 ``XDOT_PRESCALE``           1         pre-multiply the row side by scale·log2 e once per forward
                                       (seeded score accumulators; forward 2.11 -> 1.98 ms)
+``XDOT_FP32_MODE``          split     fp32 flash kernels: ``split`` (hi/lo bf16 halves, 3 bf16 MFMAs per
+                                      product: <= 9e-6 relative vs fp64, 1.6x faster step) or
+                                      ``exact`` (fp32 MFMA, ~5e-7); profiles/r3_fp32_split.md
 ``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
                                       1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
 ``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
@@ -97,6 +100,7 @@ class _Flags:
         self.ipc_wgs = _num("XDOT_IPC_WGS", 64, int)
         self.ipc_timeout_s = _num("XDOT_IPC_TIMEOUT_S", self.comm_timeout_s)
         self.prescale = _flag("XDOT_PRESCALE", default="1")
+        self.fp32_mode = _str("XDOT_FP32_MODE", "split")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
