@@ -373,6 +373,34 @@ int rows_split(int64_t B, int64_t R, int64_t T, int64_t H) {
   return std::max(base, (int)conc);
 }
 
+// Head-heavy forward grid (16-bit, whole-GPU launches).  A uniform column split makes every row
+// block pay the partial writes and a combine pass, and still ends on a part-full round: at N=1
+// (1568 row blocks, 512 slots) the auto split is 3 -> 10 rounds of 1/3 blocks plus a 3-slot
+// combine.  Instead each XCD (64 slots: 32 CUs x 2 workgroups, blockIdx % 8) runs its row blocks
+// whole and splits only its last `rem` blocks into enough column pieces to fill one more round;
+// only those tail rows go through partials and the (compact) combine.  Chosen when the round
+// model says it beats the uniform split; -> (whole, rem, split) per XCD, or false.
+bool head_heavy_plan(int64_t NB, int64_t T, int* whole, int* rem, int* split) {
+  if (NB % 8) return false;
+  const int64_t m = NB / 8, S = 64, nkt = (T + 63) / 64;
+  const int64_t full = m / S, r = m % S;
+  if (r == 0 || full == 0) return false;
+  const int su = pick_split(NB, T, 512, 0);
+  const double cu = (double)((NB * su + 511) / 512) * ((double)nkt / su + 8.0);
+  double best = 1e300;
+  int bs = 0;
+  for (int s = 1; s <= 16; ++s) {
+    if (s > 1 && nkt / s < 8) break;
+    const double c = (double)full * ((double)nkt + 8.0) + (double)((r * s + S - 1) / S) * ((double)nkt / s + 8.0);
+    if (c < best * 0.985) { best = c; bs = s; }
+  }
+  if (bs < 2 || best >= cu * 0.97) return false;
+  *whole = (int)(full * S);
+  *rem = (int)r;
+  *split = bs;
+  return true;
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
                                              int64_t H, double scale, int64_t nsplit, bool prescaled, int64_t fp32_mode) {
@@ -381,13 +409,24 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   auto out = at::empty_like(rows);
   auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   const int rpw = xdot_flash_fwd_rows_per_wg();
-  const int ns = pick_split(((g.R + rpw - 1) / rpw) * g.B * H, g.T, 512, nsplit);
+  const int64_t NB = ((g.R + rpw - 1) / rpw) * g.B * H;
+  int hw = 0, hr = 0, hs = 0;
+  const bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
+  const int ns = heavy ? hs : pick_split(NB, g.T, 512, nsplit);
   at::Tensor opart, lpart;
-  if (ns > 1) {
+  if (heavy) {  // compact partials of the split tail blocks only
+    opart = at::empty({(int64_t)hs * 8 * hr * 128 * g.D}, rows.options().dtype(at::kFloat));
+    lpart = at::empty({(int64_t)hs * 8 * hr * 128}, rows.options().dtype(at::kFloat));
+  } else if (ns > 1) {
     opart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
     lpart = at::empty({ns, g.B, H, g.R}, rows.options().dtype(at::kFloat));
   }
   xdot::fa::FwdArgs a{};
+  if (heavy) {
+    a.xrbs = (int)(NB / 8);
+    a.xwhole = hw;
+    a.xrem = hr;
+  }
   a.rows = rows.data_ptr(); a.kc = kc.data_ptr(); a.vc = vc.data_ptr(); a.out = out.data_ptr();
   a.lse = lse.data_ptr<float>();
   const bool hb = bits.has_value() && bits->defined();

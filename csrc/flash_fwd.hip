@@ -48,13 +48,33 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps wave-derived flags in SGPRs
   const Lanes L = make_lanes<D>(lane);
   const int nrb = (a.R + 127) / 128;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb = lin % nrb, bhs = lin / nrb;
-  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  int rbl, sp, ns, tail = -1;  // linear row block (bh * nrb + rb), column piece, pieces of this block
+  if (a.xrbs > 0) {
+    // head-heavy grid: XCD x runs its row blocks whole, then its last xrem split in nsplit
+    // column pieces (compact partial index `tail`), so its last round of 64 slots is full
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    if (k < a.xwhole) {
+      rbl = x * a.xrbs + k;
+      sp = 0;
+      ns = 1;
+    } else {
+      const int p = k - a.xwhole, j = p / a.nsplit;
+      rbl = x * a.xrbs + a.xwhole + j;
+      sp = p - j * a.nsplit;
+      ns = a.nsplit;
+      tail = x * a.xrem + j;
+    }
+  } else {
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    rbl = lin % (nrb * a.B * a.H);
+    sp = lin / (nrb * a.B * a.H);
+    ns = a.nsplit;
+  }
+  const int rb = rbl % nrb, bh = rbl / nrb;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int NKT = (a.T + 63) / 64;
-  const int kt_beg = (int)((int64_t)sp * NKT / a.nsplit), kt_end = (int)((int64_t)(sp + 1) * NKT / a.nsplit);
+  const int kt_beg = (int)((int64_t)sp * NKT / ns), kt_end = (int)((int64_t)(sp + 1) * NKT / ns);
   const int r0 = rb * 128 + wave * 32;
   const int row = r0 + (lane & 31);
   const bool row_ok = row < a.R;
@@ -243,7 +263,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
           q1 = q2;
         }
       }
-      // ---- block B: P(kt)·V(kt) MFMAs, each followed by its share of the row sums ----
+      // ---- block B: P(kt)·V(kt) MFMAs, each followed by its share of the row sums (scalar
+      // adds: packed v_pk_add_f32 pairs measured 0.5-3 % slower beside the MFMAs) ----
       float ls = 0.f;
       {
         u32x4 v0 = tr_frag<D>(cur + IMG, 0, 0, L), v1 = tr_frag<D>(cur + IMG, 16, 0, L);
@@ -309,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   // ---- epilogue ----
   const float l_tot = pair_sum(l_run);
   const float inv = 1.f / l_tot;
-  if (row_ok && a.nsplit == 1 && !a.force_partial) {
+  if (row_ok && ns == 1 && !a.force_partial) {
     T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
@@ -321,6 +342,18 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hf) = w;
       }
     if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = (m_run + __log2f(l_tot)) * LN2;
+  } else if (row_ok && tail >= 0) {
+    // head-heavy tail piece: compact partial, merged by flash_fwd_combine_tail
+    const int64_t pi = ((int64_t)sp * 8 * a.xrem + tail) * 128 + (row - rb * 128);
+    float* op = a.opart + pi * D;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v = {o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
+        *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) = v;
+      }
+    if (hf == 0) a.lpart[pi] = (m_run + __log2f(l_tot)) * LN2;
   } else if (row_ok) {
     // split partial: normalised fp32 output + its LSE; merged by flash_fwd_combine
     float* op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
@@ -338,6 +371,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 // merge column-split partials: lse = log Σ_s e^{lse_s}, O = Σ_s e^{lse_s - lse} O_s.
 // A split that saw only masked columns has lse_s = -inf and contributes nothing; a row with
 // every split -inf is fully masked and yields NaN like the unsplit kernel.
+constexpr int CMB_MAX = 12;  // slots merged with all loads in flight (more: a per-slot loop)
+
 template <int DT, int D>
 __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
   using T16 = typename dt_traits<DT>::T;
@@ -351,19 +386,40 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
   const int h = (c4 * 4) / D;
   const int64_t lstride = (int64_t)a.B * a.H * a.R;
   const float* lp = a.lpart + ((int64_t)b * a.H + h) * a.R + row;
-  float mx = -__builtin_inff();
-  for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, lp[s * lstride]);
-  float sum = 0.f;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int64_t ostride = (int64_t)a.B * a.R * C;
   const float* opp = a.opart + br * C + c4 * 4;
-  for (int s = 0; s < a.nsplit; ++s) {
-    const float l = lp[s * lstride];
-    if (l == -__builtin_inff()) continue;
-    const float wgt = __expf(l - mx);
-    sum += wgt;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(opp + s * ostride);
-    acc += wgt * v;
+  float mx = -__builtin_inff(), sum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (a.nsplit <= CMB_MAX) {
+    // every slot's LSE and 16-byte partial in flight at once (the loop below waits per slot)
+    float l[CMB_MAX];
+    f32x4 v[CMB_MAX];
+#pragma unroll
+    for (int s = 0; s < CMB_MAX; ++s) {
+      l[s] = s < a.nsplit ? lp[s * lstride] : -__builtin_inff();
+      v[s] = s < a.nsplit ? *reinterpret_cast<const f32x4*>(opp + s * ostride) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s = 0; s < CMB_MAX; ++s) mx = fmaxf(mx, l[s]);
+#pragma unroll
+    for (int s = 0; s < CMB_MAX; ++s) {
+      // a split that saw only masked columns wrote NaN (0 / 0): selected out, not multiplied by 0
+      const bool live = l[s] != -__builtin_inff();
+      const float wgt = live ? __expf(l[s] - mx) : 0.f;
+      const f32x4 t = wgt * v[s];
+      sum += wgt;
+      acc += live ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else {
+    for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, lp[s * lstride]);
+    for (int s = 0; s < a.nsplit; ++s) {
+      const float l = lp[s * lstride];
+      if (l == -__builtin_inff()) continue;
+      const float wgt = __expf(l - mx);
+      sum += wgt;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(opp + s * ostride);
+      acc += wgt * v;
+    }
   }
   const float inv = 1.f / sum;  // sum == 0 (fully masked row) -> NaN output, -inf lse
   if (a.out32) {  // running fp32 merge (ring attention): masked-so-far rows stay 0 / -inf
@@ -380,6 +436,52 @@ __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
   if ((c4 * 4) % D == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
 }
 
+// merge the head-heavy grid's split tail blocks (compact partials) into out / lse
+template <int DT, int D>
+__global__ __launch_bounds__(256) void flash_fwd_combine_tail(FwdArgs a) {
+  using T16 = typename dt_traits<DT>::T;
+  const int ntail = 8 * a.xrem;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)ntail * 128 * (D / 4)) return;
+  const int c4 = (int)(idx % (D / 4));
+  const int tr = (int)(idx / (D / 4));
+  const int rloc = tr & 127, t = tr >> 7;
+  const int nrb = (a.R + 127) / 128;
+  const int rbl = (t / a.xrem) * a.xrbs + a.xwhole + t % a.xrem;
+  const int rb = rbl % nrb, bh = rbl / nrb, b = bh / a.H, h = bh % a.H;
+  const int row = rb * 128 + rloc;
+  if (row >= a.R) return;
+  const int64_t pstride = (int64_t)ntail * 128, p0 = (int64_t)t * 128 + rloc;
+  float mx = -__builtin_inff(), sum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float l[16];
+  f32x4 v[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    l[s] = s < a.nsplit ? a.lpart[s * pstride + p0] : -__builtin_inff();
+    v[s] = s < a.nsplit ? *reinterpret_cast<const f32x4*>(a.opart + (s * pstride + p0) * D + 4 * c4)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) mx = fmaxf(mx, l[s]);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const bool live = l[s] != -__builtin_inff();
+    const float wgt = live ? __expf(l[s] - mx) : 0.f;
+    const f32x4 tv = wgt * v[s];
+    sum += wgt;
+    acc += live ? tv : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float inv = 1.f / sum;  // fully masked row: NaN output, -inf lse
+  T16* op = reinterpret_cast<T16*>(a.out) + ((int64_t)b * a.R + row) * (a.H * D) + h * D + 4 * c4;
+  u32x2 w;
+  w[0] = pack2<DT>(acc[0] * inv, acc[1] * inv);
+  w[1] = pack2<DT>(acc[2] * inv, acc[3] * inv);
+  if (sum == 0.f) { w[0] = pack2<DT>(__builtin_nanf(""), __builtin_nanf("")); w[1] = w[0]; }
+  *reinterpret_cast<u32x2*>(op) = w;
+  if (c4 == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
+}
+
 template <int DT, int D>
 static void launch_combine(const FwdArgs& a, hipStream_t st) {
   const int64_t n = (int64_t)a.B * a.R * (a.H * D / 4);
@@ -393,10 +495,15 @@ template <int DT, int D>
 static void launch_fwd(const FwdArgs& a, hipStream_t st) {
   constexpr int LDS = 3 * RowsCfg<D>::STAGE;
   const int nrb = (a.R + 127) / 128;
-  const dim3 grid(nrb * a.B * a.H * a.nsplit);
+  const dim3 grid(a.xrbs > 0 ? 8 * (a.xwhole + a.xrem * a.nsplit) : nrb * a.B * a.H * a.nsplit);
   if (a.prescaled) hipLaunchKernelGGL((flash_fwd_kernel<DT, D, true>), grid, dim3(256), LDS, st, a);
   else hipLaunchKernelGGL((flash_fwd_kernel<DT, D>), grid, dim3(256), LDS, st, a);
-  if (a.nsplit > 1 && !a.force_partial) launch_combine<DT, D>(a, st);
+  if (a.xrbs > 0) {
+    const int64_t n = (int64_t)8 * a.xrem * 128 * (D / 4);
+    if (a.xrem > 0) hipLaunchKernelGGL((flash_fwd_combine_tail<DT, D>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  } else if (a.nsplit > 1 && !a.force_partial) {
+    launch_combine<DT, D>(a, st);
+  }
 }
 
 }  // namespace fa

@@ -56,6 +56,11 @@ struct FwdArgs {
   float* out32;            // combine only: non-null -> write the merged O in fp32 here (fully
                            // masked rows: 0 with lse -inf), a running partial for the ring
   int fp32_mode;           // fp32 inputs: 0 exact (flash_f32.hip), 1 split-bf16 (flash_x3.hip)
+  // head-heavy grid (16-bit forward, xrbs > 0): XCD x = blockIdx % 8 owns row blocks
+  // [x*xrbs, (x+1)*xrbs) (linear index bh*nrb + rb); the first xwhole run whole, the last xrem
+  // are split into nsplit column pieces whose partials go to a compact buffer
+  // opart/lpart[(piece * 8*xrem + tail) * 128 + row-in-block] (* D for opart)
+  int xrbs, xwhole, xrem;
 };
 
 struct BwdArgs {

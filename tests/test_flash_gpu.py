@@ -306,3 +306,41 @@ def test_bf16_reduction_of_gathered_grads_bounded(gpu):
     print(f"bf16 ring reduction rel err {e16:.3e}, fp32 reduction {e32:.3e}")
     assert e32 <= 1e-2
     assert e16 <= 1.5e-2
+
+
+@pytest.mark.parametrize("prescaled", [False, True])
+def test_flash_head_heavy_grid(gpu, prescaled):
+    """Whole-GPU forward with the head-heavy grid (bindings.cpp head_heavy_plan): each XCD runs
+    its row blocks whole and splits only its last ones into column pieces (compact partials +
+    flash_fwd_combine_tail).  R = 65 row blocks per head, 8 heads: 64 whole + 1 split tail block
+    per XCD.  Checked against the fp32 reference, against the uniform nsplit = 1 launch, and a
+    fully masked row inside a tail block must come out NaN."""
+    from xdot.ops import flash
+
+    B, R, T, H, D = 1, 65 * 128, 2048, 8, 64
+    C = H * D
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rows = torch.randn(B, R, C, generator=g).to(gpu, torch.bfloat16)
+    kc = torch.randn(1, B, T, C, generator=g).to(gpu, torch.bfloat16)
+    vc = torch.randn(1, B, T, C, generator=g).to(gpu, torch.bfloat16)
+    mask = torch.rand(B, R, T, generator=g) < 0.3
+    mask[:, :, :64] = True          # fully masked tiles
+    mask[..., T - 1] = False
+    mask[0, 64 * 128 + 9] = True    # a fully masked row in the split tail block
+    mask = mask.to(gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    rk = flash.prescale(rows, scale) if prescaled else rows
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    out, lse = flash.fwd(rk, kb, vb, mk, H, scale, prescaled=prescaled)          # head-heavy (auto)
+    o1, l1 = flash.fwd(rk, kb, vb, mk, H, scale, nsplit=1, prescaled=prescaled)  # uniform, whole blocks
+    dead = 64 * 128 + 9
+    assert torch.isnan(out[0, dead]).all() and torch.isnan(o1[0, dead]).all()
+    keep = torch.ones(R, dtype=torch.bool, device=gpu)
+    keep[dead] = False
+    _, _, _, ref_o, ref_lse = _ref(rows, kc, vc, mask, H, scale)
+    _close("fwd out", out[:, keep], ref_o[:, keep], 1e-2)
+    assert (lse[..., keep] - ref_lse[..., keep]).abs().max().item() < 1e-2
+    # whole blocks are bitwise the uniform launch's; tail rows agree to bf16 rounding
+    assert torch.equal(out[:, : 64 * 128], o1[:, : 64 * 128])
+    assert (out[:, keep].float() - o1[:, keep].float()).abs().max().item() < 2e-2
