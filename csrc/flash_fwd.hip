@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 // merge column-split partials: lse = log Σ_s e^{lse_s}, O = Σ_s e^{lse_s - lse} O_s.
 // A split that saw only masked columns has lse_s = -inf and contributes nothing; a row with
 // every split -inf is fully masked and yields NaN like the unsplit kernel.
-constexpr int CMB_MAX = 12;  // slots merged with all loads in flight (more: a per-slot loop)
+constexpr int CMB_MAX = 16;  // slots merged with all loads in flight (more: a per-slot loop)
 
 template <int DT, int D>
 __global__ __launch_bounds__(256) void flash_fwd_combine(FwdArgs a) {
