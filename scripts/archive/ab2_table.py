@@ -1,4 +1,4 @@
-"""Summarise scripts/env_ab2.sh: per arm, kernel medians (bench_flash) and step medians."""
+"""Summarise scripts/archive/env_ab2.sh: per arm, kernel medians (bench_flash) and step medians."""
 import collections
 import json
 import statistics

@@ -1,4 +1,4 @@
-"""Summarise scripts/ab.sh logs: per kernel, min and median of the per-run medians."""
+"""Summarise scripts/archive/ab.sh logs: per kernel, min and median of the per-run medians."""
 import collections
 import json
 import statistics

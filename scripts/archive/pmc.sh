@@ -1,6 +1,6 @@
 #!/bin/bash
 # Collect PMC counter groups for a command, one rocprofv3 pass per group (no tracing domains).
-#   bash scripts/pmc.sh <out-tag> "<grp1 counters>" "<grp2 counters>" ... -- <python args...>
+#   bash scripts/archive/pmc.sh <out-tag> "<grp1 counters>" "<grp2 counters>" ... -- <python args...>
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$1; shift
 groups=()

@@ -1,4 +1,4 @@
-"""Summarise scripts/so_step_ab2.sh: per variant, kernel medians (bench_flash) and step medians."""
+"""Summarise scripts/archive/so_step_ab2.sh: per variant, kernel medians (bench_flash) and step medians."""
 import collections
 import json
 import os

@@ -1,4 +1,4 @@
-"""Summarise scripts/so_ab.sh: per variant, kernel medians (bench_flash) per shape."""
+"""Summarise scripts/archive/so_ab.sh: per variant, kernel medians (bench_flash) per shape."""
 import collections
 import json
 import statistics

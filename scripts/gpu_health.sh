@@ -6,6 +6,7 @@ set -o pipefail
 TAG=${1:-health}
 O=gpurun_out/$TAG
 mkdir -p $O
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke-ok')" > $O/smoke.log 2>&1 || exit $?
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf > $O/pytest.log 2>&1
 rc=$?; echo "pytest exit $rc" >> $O/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -1,4 +1,4 @@
-"""Median table of an alternating bench_rank A/B log (scripts/gpu_overlap_ab.sh)."""
+"""Median table of an alternating bench_rank A/B log (scripts/archive/gpu_overlap_ab.sh)."""
 import json
 import statistics
 import sys
