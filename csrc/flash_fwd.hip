@@ -244,7 +244,15 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       // Written in issue order and fenced with sched_barrier so the compiler keeps the MFMA /
       // VALU interleave (it otherwise clusters the MFMAs); operand reads run two MFMAs ahead.
       constexpr int NA = 2 * KS, NB = 4 * DB;
+      // D >= 96: block A's gaps cannot hold all 32 exps (2.67 v_exp + 1.33 cvt + a row read per
+      // 32-cycle MFMA gap is ~39 issue cycles): the exps of P's last 8 columns (pf[3]) move into
+      // block B, whose MFMAs run k-step-major so pf[3] is first needed at MFMA 3*DB >= 9
+      constexpr int NX = DB >= 3 ? 8 : 0, JA = 32 - NX;
       u32x4 pf[4];
+      auto p_of = [&](int j) {
+        sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
+        if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
+      };
       {
         u32x4 q0 = row_frag<D>(nxt, 0, 0, L), q1 = row_frag<D>(nxt, (1 / KS) * 32, 1 % KS, L);
 #pragma unroll
@@ -254,10 +262,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
           if (i + 2 < NA) q2 = row_frag<D>(nxt, ((i + 2) / KS) * 32, (i + 2) % KS, L);
           sn[tt] = mfma32<DT>::run(q0, kf[ks], ks == 0 ? (PS ? mseed : f32x16{}) : sn[tt]);
 #pragma unroll
-          for (int j = (i * 32) / NA; j < ((i + 1) * 32) / NA; ++j) {
-            sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
-            if ((j & 7) == 7) pf[j >> 3] = acc_to_frag<DT>(sc[j >> 4], (j >> 3) & 1);
-          }
+          for (int j = (i * JA) / NA; j < ((i + 1) * JA) / NA; ++j) p_of(j);
           __builtin_amdgcn_sched_barrier(0);
           q0 = q1;
           q1 = q2;
@@ -267,15 +272,26 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       // adds: packed v_pk_add_f32 pairs measured 0.5-3 % slower beside the MFMAs) ----
       float ls = 0.f;
       {
-        u32x4 v0 = tr_frag<D>(cur + IMG, 0, 0, L), v1 = tr_frag<D>(cur + IMG, 16, 0, L);
+        // MFMA i of block B: (k-step, d block) = d-block-major, or k-step-major when NX > 0
+        auto kb_of = [&](int i) { return NX ? i / DB : (i & 3); };
+        auto db_of = [&](int i) { return NX ? i % DB : (i >> 2); };
+        u32x4 v0 = tr_frag<D>(cur + IMG, kb_of(0) * 16, db_of(0) * 32, L);
+        u32x4 v1 = tr_frag<D>(cur + IMG, kb_of(1) * 16, db_of(1) * 32, L);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-          const int db = i >> 2, k4 = i & 3;
+          const int db = db_of(i), k4 = kb_of(i);
           u32x4 v2 = v1;
-          if (i + 2 < NB) v2 = tr_frag<D>(cur + IMG, ((i + 2) & 3) * 16, ((i + 2) >> 2) * 32, L);
+          if (i + 2 < NB) v2 = tr_frag<D>(cur + IMG, kb_of(i + 2) * 16, db_of(i + 2) * 32, L);
           o[db] = mfma32<DT>::run(v0, pf[k4], o[db]);
+          if (i < NX) p_of(JA + i);
+          // row sums: columns < JA spread over every gap, the moved ones after their exps
 #pragma unroll
-          for (int j = (i * 32) / NB; j < ((i + 1) * 32) / NB; ++j) ls += sc[j >> 4][j & 15];
+          for (int j = (i * JA) / NB; j < ((i + 1) * JA) / NB; ++j) ls += sc[j >> 4][j & 15];
+          if (NX && i >= NX) {
+#pragma unroll
+            for (int j = JA + ((i - NX) * NX) / (NB - NX); j < JA + ((i - NX + 1) * NX) / (NB - NX); ++j)
+              ls += sc[j >> 4][j & 15];
+          }
           asm volatile("" : "+v"(ls));  // keeps the adds here (LLVM would sink them past the branch)
           __builtin_amdgcn_sched_barrier(0);
           v0 = v1;
