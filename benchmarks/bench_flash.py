@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--mask-density", type=float, default=0.0,
                     help="with --mask: fraction of randomly masked entries (0: all-False)")
     ap.add_argument("--nsplit", type=int, default=0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--fp32-mode", default=None, choices=["split", "exact"],
+                    help="fp32 kernel family (default: XDOT_FP32_MODE)")
     ap.add_argument("--no-prescale", action="store_true",
                     help="kernels scale every score (default: pre-scaled rows + seeded accumulators, the module's path)")
     ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
@@ -61,17 +64,22 @@ def main():
     R = a.R or T
     C = H * D
     g = torch.Generator(device=dev).manual_seed(0)
-    rows = torch.randn(B, R, C, device=dev, dtype=torch.bfloat16, generator=g)
-    qv = torch.randn(B, T, 2 * C, device=dev, dtype=torch.bfloat16, generator=g)
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    if a.fp32_mode is not None:
+        from xdot.utils.env import FLAGS
+
+        FLAGS.fp32_mode = a.fp32_mode
+    rows = torch.randn(B, R, C, device=dev, dtype=dt, generator=g)
+    qv = torch.randn(B, T, 2 * C, device=dev, dtype=dt, generator=g)
     kc, vc = qv[..., :C], qv[..., C:]
-    do = torch.randn(B, R, C, device=dev, dtype=torch.bfloat16, generator=g)
+    do = torch.randn(B, R, C, device=dev, dtype=dt, generator=g)
     mask = None
     if a.mask:
         mask = torch.rand(B, R, T, device=dev, generator=g) < a.mask_density
         mask[..., 0] = False
     mk = flash.prepare_mask(mask, B, R, T)
     scale = 1.0 / math.sqrt(D)
-    ps = not a.no_prescale
+    ps = not a.no_prescale and dt != torch.float32
     rk = flash.prescale(rows, scale) if ps else rows
     out, lse = flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps)
     dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps)

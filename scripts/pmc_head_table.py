@@ -11,7 +11,8 @@ for f in sorted(glob.glob(d + "/g*/pmc_counter_collection.csv")):
     per = collections.defaultdict(float)  # (kernel, dispatch, counter) -> summed value
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if "flash_" not in k or ("fwd_kernel" not in k and "cols" not in k and "rows_kernel" not in k):
+        if not any(x in k for x in ("flash_", "fa3::", "fa32::")) or (
+                "fwd_kernel" not in k and "cols" not in k and "rows_kernel" not in k):
             continue
         per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (k, _, c), v in per.items():

@@ -182,3 +182,24 @@ def test_extension_schema_loads_on_cpu():
                         "print(len([n for n in dir(torch.ops.xdot) if not n.startswith('_')]))"],
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
+
+
+def test_fp32_mode_codes():
+    """XDOT_FP32_MODE -> kernel family code of fp32 operands (16-bit dtypes always 0)."""
+    import torch
+
+    from xdot.ops import flash
+    from xdot.utils.env import FLAGS
+
+    assert flash.fp32_code(torch.float32, "split") == 1
+    assert flash.fp32_code(torch.float32, "exact") == 0
+    assert flash.fp32_code(torch.bfloat16, "split") == 0
+    old = FLAGS.fp32_mode
+    try:
+        FLAGS.fp32_mode = "exact"
+        assert flash.fp32_code(torch.float32) == 0
+        FLAGS.fp32_mode = "bogus"
+        with pytest.raises(ValueError):
+            flash.fp32_code(torch.float32)
+    finally:
+        FLAGS.fp32_mode = old
