@@ -313,12 +313,12 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // backward, row side: dK = scale · Σ_cols dS · Q_cols.  4 waves x 32 rows, column split.
-// One LDS stage (the next tile waits in registers).
+// Two LDS stages (the next tile is stored while the current one is read: one barrier per tile).
 template <int D> struct RowsL {
   using Q = Img<D, true, true>;
   using V = Img<D, true, false>;
   static constexpr int STAGE = Q::BYTES + V::BYTES;
-  static constexpr int LDS = STAGE;
+  static constexpr int LDS = 2 * STAGE;
 };
 
 template <int D>
@@ -357,21 +357,22 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
 
-  const char* qi = smem;
-  const char* vi = smem + RL::Q::BYTES;
   Tile<D> tq, tv;
   if (kt_beg < kt_end) {
     tq.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
     tv.load(vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
-  }
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
     tq.template store<true, true>(smem, tid);
     tv.template store<true, false>(smem + RL::Q::BYTES, tid);
     __syncthreads();
-    if (kt + 1 < kt_end) {
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    if (more) {
       tq.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
       tv.load(vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
     }
+    const char* qi = smem + ((kt - kt_beg) & 1) * RL::STAGE;
+    const char* vi = qi + RL::Q::BYTES;
     int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
@@ -391,6 +392,11 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
         s[r] = ex2(x) * (dp[r] - dlt);  // dSᵀ / scale
       }
       trprod<D, true, true>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+    }
+    if (more) {
+      char* nx = smem + ((kt + 1 - kt_beg) & 1) * RL::STAGE;
+      tq.template store<true, true>(nx, tid);
+      tv.template store<true, false>(nx + RL::Q::BYTES, tid);
     }
     __syncthreads();
   }
