@@ -126,10 +126,12 @@ def all_chunk_into(out: torch.Tensor, left: torch.Tensor, chunk: torch.Tensor, d
     if _ext.use_hip(out, left, chunk) and hip_dtype_ok(left, chunk) and out.dtype in _HIP_IN:
         left, sA, lda = _m3(left)
         chunk, sBj, sBp, ldb = _m4(chunk)
-        out, sC, ldc = _m3(out)
-        strided_gemm(left, chunk, out[..., d0:], M=R, N=c, K=R, nseg=N, nb1=1, nb2=Pn,
+        out_, sC, ldc = _m3(out)
+        strided_gemm(left, chunk, out_[..., d0:], M=R, N=c, K=R, nseg=N, nb1=1, nb2=Pn,
                      lda=lda, ldb=ldb, ldc=ldc, sA2=sA, sB2=sBp, sC2=sC,
                      sAseg=R, sBseg=sBj, a_mc=False, b_mc=True)
+        if out_ is not out:  # _m3 made a contiguous temporary: write the columns back
+            out[..., d0:d0 + c].copy_(out_[..., d0:d0 + c])
         return
     ct = torch.promote_types(left.dtype, chunk.dtype)
     splits = left.reshape(Pn, R, N, R).permute(2, 0, 1, 3).to(ct)     # no stack copy
