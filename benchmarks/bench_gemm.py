@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cases", default="nt,all,tn,nt_small,all3,tn3")
-    ap.add_argument("--path", default="auto", choices=["auto", "v1", "v2"],
+    ap.add_argument("--path", default="auto", choices=["auto", "v1", "v2", "v3"],
                     help="xdot kernel: auto (library route for plain large products), v1 128x128, v2 256x256")
     a = ap.parse_args()
     from xdot.ops.gemm import strided_gemm
@@ -40,7 +40,7 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     path = a.path
-    pc = {"auto": 0, "v1": 1, "v2": 2}[path]
+    pc = {"auto": 0, "v1": 1, "v2": 2, "v3": 3}[path]
     for case in a.cases.split(","):
         if case in ("nt", "nt_small"):
             M = N = 75000 if case == "nt" else 25000

@@ -189,7 +189,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;
   if (v2 && a_mc) v2 = M % 8 == 0;
   if (v2 && b_mc) v2 = N % 8 == 0;
-  if (v2 && mode != 2) {
+  if (v2 && mode != 2 && mode != 3) {
     // auto: enough 256x256 tiles (>= 32 per batch entry or >= 512 overall) -- small outputs
     // batched over K slabs (the split-K weight gradients of xdot.ops.linear) keep the 128x128
     // kernel, which fills the GPU without a second split.  Skinny outputs (one side 64..191,
@@ -199,6 +199,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
     v2 = M >= 64 && N >= 64 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
   }
+  TORCH_CHECK(mode != 3 || (v2 && K > 0), "xdot.gemm: path 3 (gemm3) needs 16-bit operands with aligned layouts");
   if (v2 && K > 0) {
     // split-K: fewest k-slices S minimising ceil(items / CUs) / S (idle CUs of the last round),
     // each slice >= 4 k-tiles of 64, with a 3 % charge per slice for the fp32 partial round trip
@@ -213,6 +214,13 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     }
     at::Tensor ws;
     if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
+    if (mode == 3) {
+      const int rc3 = xdot_gemm3_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
+                                        a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
+      TORCH_CHECK(rc3 == 0, "xdot.gemm: path 3 (gemm3) not eligible for this call (", rc3, ")");
+      check_launch(hipGetLastError(), "gemm3");
+      return;
+    }
     const int rc2 = xdot_gemm2_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
                                       a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
     if (rc2 == 0) {

@@ -542,3 +542,25 @@ extern "C" int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in
 #undef G2_DT
   return -1;
 }
+
+extern "C" int xdot_num_cus() { return xdot::num_cus(); }
+
+// C = alpha * sum_s ws[s] + beta * C for a split-K GEMM's fp32 slices (slices summed in order)
+extern "C" int xdot_gemm_reduce_launch(const xdot::GemmArgs* ap, const float* ws, int splits, int batches, int dt_out,
+                                       hipStream_t st) {
+  using namespace xdot;
+  const GemmArgs& a = *ap;
+  const int64_t n = (int64_t)a.M * a.N * batches;
+  const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && a.sC1 % 4 == 0 && a.sC2 % 4 == 0 &&
+                  (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
+#define RED(DT)                                                                                                      \
+  if (dt_out == DT) {                                                                                                \
+    if (v4) hipLaunchKernelGGL((gemm2_reduce4<DT>), dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches); \
+    else hipLaunchKernelGGL((gemm2_reduce<DT>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, ws, splits, batches);        \
+    return 0;                                                                                                        \
+  }
+  RED(DT_BF16) RED(DT_F16) RED(DT_F32)
+#undef RED
+  return -1;
+}
+

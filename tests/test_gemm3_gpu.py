@@ -1,0 +1,92 @@
+"""Numerics of the 8-phase 16x16x32 GEMM (csrc/gemm3.hip) against fp32 PyTorch (GPU only).
+
+Every call forces the v3 path (``path=3`` raises if the kernel does not take the call): all four
+operand layouts, edge tiles shifted inside the matrix, K tails (zero-filled DMA lanes), K
+segments, split-K slices, fp32 and 16-bit outputs, persistent workgroups crossing items.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HALF = [torch.bfloat16, torch.float16]
+LAYOUTS = [(False, False), (False, True), (True, False), (True, True)]
+
+
+def _tol(dt, k):
+    return (2e-2 if dt == torch.bfloat16 else 4e-3) * math.sqrt(max(k, 1) / 64)
+
+
+def _run(gpu, dt, a_mc, b_mc, M, N, K, nseg=1, batches=2, alpha=1.0, out_dt=torch.float32, seed=0, path=3):
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(seed + M * 7 + N + K)
+    A = torch.randn(batches, nseg, *((K, M) if a_mc else (M, K)), generator=g).to(gpu, dt)
+    B = torch.randn(batches, nseg, *((K, N) if b_mc else (N, K)), generator=g).to(gpu, dt)
+    C = torch.full((batches, M, N), float("nan"), device=gpu, dtype=out_dt)
+    strided_gemm(A, B, C, M=M, N=N, K=K, nseg=nseg, nb2=batches, lda=(M if a_mc else K),
+                 ldb=(N if b_mc else K), ldc=N, sA2=nseg * M * K, sB2=nseg * N * K, sC2=M * N,
+                 sAseg=M * K, sBseg=N * K, a_mc=a_mc, b_mc=b_mc, alpha=alpha, path=path)
+    Af, Bf = A.float(), B.float()
+    opA = Af.transpose(-1, -2) if a_mc else Af        # (b, s, M, K)
+    opB = Bf if b_mc else Bf.transpose(-1, -2)        # (b, s, K, N)
+    ref = alpha * torch.matmul(opA, opB).sum(1)
+    assert torch.isfinite(C.float()).all(), "unwritten output elements"
+    err = (C.float() - ref).abs().max().item()
+    tol = _tol(dt, K * nseg) * max(1.0, ref.abs().max().item() / 4)
+    if out_dt != torch.float32:
+        tol += ref.abs().max().item() * (2 ** -7 if out_dt == torch.bfloat16 else 2 ** -10)
+    assert err <= tol, (err, tol)
+    return C
+
+
+@pytest.mark.parametrize("dt", HALF)
+@pytest.mark.parametrize("a_mc,b_mc", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 264, 96), (776, 1000, 40), (264, 520, 200), (256, 264, 8)])
+def test_gemm3_layouts_tails(gpu, dt, a_mc, b_mc, M, N, K):
+    _run(gpu, dt, a_mc, b_mc, M, N, K, alpha=0.5)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", LAYOUTS)
+@pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
+def test_gemm3_segments(gpu, a_mc, b_mc, out_dt):
+    """3 K segments with a K tail each: the k-tile stream crosses segment boundaries"""
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 512, 264, 104, nseg=3, alpha=0.25, out_dt=out_dt)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", [(False, False), (True, True), (False, True)])
+@pytest.mark.parametrize("K", [4096, 4104])
+def test_gemm3_split_k(gpu, a_mc, b_mc, K):
+    """one 256x256 tile per batch and a long K: the dispatcher splits K (fp32 slices + reduce)"""
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 256, 256, K, batches=1, alpha=2.0, out_dt=torch.bfloat16)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", LAYOUTS)
+def test_gemm3_persistent_many_items(gpu, a_mc, b_mc):
+    """405 items on <= 256 workgroups: each persistent workgroup crosses item boundaries (shifted
+    edge tiles, K tails, segments, batches) with the DMA stream running on"""
+    _run(gpu, torch.bfloat16, a_mc, b_mc, 2056, 2056, 200, nseg=2, batches=5, alpha=0.5, out_dt=torch.bfloat16)
+
+
+def test_gemm3_odd_n_kc(gpu):
+    """k-contiguous B with N % 8 != 0 (nt's per-rank column count at T/N = 3125): the last
+    column tile is shifted by a non-multiple of 8 and stored through unaligned 16-byte stores"""
+    _run(gpu, torch.bfloat16, False, False, 600, 3125, 96, batches=1, out_dt=torch.bfloat16)
+
+
+def test_gemm3_matches_v2_bitwise_order(gpu):
+    """same products as the v2 kernel within rounding (independent implementations)"""
+    c3 = _run(gpu, torch.bfloat16, False, True, 1024, 768, 1000, batches=1, out_dt=torch.float32, path=3)
+    c2 = _run(gpu, torch.bfloat16, False, True, 1024, 768, 1000, batches=1, out_dt=torch.float32, path=2)
+    assert (c3 - c2).abs().max().item() < 1e-2
+
+
+def test_gemm3_rejects_beta(gpu):
+    from xdot.ops.gemm import strided_gemm
+
+    A = torch.randn(256, 64, device=gpu, dtype=torch.bfloat16)
+    C = torch.zeros(256, 256, device=gpu, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        strided_gemm(A, A, C, M=256, N=256, K=64, lda=64, ldb=64, ldc=256, beta=1.0, path=3)
