@@ -82,6 +82,47 @@ int gemm_lib() {
 // kernel; the xdot kernels stay ahead on skinny long-K bf16 products (all3: 25000 x 768 x
 // 75000, split-K: 1.4x) and own every layout a single strided batch cannot express (two batch
 // levels, scattered K segments, mixed dtypes, small products).
+// split-K: fewest k-slices S minimising ceil(items / CUs) / S (idle CUs of the last round),
+// each slice >= 4 k-tiles of 64, with a 3 % charge per slice for the fp32 partial round trip
+int64_t pick_splits(int64_t tiles, int64_t kt64) {
+  const int64_t ncu = 256;
+  int64_t S = 1;
+  double best = 1e300;
+  for (int64_t s = 1; s <= 64 && (s == 1 || kt64 / s >= 4); ++s) {
+    const double cost = (double)((tiles * s + ncu - 1) / ncu) / (double)s * (1.0 + 0.03 * (s - 1));
+    if (cost < best * 0.98) { best = cost; S = s; }
+  }
+  return S;
+}
+
+// XDOT_FP32_MODE: split (default) = large fp32 products run as three bf16 products (hi/lo
+// halves) on gemm3; exact = the exact-fp32 MFMA kernel / library GEMM
+int fp32_split() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_FP32_MODE");
+    return (e && e[0] == 'e') ? 0 : 1;
+  }();
+  return v;
+}
+
+// XDOT_GEMM3: 1 (default) = the automatic path tries the 8-phase kernel first (csrc/gemm3.hip)
+int gemm3_auto() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM3");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+// XDOT_GEMM3_ROTATE: 1 (default) = gemm3 staggers the workgroups' first items (see csrc/gemm3.hip)
+int gemm3_rotate() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_GEMM3_ROTATE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 bool gemm_library(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K,
                   int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA1,
                   int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1, int64_t sC2, int64_t sAseg, int64_t sBseg,
@@ -180,6 +221,49 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   // alignment rules and whose output fills 256-wide tiles; split-K when the tiles alone would
   // leave CUs idle.  path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call)
   const int mode = (int)path;
+  // fp32 operands on the bf16 matrix pipe (XDOT_FP32_MODE=split, the default; path 4 forces it):
+  // hi/lo bf16 copies, three bf16 products in one gemm3 call (csrc/gemm3.hip, split3_kernel)
+  if (A.scalar_type() == at::kFloat && (mode == 4 || (mode == 0 && fp32_split() && gemm3_auto()))) {
+    const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
+    const bool big = 2.0 * (double)M * N * K * nseg * nb1 * nb2 >= 2e9 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
+    const bool ok = beta == 0.0 && K > 0 && M >= 256 && N >= 256 && K % 8 == 0 && (!a_mc || M % 8 == 0) &&
+                    (!b_mc || N % 8 == 0) && C.scalar_type() == at::kFloat && nb1 * nb2 * 3 * nseg <= 65535;
+    TORCH_CHECK(mode != 4 || ok, "xdot.gemm: path 4 (split fp32) not eligible for this call");
+    if (ok && (mode == 4 || big)) {
+      const int64_t Ra = a_mc ? K : M, Ca = a_mc ? M : K, Rb = b_mc ? K : N, Cb = b_mc ? N : K;
+      at::Tensor a3 = at::empty({nb1 * nb2 * 3 * nseg * Ra * Ca}, A.options().dtype(at::kBFloat16));
+      at::Tensor b3 = at::empty({nb1 * nb2 * 3 * nseg * Rb * Cb}, A.options().dtype(at::kBFloat16));
+      hipStream_t st = cur_stream(A);
+      // A' = [hi, lo, hi], B' = [hi, hi, lo]: hi.hi + lo.hi + hi.lo
+      xdot_split3_launch(A.data_ptr<float>(), a3.data_ptr(), sA1, sA2, sAseg, lda, (int)nb1, (int)nb2, (int)nseg,
+                         (int)Ra, (int)Ca, 0b010, st);
+      xdot_split3_launch(B.data_ptr<float>(), b3.data_ptr(), sB1, sB2, sBseg, ldb, (int)nb1, (int)nb2, (int)nseg,
+                         (int)Rb, (int)Cb, 0b100, st);
+      check_launch(hipGetLastError(), "split3");
+      xdot::GemmArgs g3a = g;
+      g3a.A = a3.data_ptr();
+      g3a.B = b3.data_ptr();
+      g3a.nseg = (int)(3 * nseg);
+      g3a.lda = Ca;
+      g3a.ldb = Cb;
+      g3a.sAseg = Ra * Ca;
+      g3a.sBseg = Rb * Cb;
+      g3a.sA2 = 3 * nseg * Ra * Ca;
+      g3a.sA1 = nb2 * g3a.sA2;
+      g3a.sB2 = 3 * nseg * Rb * Cb;
+      g3a.sB1 = nb2 * g3a.sB2;
+      const int64_t tiles = tpb * nb1 * nb2;
+      const int64_t kt64 = 3 * nseg * ((K + 63) / 64);
+      const int64_t S = pick_splits(tiles, kt64);
+      at::Tensor ws;
+      if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
+      const int rc3 = xdot_gemm3_launch(&g3a, (int)(nb1 * nb2), xdot::DT_BF16, xdot::DT_F32, a_mc, b_mc, (int)S,
+                                        S > 1 ? ws.data_ptr<float>() : nullptr, nullptr, st);
+      TORCH_CHECK(rc3 == 0, "xdot.gemm: split fp32 gemm3 launch declined (", rc3, ")");
+      check_launch(hipGetLastError(), "gemm3 (split fp32)");
+      return;
+    }
+  }
   if (mode == 0 && gemm_lib() &&
       gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
                    b_mc, alpha, beta))
@@ -206,20 +290,26 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb1 * nb2;
     const int64_t kt64 = nseg * ((K + 63) / 64);
     const int64_t ncu = 256;
-    int64_t S = 1;
-    double best = 1e300;
-    for (int64_t s = 1; s <= 64 && (s == 1 || kt64 / s >= 4); ++s) {
-      const double cost = (double)((tiles * s + ncu - 1) / ncu) / (double)s * (1.0 + 0.03 * (s - 1));
-      if (cost < best * 0.98) { best = cost; S = s; }
-    }
+    const int64_t S = pick_splits(tiles, kt64);
     at::Tensor ws;
     if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
-    if (mode == 3) {
+    // v3 (8-phase 16x16x32, csrc/gemm3.hip) first: beta = 0, M and N >= 256; it declines
+    // (-3) the rest, which the v2 kernel takes
+    if (mode == 3 || (mode == 0 && gemm3_auto())) {
+      // rotation (staggered epilogues) when every workgroup walks >= 2 items of short K, i.e.
+      // when the output stream is a large share of the traffic
+      at::Tensor rws;
+      const int64_t items = tiles * S;
+      if (gemm3_rotate() && items >= 2 * ncu && kt64 / S <= 48)
+        rws = at::empty({(int64_t)xdot_gemm3_rotation_floats()}, A.options().dtype(at::kFloat));
       const int rc3 = xdot_gemm3_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
-                                        a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
-      TORCH_CHECK(rc3 == 0, "xdot.gemm: path 3 (gemm3) not eligible for this call (", rc3, ")");
-      check_launch(hipGetLastError(), "gemm3");
-      return;
+                                        a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr,
+                                        rws.defined() ? rws.data_ptr<float>() : nullptr, cur_stream(A));
+      TORCH_CHECK(mode != 3 || rc3 == 0, "xdot.gemm: path 3 (gemm3) not eligible for this call (", rc3, ")");
+      if (rc3 == 0) {
+        check_launch(hipGetLastError(), "gemm3");
+        return;
+      }
     }
     const int rc2 = xdot_gemm2_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
                                       a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));

@@ -34,6 +34,9 @@ namespace xdot {
 namespace g3 {
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+#ifndef G3_STORE_AUX
+#define G3_STORE_AUX 0  // cache policy of the output stores (A/B knob of scripts/gemm3_ab.sh)
+#endif
 constexpr int HALF = 16384;       // one half-tile image (128 x 64 x 2 B)
 constexpr int SLOT = 4 * HALF;    // [A 0-127 | A 128-255 | B 0-127 | B 128-255]
 constexpr int LDS = 2 * SLOT;     // 128 KiB: two k-tiles
@@ -80,7 +83,8 @@ __device__ __forceinline__ void swap16(uint32_t& x, uint32_t& y) {
 // Work item = (split zs, batch z, output tile).  Walked by a persistent grid: workgroup slot s
 // takes items s, s + G, ...; the LDS ring runs straight across items.
 template <int DTI, int DTO, bool A_MC, bool B_MC, int EPI>
-__global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restrict__ ws, int W, int batches, int nsplit) {
+__global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restrict__ ws, float* __restrict__ rws, int W, int batches,
+                                                   int nsplit) {
   using namespace g3;
   using fa::smem;
   using fa::lds_addr;
@@ -100,12 +104,15 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   const int ktiles = (p.K + BK - 1) / BK;
   const int ntot = ktiles * p.nseg;
   const int ntile = p.tiles_m * p.tiles_n;
-  constexpr int GM = 8;
-  const int gsz = GM * p.tiles_n;
+  constexpr int GM = 8, SB = 32;
   const int64_t lda2 = p.lda * 2, ldb2 = p.ldb * 2;
   // byte steps of one k-tile / one half-tile inside an operand
   const int64_t a_kstep = A_MC ? 64 * lda2 : 128, b_kstep = B_MC ? 64 * ldb2 : 128;
   const int64_t a_half = A_MC ? 256 : 128 * lda2, b_half = B_MC ? 256 : 128 * ldb2;
+  // byte jump from the last k-tile of a K segment to the first of the next
+  const int64_t a_segjump = 2 * p.sAseg - (int64_t)(ktiles - 1) * a_kstep;
+  const int64_t b_segjump = 2 * p.sBseg - (int64_t)(ktiles - 1) * b_kstep;
+  const int kl_t = p.K - (ktiles - 1) * BK;  // valid k of every segment's last k-tile
 
   struct Item {
     int m0, n0, mo, no, z, zs, tb, te;
@@ -117,9 +124,20 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     const int zz = L / ntile, tl = L % ntile;
     it.zs = zz / batches;
     it.z = zz % batches;
-    const int gi = tl / gsz, first_m = gi * GM;
-    const int gm_n = min(GM, p.tiles_m - first_m);
-    const int tm = first_m + (tl % gsz) % gm_n, tn = (tl % gsz) / gm_n;
+    // tile order: super-blocks of SB x SB tiles (row-major over the super-block grid), inside
+    // one super-block groups of GM m-tiles sweeping its n-tiles.  A super-block's panels are
+    // re-read while at most SB^2 x 128 KiB of output streams out (<= 128 MiB: they stay in the
+    // 256 MiB Infinity Cache; a whole-row sweep at N = 75000 wrote 300 MB between two uses)
+    const int sbr = tl / (SB * p.tiles_n);
+    const int sbm = min(SB, p.tiles_m - sbr * SB);
+    const int r1 = tl - sbr * SB * p.tiles_n;
+    const int sbc = r1 / (sbm * SB);
+    const int sbn = min(SB, p.tiles_n - sbc * SB);
+    const int r2 = r1 - sbc * sbm * SB;
+    const int gi = r2 / (GM * sbn);
+    const int gm_n = min(GM, sbm - gi * GM);
+    const int r3 = r2 - gi * GM * sbn;
+    const int tm = sbr * SB + gi * GM + r3 % gm_n, tn = sbc * SB + r3 / gm_n;
     it.mo = tm * BM;
     it.no = tn * BN;
     it.m0 = min(it.mo, p.M - BM);  // (an mn-contiguous operand has M / N % 8 == 0: 16-byte DMA sources)
@@ -136,41 +154,59 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   // segment, valid k kl, operand bytes a / b of the k-tile).  Kept small: it lives in SGPRs
   // twice (the k-tiles one and two ahead of the compute side).
   struct Cur {
-    int L, k, te, kt, kl;
+    int L, k, te, kt, kl, wrap;
     const char* a;
     const char* b;
   };
-  auto cur_of = [&](int L) __attribute__((always_inline)) {
+  // k-tile k of item L, its stream segment ending at te (wrap: the first item's rotated-away prefix)
+  auto cur_at = [&](int L, int k, int te, int wrap) __attribute__((always_inline)) {
     Cur c;
     const Item it = item_of(L);
     c.L = L;
-    c.k = it.tb;
-    c.te = it.te;
-    const int seg = c.k / ktiles;
-    c.kt = c.k - seg * ktiles;
-    c.kl = __builtin_amdgcn_readfirstlane(min(BK, p.K - c.kt * BK));
+    c.k = k;
+    c.te = te;
+    c.wrap = wrap;
+    const int seg = k / ktiles;
+    c.kt = k - seg * ktiles;
+    c.kl = c.kt == ktiles - 1 ? kl_t : BK;
     c.a = it.a + 2 * (int64_t)seg * p.sAseg + (int64_t)c.kt * a_kstep;
     c.b = it.b + 2 * (int64_t)seg * p.sBseg + (int64_t)c.kt * b_kstep;
     return c;
   };
-  // the k-tile after c (past the last item: c itself again -- its DMAs are harmless repeats)
+  // Rotation (rws != nullptr): the workgroup starts its first item `rot` k-tiles in and
+  // finishes the skipped prefix after its last item (partial sums parked in rws meanwhile).
+  // Offsets differ across each XCD's 32 slots, so the workgroups' epilogues -- 128 KiB of output
+  // each -- no longer land in one burst that every workgroup then waits out in its next vmcnt.
+  int tb0, te0;
+  {
+    const Item it = item_of(slot0);
+    tb0 = it.tb;
+    te0 = it.te;
+  }
+  const int rot = rws ? (((slot0 & 31) * (te0 - tb0)) >> 5) : 0;
+  // the k-tile after c in the workgroup's stream (after the end: c itself again -- its DMAs
+  // are harmless repeats)
   auto next_of = [&](const Cur& c) __attribute__((always_inline)) {
     if (c.k + 1 < c.te) {
       Cur n = c;
       n.k = c.k + 1;
       if (c.kt + 1 == ktiles) {  // next K segment
         n.kt = 0;
-        n.a = c.a + 2 * p.sAseg - (int64_t)(ktiles - 1) * a_kstep;
-        n.b = c.b + 2 * p.sBseg - (int64_t)(ktiles - 1) * b_kstep;
+        n.a = c.a + a_segjump;
+        n.b = c.b + b_segjump;
       } else {
         n.kt = c.kt + 1;
         n.a = c.a + a_kstep;
         n.b = c.b + b_kstep;
       }
-      n.kl = __builtin_amdgcn_readfirstlane(min(BK, p.K - n.kt * BK));
+      n.kl = n.kt == ktiles - 1 ? kl_t : BK;
       return n;
     }
-    if (c.L + G < W) return cur_of(c.L + G);
+    if (!c.wrap && c.L + G < W) {
+      const Item it = item_of(c.L + G);
+      return cur_at(c.L + G, it.tb, it.te, 0);
+    }
+    if (!c.wrap && rot > 0) return cur_at(slot0, tb0, tb0 + rot, 1);
     return c;
   };
 
@@ -204,7 +240,6 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     }
   }
   // the same for the K-tail k-tile (every segment's tail has kl_t valid k)
-  const int kl_t = p.K - (ktiles - 1) * BK;
   uint32_t oat[2], obt[2];
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
@@ -300,43 +335,80 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   //          by v_permlane16_swap into 8 consecutive columns per lane;
   //   EPI 1: split-K fp32 slices (unscaled; the reduce applies alpha / beta);
   //   EPI 3: fp32 C, beta = 0.
+  // Stores go through buffer descriptors: the 64-bit row base is scalar (one descriptor per
+  // 16-row strip), the lane's 32-bit offset is the same for every strip of every item -- no
+  // per-store 64-bit address registers next to the 128 accumulator registers.
+  const int64_t ldo = EPI == 1 ? (int64_t)p.N : p.ldc;
+  const int voff = EPI == 0 ? (int)((l15 * ldo + 16 * (g & 1) + 8 * (g >> 1)) * 2) : (int)((l15 * ldo + 4 * g) * 4);
   auto epilogue = [&](const Item& it) __attribute__((always_inline)) {
     const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
     const float alpha = p.alpha;
+    const char* cb;
+    if constexpr (EPI == 1)
+      cb = reinterpret_cast<const char*>(ws + ((int64_t)it.zs * batches + it.z) * (int64_t)p.M * p.N + it.n0 + 32 * wn);
+    else
+      cb = reinterpret_cast<const char*>(p.C) + sizeof(TO) * (z1 * p.sC1 + z2 * p.sC2 + it.n0 + 32 * wn);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const int m = it.m0 + 128 * j + 64 * wm + 16 * mt + l15;
+        const int r0 = it.m0 + 128 * j + 64 * wm + 16 * mt;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb + (int64_t)r0 * ldo * (EPI == 0 ? 2 : 4)), 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const int nb = it.n0 + 128 * i + 32 * wn;
           f32x4 x = acc[4 * j + mt][2 * i], y = acc[4 * j + mt][2 * i + 1];
-          if constexpr (EPI == 1) {
-            float* row = ws + ((int64_t)it.zs * batches + it.z) * (int64_t)p.M * p.N + (int64_t)m * p.N;
-            *reinterpret_cast<f32x4*>(row + nb + 4 * g) = x;
-            *reinterpret_cast<f32x4*>(row + nb + 16 + 4 * g) = y;
-          } else if constexpr (EPI == 3) {
-            float* row = reinterpret_cast<float*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)m * p.ldc;
-            *reinterpret_cast<f32x4_ua*>(row + nb + 4 * g) = x * alpha;
-            *reinterpret_cast<f32x4_ua*>(row + nb + 16 + 4 * g) = y * alpha;
-          } else if constexpr (EPI == 0) {
+#ifdef G3_DIAG_NOSTORE
+          if (x[0] == 12345.f && y[1] == -7.f) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff, 0, 0);
+          continue;
+#endif
+          if constexpr (EPI == 0) {
             x *= alpha;
             y *= alpha;
-            TO* dst = reinterpret_cast<TO*>(p.C) + z1 * p.sC1 + z2 * p.sC2 + (int64_t)m * p.ldc +
-                      (nb + 16 * (g & 1) + 8 * (g >> 1));
             uint32_t X0 = fa::pack2<DTO>(x[0], x[1]), X1 = fa::pack2<DTO>(x[2], x[3]);
             uint32_t Y0 = fa::pack2<DTO>(y[0], y[1]), Y1 = fa::pack2<DTO>(y[2], y[3]);
             swap16(X0, Y0);
             swap16(X1, Y1);
-            *reinterpret_cast<u32x4_ua*>(dst) = u32x4{X0, X1, Y0, Y1};
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{X0, X1, Y0, Y1}, rs, voff + 256 * i, 0, G3_STORE_AUX);
+          } else {
+            if constexpr (EPI == 3) {
+              x *= alpha;
+              y *= alpha;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff + 512 * i, 0, G3_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, voff + 512 * i + 64, 0, G3_STORE_AUX);
           }
         }
       }
   };
-  // store instructions one epilogue issues per lane (exact: the vmcnt waits of the k-tile after
-  // an epilogue count them)
+  // rotation: park / pick up the first item's partial sums (wave-private, lane-linear: every
+  // store and load is one coalesced 1 KiB wave access)
+  auto rw_rsrc = [&]() __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(rws + ((int64_t)slot0 * 8 + wave) * (32 * 256), 0, 0x7FFFFFF0, 0x00020000);
+  };
+  auto park = [&]() __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rwr = rw_rsrc();
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rwr, 16 * lane, (a * 4 + b) * 1024, 0);
+  };
+  auto pick_up = [&]() __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rwr = rw_rsrc();
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwr, 16 * lane, (a * 4 + b) * 1024, 0));
+  };
+  // store instructions an epilogue (or a park, 32) issues per lane, at least: the vmcnt waits of
+  // the k-tile after it count them
+#ifdef G3_DIAG_NOSTORE
+  constexpr int EPI_ST = 0;
+#else
   constexpr int EPI_ST = EPI == 0 ? 16 : 32;
+#endif
 
   // ---- prologue: k-tiles 0 (slot 0) and 1 (slot 1) in the steady-state issue order ----
   // steady state, k-tile v (slot v & 1, quadrant order by parity P = v & 1):
@@ -345,7 +417,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   //   q2: reads A quarter 1                          issues A half 0    of k-tile v + 2
   //   q3: no reads                                   issues B half P    of k-tile v + 2
   // waits vmcnt(8) in q0, q1, q3 (after their issue): data waited in phase q is read in q+1.
-  Cur c1 = cur_of(slot0);
+  Cur c1 = cur_at(slot0, tb0 + rot, te0, 0);
   issue(c1, 0, 0);
   issue(c1, 2, 0);
   issue(c1, 3, 0);
@@ -358,13 +430,9 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   if (wm == 1) fa::raw_barrier();  // waves 4-7 run one barrier behind
 
   int cL = slot0;
-  int ck, cte, ckt;  // compute side: flattened k index, its end, k-tile within the segment
-  {
-    const Item it = item_of(cL);
-    ck = it.tb;
-    cte = it.te;
-    ckt = ck % ktiles;
-  }
+  // compute side: flattened k index, its segment end, k-tile within the K segment, and the
+  // stream phase (0: first item after the rotation offset, 1: whole items, 2: the prefix)
+  int ck = tb0 + rot, cte = te0, ckt = ck % ktiles, phase = rot ? 0 : 1;
   bool after_epi = false;
   Cur c2 = c1;
 
@@ -417,18 +485,28 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     after_epi = false;
     if (++ckt == ktiles) ckt = 0;
     if (++ck == cte) {
-      epilogue(item_of(cL));
+      if (phase == 2) return true;  // the prefix: its epilogue follows the loop
+      if (phase == 0) park();
+      else epilogue(item_of(cL));
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      cL += G;
-      if (cL >= W) return true;
-      const Item it = item_of(cL);
-      ck = it.tb;
-      cte = it.te;
-      ckt = ck % ktiles;
       after_epi = true;
+      cL += G;
+      if (cL < W) {
+        const Item it = item_of(cL);
+        ck = it.tb;
+        cte = it.te;
+        phase = 1;
+      } else {
+        if (rot == 0) return true;
+        cL = slot0;
+        ck = tb0;
+        cte = tb0 + rot;
+        phase = 2;
+      }
+      ckt = ck % ktiles;
     }
     return false;
   };
@@ -436,17 +514,22 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     if (step(I0{})) break;
     if (step(I1{})) break;
   }
+  if (phase == 2) {
+    if (EPI == 0 || EPI == 3) fa::wait_vm<0>();  // the parked partial was stored by this lane
+    pick_up();
+    epilogue(item_of(cL));
+  }
   fa::wait_vm<0>();  // repeat DMAs of the final k-tiles must land before the LDS goes away
   if (wm == 0) fa::raw_barrier();  // balance the stagger
 }
 
 template <int DTI, int DTO, bool AMC, bool BMC>
-static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, int ncu, hipStream_t st) {
+static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, float* rws, int ncu, hipStream_t st) {
   const int W = a.tiles_m * a.tiles_n * batches * splits;
   const int G = W < ncu ? W : ncu;
   float* w = splits > 1 ? ws : nullptr;
   // epilogue modes (see the kernel): split-K slices 1, 16-bit C 0, fp32 C 3
-#define G3L(E) hipLaunchKernelGGL((gemm3_kernel<DTI, DTO, AMC, BMC, E>), dim3(G), dim3(g3::NT), g3::LDS, st, a, w, W, batches, splits)
+#define G3L(E) hipLaunchKernelGGL((gemm3_kernel<DTI, DTO, AMC, BMC, E>), dim3(G), dim3(g3::NT), g3::LDS, st, a, w, rws, W, batches, splits)
   if (w) G3L(1);
   else if constexpr (DTO == DT_F32) G3L(3);
   else G3L(0);
@@ -454,11 +537,12 @@ static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, int
 }
 
 template <int DTI, int DTO>
-static void launch3_d(const GemmArgs& a, int batches, bool amc, bool bmc, int splits, float* ws, int ncu, hipStream_t st) {
-  if (!amc && !bmc) return launch3_t<DTI, DTO, false, false>(a, batches, splits, ws, ncu, st);
-  if (!amc && bmc) return launch3_t<DTI, DTO, false, true>(a, batches, splits, ws, ncu, st);
-  if (amc && !bmc) return launch3_t<DTI, DTO, true, false>(a, batches, splits, ws, ncu, st);
-  return launch3_t<DTI, DTO, true, true>(a, batches, splits, ws, ncu, st);
+static void launch3_d(const GemmArgs& a, int batches, bool amc, bool bmc, int splits, float* ws, float* rws, int ncu,
+                      hipStream_t st) {
+  if (!amc && !bmc) return launch3_t<DTI, DTO, false, false>(a, batches, splits, ws, rws, ncu, st);
+  if (!amc && bmc) return launch3_t<DTI, DTO, false, true>(a, batches, splits, ws, rws, ncu, st);
+  if (amc && !bmc) return launch3_t<DTI, DTO, true, false>(a, batches, splits, ws, rws, ncu, st);
+  return launch3_t<DTI, DTO, true, true>(a, batches, splits, ws, rws, ncu, st);
 }
 
 }  // namespace xdot
@@ -468,8 +552,10 @@ extern "C" int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws,
                                        hipStream_t st);
 
 // Eligibility: see the file header.  -3 = shape/layout not eligible (caller falls back).
+// rws: rotation workspace (xdot_gemm3_rotation_floats() floats) or nullptr (no rotation)
+extern "C" int xdot_gemm3_rotation_floats() { return xdot_num_cus() * 256 * 256; }
 extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
-                                 int splits, float* ws, hipStream_t st) {
+                                 int splits, float* ws, float* rws, hipStream_t st) {
   using namespace xdot;
   GemmArgs g = *a;
   if (g.M < g3::BM || g.N < g3::BN || (g.K % 8) != 0 || g.beta != 0.f) return -3;
@@ -479,11 +565,55 @@ extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in
   if (splits < 1 || (splits > 1 && !ws)) return -2;
   const int ncu = xdot_num_cus();
 #define G3_DT(I, O) \
-  if (dt_in == I && dt_out == O) { launch3_d<I, O>(g, batches, a_mc, b_mc, splits, ws, ncu, st); goto done; }
+  if (dt_in == I && dt_out == O) { launch3_d<I, O>(g, batches, a_mc, b_mc, splits, ws, rws, ncu, st); goto done; }
   G3_DT(DT_BF16, DT_BF16) G3_DT(DT_BF16, DT_F32) G3_DT(DT_F16, DT_F16) G3_DT(DT_F16, DT_F32)
 #undef G3_DT
   return -1;
 done:
   if (splits > 1) return xdot_gemm_reduce_launch(&g, ws, splits, batches, dt_out, st);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32 on the bf16 matrix pipe: x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (the residual
+// after lo is ~2^-17 |x|).  A x B ~= hi_A hi_B + lo_A hi_B + hi_A lo_B: three bf16 products, one
+// GEMM with 3x the K segments over compact operand copies A' = [hi, lo, hi], B' = [hi, hi, lo]
+// per (batch, segment): layout [z1][z2][part][seg][R][C] (uniform segment stride R*C).
+namespace xdot {
+struct Split3Args {
+  const float* src;
+  __bf16* dst;
+  int64_t s1, s2, sseg, ld;  // source strides (elements)
+  int nb2, nseg, R, C;       // C: contiguous extent of the source rows
+  int lo_mask;               // bit p: part p holds the lo halves
+  int64_t n;                 // nb1 * nb2 * nseg * R * C
+};
+__global__ __launch_bounds__(256) void split3_kernel(Split3Args a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const int c = (int)(i % a.C);
+  int64_t t = i / a.C;
+  const int r = (int)(t % a.R);
+  t /= a.R;
+  const int seg = (int)(t % a.nseg);
+  t /= a.nseg;
+  const int z2 = (int)(t % a.nb2);
+  const int z1 = (int)(t / a.nb2);
+  const float x = a.src[z1 * a.s1 + z2 * a.s2 + seg * a.sseg + (int64_t)r * a.ld + c];
+  const __bf16 hi = (__bf16)x;
+  const __bf16 lo = (__bf16)(x - (float)hi);
+  const int64_t RC = (int64_t)a.R * a.C;
+  __bf16* d = a.dst + ((int64_t)(z1 * a.nb2 + z2) * 3 * a.nseg + seg) * RC + (int64_t)r * a.C + c;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) d[(int64_t)p * a.nseg * RC] = ((a.lo_mask >> p) & 1) ? lo : hi;
+}
+}  // namespace xdot
+
+extern "C" int xdot_split3_launch(const float* src, void* dst, int64_t s1, int64_t s2, int64_t sseg, int64_t ld,
+                                  int nb1, int nb2, int nseg, int R, int C, int lo_mask, hipStream_t st) {
+  xdot::Split3Args a{src, reinterpret_cast<__bf16*>(dst), s1, s2, sseg, ld, nb2, nseg, R, C, lo_mask,
+                     (int64_t)nb1 * nb2 * nseg * R * C};
+  if (a.n == 0) return 0;
+  hipLaunchKernelGGL(xdot::split3_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
   return 0;
 }

@@ -90,3 +90,43 @@ def test_gemm3_rejects_beta(gpu):
     C = torch.zeros(256, 256, device=gpu, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         strided_gemm(A, A, C, M=256, N=256, K=64, lda=64, ldb=64, ldc=256, beta=1.0, path=3)
+
+
+def _rel_fro(x, ref):
+    return ((x.double() - ref).norm() / ref.norm()).item()
+
+
+@pytest.mark.parametrize("a_mc,b_mc", LAYOUTS)
+@pytest.mark.parametrize("M,N,K,nseg", [(520, 776, 200, 1), (264, 296, 96, 3)])
+def test_gemm3_split_fp32(gpu, a_mc, b_mc, M, N, K, nseg):
+    """fp32 operands as hi/lo bf16 halves, three products on the bf16 pipe (path 4), against an
+    fp64 reference: relative Frobenius error <= 2e-5 (exact fp32 is ~1e-7; bf16 ~3e-3)"""
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    batches = 2
+    A = torch.randn(batches, nseg, *((K, M) if a_mc else (M, K)), generator=g, dtype=torch.float64)
+    B = torch.randn(batches, nseg, *((K, N) if b_mc else (N, K)), generator=g, dtype=torch.float64)
+    C = torch.full((batches, M, N), float("nan"), device=gpu)
+    strided_gemm(A.float().to(gpu), B.float().to(gpu), C, M=M, N=N, K=K, nseg=nseg, nb2=batches,
+                 lda=(M if a_mc else K), ldb=(N if b_mc else K), ldc=N, sA2=nseg * M * K, sB2=nseg * N * K,
+                 sC2=M * N, sAseg=M * K, sBseg=N * K, a_mc=a_mc, b_mc=b_mc, alpha=0.5, path=4)
+    Af, Bf = A.float().double(), B.float().double()   # the fp32 inputs, exactly
+    opA = Af.transpose(-1, -2) if a_mc else Af
+    opB = Bf if b_mc else Bf.transpose(-1, -2)
+    ref = 0.5 * torch.matmul(opA, opB).sum(1)
+    err = _rel_fro(C.cpu(), ref)
+    assert err <= 2e-5, err
+
+
+def test_gemm3_split_fp32_split_k(gpu):
+    """split fp32 with split-K slices (one tile, long K)"""
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn(256, 4104, generator=g, dtype=torch.float64)
+    B = torch.randn(256, 4104, generator=g, dtype=torch.float64)
+    C = torch.empty(256, 256, device=gpu)
+    strided_gemm(A.float().to(gpu), B.float().to(gpu), C, M=256, N=256, K=4104, lda=4104, ldb=4104, ldc=256, path=4)
+    ref = A.float().double() @ B.float().double().t()
+    assert _rel_fro(C.cpu(), ref) <= 2e-5
