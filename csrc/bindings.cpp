@@ -114,15 +114,6 @@ int gemm3_auto() {
   return v;
 }
 
-// XDOT_GEMM3_ROTATE: 1 (default) = gemm3 staggers the workgroups' first items (see csrc/gemm3.hip)
-int gemm3_rotate() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_GEMM3_ROTATE");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
-}
-
 bool gemm_library(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, int64_t N, int64_t K,
                   int64_t nseg, int64_t nb1, int64_t nb2, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA1,
                   int64_t sA2, int64_t sB1, int64_t sB2, int64_t sC1, int64_t sC2, int64_t sAseg, int64_t sBseg,
@@ -258,7 +249,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
       at::Tensor ws;
       if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
       const int rc3 = xdot_gemm3_launch(&g3a, (int)(nb1 * nb2), xdot::DT_BF16, xdot::DT_F32, a_mc, b_mc, (int)S,
-                                        S > 1 ? ws.data_ptr<float>() : nullptr, nullptr, st);
+                                        S > 1 ? ws.data_ptr<float>() : nullptr, st);
       TORCH_CHECK(rc3 == 0, "xdot.gemm: split fp32 gemm3 launch declined (", rc3, ")");
       check_launch(hipGetLastError(), "gemm3 (split fp32)");
       return;
@@ -296,15 +287,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     // v3 (8-phase 16x16x32, csrc/gemm3.hip) first: beta = 0, M and N >= 256; it declines
     // (-3) the rest, which the v2 kernel takes
     if (mode == 3 || (mode == 0 && gemm3_auto())) {
-      // rotation (staggered epilogues) when every workgroup walks >= 2 items of short K, i.e.
-      // when the output stream is a large share of the traffic
-      at::Tensor rws;
-      const int64_t items = tiles * S;
-      if (gemm3_rotate() && items >= 2 * ncu && kt64 / S <= 48)
-        rws = at::empty({(int64_t)xdot_gemm3_rotation_floats()}, A.options().dtype(at::kFloat));
       const int rc3 = xdot_gemm3_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
-                                        a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr,
-                                        rws.defined() ? rws.data_ptr<float>() : nullptr, cur_stream(A));
+                                        a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
       TORCH_CHECK(mode != 3 || rc3 == 0, "xdot.gemm: path 3 (gemm3) not eligible for this call (", rc3, ")");
       if (rc3 == 0) {
         check_launch(hipGetLastError(), "gemm3");

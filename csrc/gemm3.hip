@@ -20,7 +20,8 @@
 //   * persistent grid walking (split, batch, tile) items; the k-tile stream runs straight
 //     across items (the next item's tiles are in flight during this item's last phases); the
 //     epilogue converts in registers and stores 16 bytes per lane (v_permlane16_swap pairs
-//     two 16x16 accumulators into 8 consecutive columns) -- no LDS round trip;
+//     two 16x16 accumulators into 8 consecutive columns), one output quadrant per phase of the
+//     item's last k-tile -- no LDS round trip, no store burst for the DMA stream to queue behind;
 //   * edge tiles are shifted inside the matrix (m0 = min(256 tm, M - 256)), so every DMA
 //     source is in bounds with item-independent per-lane offsets; the overlap rows/columns
 //     are recomputed bitwise identically and simply stored twice (hence beta = 0 only);
@@ -83,8 +84,7 @@ __device__ __forceinline__ void swap16(uint32_t& x, uint32_t& y) {
 // Work item = (split zs, batch z, output tile).  Walked by a persistent grid: workgroup slot s
 // takes items s, s + G, ...; the LDS ring runs straight across items.
 template <int DTI, int DTO, bool A_MC, bool B_MC, int EPI>
-__global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restrict__ ws, float* __restrict__ rws, int W, int batches,
-                                                   int nsplit) {
+__global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restrict__ ws, int W, int batches, int nsplit) {
   using namespace g3;
   using fa::smem;
   using fa::lds_addr;
@@ -153,19 +153,22 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   // ---- issue side: cursor of one k-tile (item L, flattened k index k < te, k-tile kt of its
   // segment, valid k kl, operand bytes a / b of the k-tile).  Kept small: it lives in SGPRs
   // twice (the k-tiles one and two ahead of the compute side).
+  // An item's k-tile count is padded to an even number (te2 = tb + round_up_even(te - tb)):
+  // every item then starts on LDS-slot parity 0 and ends on parity 1 (see the item loop).  The
+  // pad k-tile (k >= te) is DMA'd entirely out of range, i.e. zeros, and adds nothing.
   struct Cur {
-    int L, k, te, kt, kl, wrap;
+    int L, k, te, te2, kt, kl;  // kl: valid k of this k-tile (0: pad)
     const char* a;
     const char* b;
   };
-  // k-tile k of item L, its stream segment ending at te (wrap: the first item's rotated-away prefix)
-  auto cur_at = [&](int L, int k, int te, int wrap) __attribute__((always_inline)) {
+  // k-tile k of item L (k < te2)
+  auto cur_at = [&](int L, int k, int te) __attribute__((always_inline)) {
     Cur c;
     const Item it = item_of(L);
     c.L = L;
     c.k = k;
     c.te = te;
-    c.wrap = wrap;
+    c.te2 = te + ((te - it.tb) & 1);
     const int seg = k / ktiles;
     c.kt = k - seg * ktiles;
     c.kl = c.kt == ktiles - 1 ? kl_t : BK;
@@ -173,17 +176,6 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     c.b = it.b + 2 * (int64_t)seg * p.sBseg + (int64_t)c.kt * b_kstep;
     return c;
   };
-  // Rotation (rws != nullptr): the workgroup starts its first item `rot` k-tiles in and
-  // finishes the skipped prefix after its last item (partial sums parked in rws meanwhile).
-  // Offsets differ across each XCD's 32 slots, so the workgroups' epilogues -- 128 KiB of output
-  // each -- no longer land in one burst that every workgroup then waits out in its next vmcnt.
-  int tb0, te0;
-  {
-    const Item it = item_of(slot0);
-    tb0 = it.tb;
-    te0 = it.te;
-  }
-  const int rot = rws ? (((slot0 & 31) * (te0 - tb0)) >> 5) : 0;
   // the k-tile after c in the workgroup's stream (after the end: c itself again -- its DMAs
   // are harmless repeats)
   auto next_of = [&](const Cur& c) __attribute__((always_inline)) {
@@ -202,11 +194,16 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
       n.kl = n.kt == ktiles - 1 ? kl_t : BK;
       return n;
     }
-    if (!c.wrap && c.L + G < W) {
-      const Item it = item_of(c.L + G);
-      return cur_at(c.L + G, it.tb, it.te, 0);
+    if (c.k + 1 < c.te2) {  // the pad k-tile
+      Cur n = c;
+      n.k = c.k + 1;
+      n.kl = 0;
+      return n;
     }
-    if (!c.wrap && rot > 0) return cur_at(slot0, tb0, tb0 + rot, 1);
+    if (c.L + G < W) {
+      const Item it = item_of(c.L + G);
+      return cur_at(c.L + G, it.tb, it.te);
+    }
     return c;
   };
 
@@ -255,8 +252,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     const char* b0 = isA ? c.a + h * a_half : c.b + h * b_half;
     // full k-tile: the precomputed offsets; K tail: dead chunks / k rows out of range (zeros)
     const uint32_t* ot = isA ? oat : obt;
-    const bool full = c.kl == BK;
-    bdma2(rsrc_of(b0), full ? o[0] : ot[0], full ? o[1] : ot[1], dst);
+    const bool full = c.kl == BK, pad = c.kl == 0;
+    bdma2(rsrc_of(b0), full ? o[0] : pad ? OOB : ot[0], full ? o[1] : pad ? OOB : ot[1], dst);
   };
 
   // ---- LDS fragment reads (16x16x32 operand: lane l holds mn = base + (l & 15), k = 8 (l >> 4) .. +7) ----
@@ -340,7 +337,11 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   // per-store 64-bit address registers next to the 128 accumulator registers.
   const int64_t ldo = EPI == 1 ? (int64_t)p.N : p.ldc;
   const int voff = EPI == 0 ? (int)((l15 * ldo + 16 * (g & 1) + 8 * (g >> 1)) * 2) : (int)((l15 * ldo + 4 * g) * 4);
-  auto epilogue = [&](const Item& it) __attribute__((always_inline)) {
+  // Output quadrant (j, i) of the wave (acc[4 j + mt][2 i + nt], mt < 4, nt < 2): stored as soon
+  // as its last MFMA of the item has issued -- in the next phase's load segment, so an item's
+  // 16 (32 fp32) store instructions per wave spread over 4 phases instead of one burst that the
+  // DMA stream queues behind -- then zeroed for the next item.
+  auto store_quad = [&](const Item& it, const int j, const int i) __attribute__((always_inline)) {
     const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
     const float alpha = p.alpha;
     const char* cb;
@@ -349,65 +350,43 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     else
       cb = reinterpret_cast<const char*>(p.C) + sizeof(TO) * (z1 * p.sC1 + z2 * p.sC2 + it.n0 + 32 * wn);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int r0 = it.m0 + 128 * j + 64 * wm + 16 * mt;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb + (int64_t)r0 * ldo * (EPI == 0 ? 2 : 4)), 0, 0x7FFFFFF0, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          f32x4 x = acc[4 * j + mt][2 * i], y = acc[4 * j + mt][2 * i + 1];
+    for (int mt = 0; mt < 4; ++mt) {
+      const int r0 = it.m0 + 128 * j + 64 * wm + 16 * mt;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb + (int64_t)r0 * ldo * (EPI == 0 ? 2 : 4)), 0, 0x7FFFFFF0, 0x00020000);
+      f32x4& xr = acc[4 * j + mt][2 * i];
+      f32x4& yr = acc[4 * j + mt][2 * i + 1];
+      f32x4 x = xr, y = yr;
 #ifdef G3_DIAG_NOSTORE
-          if (x[0] == 12345.f && y[1] == -7.f) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff, 0, 0);
-          continue;
-#endif
-          if constexpr (EPI == 0) {
-            x *= alpha;
-            y *= alpha;
-            uint32_t X0 = fa::pack2<DTO>(x[0], x[1]), X1 = fa::pack2<DTO>(x[2], x[3]);
-            uint32_t Y0 = fa::pack2<DTO>(y[0], y[1]), Y1 = fa::pack2<DTO>(y[2], y[3]);
-            swap16(X0, Y0);
-            swap16(X1, Y1);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{X0, X1, Y0, Y1}, rs, voff + 256 * i, 0, G3_STORE_AUX);
-          } else {
-            if constexpr (EPI == 3) {
-              x *= alpha;
-              y *= alpha;
-            }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff + 512 * i, 0, G3_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, voff + 512 * i + 64, 0, G3_STORE_AUX);
-          }
-        }
-      }
-  };
-  // rotation: park / pick up the first item's partial sums (wave-private, lane-linear: every
-  // store and load is one coalesced 1 KiB wave access)
-  auto rw_rsrc = [&]() __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(rws + ((int64_t)slot0 * 8 + wave) * (32 * 256), 0, 0x7FFFFFF0, 0x00020000);
-  };
-  auto park = [&]() __attribute__((always_inline)) {
-    const __amdgpu_buffer_rsrc_t rwr = rw_rsrc();
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rwr, 16 * lane, (a * 4 + b) * 1024, 0);
-  };
-  auto pick_up = [&]() __attribute__((always_inline)) {
-    const __amdgpu_buffer_rsrc_t rwr = rw_rsrc();
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwr, 16 * lane, (a * 4 + b) * 1024, 0));
-  };
-  // store instructions an epilogue (or a park, 32) issues per lane, at least: the vmcnt waits of
-  // the k-tile after it count them
-#ifdef G3_DIAG_NOSTORE
-  constexpr int EPI_ST = 0;
+      if (x[0] == 12345.f && y[1] == -7.f) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff, 0, 0);
 #else
-  constexpr int EPI_ST = EPI == 0 ? 16 : 32;
+      if constexpr (EPI == 0) {
+        x *= alpha;
+        y *= alpha;
+        uint32_t X0 = fa::pack2<DTO>(x[0], x[1]), X1 = fa::pack2<DTO>(x[2], x[3]);
+        uint32_t Y0 = fa::pack2<DTO>(y[0], y[1]), Y1 = fa::pack2<DTO>(y[2], y[3]);
+        swap16(X0, Y0);
+        swap16(X1, Y1);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{X0, X1, Y0, Y1}, rs, voff + 256 * i, 0, G3_STORE_AUX);
+      } else {
+        if constexpr (EPI == 3) {
+          x *= alpha;
+          y *= alpha;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff + 512 * i, 0, G3_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, voff + 512 * i + 64, 0, G3_STORE_AUX);
+      }
+#endif
+      xr = f32x4{0.f, 0.f, 0.f, 0.f};
+      yr = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // store instructions of one quadrant per lane (exact: the vmcnt waits around an item boundary
+  // count them)
+#ifdef G3_DIAG_NOSTORE
+  constexpr int SPQ = 0;
+#else
+  constexpr int SPQ = EPI == 0 ? 4 : 8;
 #endif
 
   // ---- prologue: k-tiles 0 (slot 0) and 1 (slot 1) in the steady-state issue order ----
@@ -417,7 +396,11 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   //   q2: reads A quarter 1                          issues A half 0    of k-tile v + 2
   //   q3: no reads                                   issues B half P    of k-tile v + 2
   // waits vmcnt(8) in q0, q1, q3 (after their issue): data waited in phase q is read in q+1.
-  Cur c1 = cur_at(slot0, tb0 + rot, te0, 0);
+  Cur c1;
+  {
+    const Item it = item_of(slot0);
+    c1 = cur_at(slot0, it.tb, it.te);
+  }
   issue(c1, 0, 0);
   issue(c1, 2, 0);
   issue(c1, 3, 0);
@@ -430,43 +413,57 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   if (wm == 1) fa::raw_barrier();  // waves 4-7 run one barrier behind
 
   int cL = slot0;
-  // compute side: flattened k index, its segment end, k-tile within the K segment, and the
-  // stream phase (0: first item after the rotation offset, 1: whole items, 2: the prefix)
-  int ck = tb0 + rot, cte = te0, ckt = ck % ktiles, phase = rot ? 0 : 1;
-  bool after_epi = false;
+  // compute side: flattened k index and its end
+  int ck, cte;  // cte: the padded end
+  {
+    const Item it = item_of(cL);
+    ck = it.tb;
+    cte = it.te + ((it.te - it.tb) & 1);
+  }
+  bool first = false;  // this k-tile is an item's first after an item boundary
   Cur c2 = c1;
 
   u32x4 fa_[4][2], fb0[2][2], fb1[2][2];
 
-  // one k-tile of parity P from slot P (wide: the previous item's epilogue stores sit in the
-  // vmcnt window of this k-tile's waits)
-  auto ktile = [&](auto Pc, const bool wide) __attribute__((always_inline)) {
+  // One k-tile of parity P from slot P.  LAST: the item's last k-tile -- quadrants 0-2 are
+  // stored in the load segments of phases 1-3, quadrant 3 after the k-tile.  The waits count the
+  // quadrant stores issued after the DMAs they wait for (SPQ per quadrant): on the last k-tile
+  // q1 +1, q3 +3 quadrants; on the next item's first k-tile q0 +4, q1 +3, q3 +1.
+  auto ktile = [&](auto Pc, auto Lc, const Item& it) __attribute__((always_inline)) {
     constexpr int P = decltype(Pc)::value;
+    constexpr bool LAST = decltype(Lc)::value;
     const char* st = smem + P * SLOT;
     // q0
     read_a(fa_, st, 0);
     read_b(P ? fb1 : fb0, st, P);
     issue(c1, 2 + P, 1 - P);
-    if (wide) fa::wait_vm<8 + EPI_ST>(); else fa::wait_vm<8>();
+    if (!LAST && first) fa::wait_vm<8 + 4 * SPQ>(); else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb1 : fb0, 0, P);
     fa::raw_barrier();
     // q1
+    if constexpr (LAST) store_quad(it, 0, P);
     read_b(P ? fb0 : fb1, st, 1 - P);
     issue(c1, 1, 1 - P);
-    if (wide) fa::wait_vm<8 + EPI_ST>(); else fa::wait_vm<8>();
+    if constexpr (LAST) fa::wait_vm<8 + SPQ>();
+    else if (first) fa::wait_vm<8 + 3 * SPQ>();
+    else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb0 : fb1, 0, 1 - P);
     fa::raw_barrier();
     // q2
+    if constexpr (LAST) store_quad(it, 0, 1 - P);
     read_a(fa_, st, 1);
     issue(c2, 0, P);
     fa::raw_barrier();
     quad(fa_, P ? fb0 : fb1, 1, 1 - P);
     fa::raw_barrier();
     // q3
+    if constexpr (LAST) store_quad(it, 1, 1 - P);
     issue(c2, 2 + P, P);
-    if (wide) fa::wait_vm<8 + EPI_ST>(); else fa::wait_vm<8>();
+    if constexpr (LAST) fa::wait_vm<8 + 3 * SPQ>();
+    else if (first) fa::wait_vm<8 + SPQ>();
+    else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb1 : fb0, 1, P);
     fa::raw_barrier();
@@ -474,62 +471,47 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  // The epilogue of an item runs between its last k-tile and the next item's first, whose
-  // q0 issue follows it (that k-tile's vmcnt waits count the stores).  Every helper has ONE
-  // inlined copy in the loop (the item decode is dozens of scalar instructions).
-  // returns true when the workgroup's last item is done
-  auto step = [&](auto Pc) __attribute__((always_inline)) -> bool {
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  // Items have an even number n >= 2 of k-tiles (odd counts padded), so every item starts on
+  // parity 0 and ends on parity 1: per item, (n / 2 - 1) pairs of plain k-tiles, then a plain
+  // parity-0 k-tile and the LAST parity-1 one -- straight-line code, no branch between
+  // alternative k-tile bodies (which makes the register allocator shuffle the accumulators).
+  auto plain = [&](auto Pc) __attribute__((always_inline)) {
     c2 = next_of(c1);
-    ktile(Pc, after_epi);
+    ktile(Pc, BF{}, Item{});
     c1 = c2;
-    after_epi = false;
-    if (++ckt == ktiles) ckt = 0;
-    if (++ck == cte) {
-      if (phase == 2) return true;  // the prefix: its epilogue follows the loop
-      if (phase == 0) park();
-      else epilogue(item_of(cL));
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      after_epi = true;
-      cL += G;
-      if (cL < W) {
-        const Item it = item_of(cL);
-        ck = it.tb;
-        cte = it.te;
-        phase = 1;
-      } else {
-        if (rot == 0) return true;
-        cL = slot0;
-        ck = tb0;
-        cte = tb0 + rot;
-        phase = 2;
-      }
-      ckt = ck % ktiles;
-    }
-    return false;
+    first = false;
   };
   while (true) {
-    if (step(I0{})) break;
-    if (step(I1{})) break;
-  }
-  if (phase == 2) {
-    if (EPI == 0 || EPI == 3) fa::wait_vm<0>();  // the parked partial was stored by this lane
-    pick_up();
-    epilogue(item_of(cL));
+    for (int k = ck; k + 2 < cte; k += 2) {
+      plain(I0{});
+      plain(I1{});
+    }
+    plain(I0{});
+    c2 = next_of(c1);
+    const Item it = item_of(cL);
+    ktile(I1{}, BT{}, it);
+    store_quad(it, 1, 1);
+    c1 = c2;
+    first = true;
+    cL += G;
+    if (cL >= W) break;
+    const Item nx = item_of(cL);
+    ck = nx.tb;
+    cte = nx.te + ((nx.te - nx.tb) & 1);
   }
   fa::wait_vm<0>();  // repeat DMAs of the final k-tiles must land before the LDS goes away
   if (wm == 0) fa::raw_barrier();  // balance the stagger
 }
 
 template <int DTI, int DTO, bool AMC, bool BMC>
-static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, float* rws, int ncu, hipStream_t st) {
+static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, int ncu, hipStream_t st) {
   const int W = a.tiles_m * a.tiles_n * batches * splits;
   const int G = W < ncu ? W : ncu;
   float* w = splits > 1 ? ws : nullptr;
   // epilogue modes (see the kernel): split-K slices 1, 16-bit C 0, fp32 C 3
-#define G3L(E) hipLaunchKernelGGL((gemm3_kernel<DTI, DTO, AMC, BMC, E>), dim3(G), dim3(g3::NT), g3::LDS, st, a, w, rws, W, batches, splits)
+#define G3L(E) hipLaunchKernelGGL((gemm3_kernel<DTI, DTO, AMC, BMC, E>), dim3(G), dim3(g3::NT), g3::LDS, st, a, w, W, batches, splits)
   if (w) G3L(1);
   else if constexpr (DTO == DT_F32) G3L(3);
   else G3L(0);
@@ -537,12 +519,11 @@ static void launch3_t(const GemmArgs& a, int batches, int splits, float* ws, flo
 }
 
 template <int DTI, int DTO>
-static void launch3_d(const GemmArgs& a, int batches, bool amc, bool bmc, int splits, float* ws, float* rws, int ncu,
-                      hipStream_t st) {
-  if (!amc && !bmc) return launch3_t<DTI, DTO, false, false>(a, batches, splits, ws, rws, ncu, st);
-  if (!amc && bmc) return launch3_t<DTI, DTO, false, true>(a, batches, splits, ws, rws, ncu, st);
-  if (amc && !bmc) return launch3_t<DTI, DTO, true, false>(a, batches, splits, ws, rws, ncu, st);
-  return launch3_t<DTI, DTO, true, true>(a, batches, splits, ws, rws, ncu, st);
+static void launch3_d(const GemmArgs& a, int batches, bool amc, bool bmc, int splits, float* ws, int ncu, hipStream_t st) {
+  if (!amc && !bmc) return launch3_t<DTI, DTO, false, false>(a, batches, splits, ws, ncu, st);
+  if (!amc && bmc) return launch3_t<DTI, DTO, false, true>(a, batches, splits, ws, ncu, st);
+  if (amc && !bmc) return launch3_t<DTI, DTO, true, false>(a, batches, splits, ws, ncu, st);
+  return launch3_t<DTI, DTO, true, true>(a, batches, splits, ws, ncu, st);
 }
 
 }  // namespace xdot
@@ -552,10 +533,8 @@ extern "C" int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws,
                                        hipStream_t st);
 
 // Eligibility: see the file header.  -3 = shape/layout not eligible (caller falls back).
-// rws: rotation workspace (xdot_gemm3_rotation_floats() floats) or nullptr (no rotation)
-extern "C" int xdot_gemm3_rotation_floats() { return xdot_num_cus() * 256 * 256; }
 extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
-                                 int splits, float* ws, float* rws, hipStream_t st) {
+                                 int splits, float* ws, hipStream_t st) {
   using namespace xdot;
   GemmArgs g = *a;
   if (g.M < g3::BM || g.N < g3::BN || (g.K % 8) != 0 || g.beta != 0.f) return -3;
@@ -563,9 +542,10 @@ extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in
   g.tiles_n = (g.N + g3::BN - 1) / g3::BN;
   if (batches == 0 || g.K == 0) return -3;
   if (splits < 1 || (splits > 1 && !ws)) return -2;
+  if ((int64_t)((g.K + g3::BK - 1) / g3::BK) * g.nseg < splits) return -3;  // every item >= 1 k-tile
   const int ncu = xdot_num_cus();
 #define G3_DT(I, O) \
-  if (dt_in == I && dt_out == O) { launch3_d<I, O>(g, batches, a_mc, b_mc, splits, ws, rws, ncu, st); goto done; }
+  if (dt_in == I && dt_out == O) { launch3_d<I, O>(g, batches, a_mc, b_mc, splits, ws, ncu, st); goto done; }
   G3_DT(DT_BF16, DT_BF16) G3_DT(DT_BF16, DT_F32) G3_DT(DT_F16, DT_F16) G3_DT(DT_F16, DT_F32)
 #undef G3_DT
   return -1;

@@ -140,11 +140,8 @@ int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out
 int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);
 // 8-phase 16x16x32 16-bit GEMM (csrc/gemm3.hip): M, N >= 256, K % 8 == 0; -3 = not eligible
-// rws: rotation workspace of xdot_gemm3_rotation_floats() floats (staggers the workgroups'
-// epilogues; nullptr = off)
 int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
-                      int splits, float* ws, float* rws, hipStream_t st);
-int xdot_gemm3_rotation_floats();
+                      int splits, float* ws, hipStream_t st);
 // fp32 operand -> compact bf16 parts [z1][z2][3][seg][R][C] (hi, or lo where lo_mask bit p is set)
 int xdot_split3_launch(const float* src, void* dst, int64_t s1, int64_t s2, int64_t sseg, int64_t ld,
                        int nb1, int nb2, int nseg, int R, int C, int lo_mask, hipStream_t st);

@@ -1,7 +1,7 @@
 """Runtime flags (environment variables): the ONE place xdot reads ``XDOT_*`` variables.
 
 Read once at import (``FLAGS.reload()`` re-reads them) and overridable in code; the native
-extension reads the three marked (C++) itself, at its first use.  The reference has a single
+extension reads the ones marked (C++) itself, at its first use.  The reference has a single
 flag (``DISTRIBUTED_DOT_DEBUG``, ``multiplication/functions.py:21``); everything else here is a
 documented default of this MI355X build, mostly with the measurement that chose it.
 
@@ -36,9 +36,10 @@ variable                    default   effect
 ``XDOT_IPC_TIMEOUT_S``      (comm)    bound of every IPC device-side wait
 ``XDOT_PRESCALE``           1         pre-multiply the row side by scale·log2 e once per forward
                                       (seeded score accumulators; forward 2.11 -> 1.98 ms)
-``XDOT_FP32_MODE``          split     fp32 flash kernels: ``split`` (hi/lo bf16 halves, 3 bf16 MFMAs per
-                                      product: <= 9e-6 relative vs fp64, 1.6x faster step) or
-                                      ``exact`` (fp32 MFMA, ~5e-7); profiles/r3_fp32_split.md
+``XDOT_FP32_MODE``          split     fp32 flash kernels and large fp32 GEMMs (read by Python and C++):
+                                      ``split`` (hi/lo bf16 halves, 3 bf16 products: <= 9e-6 flash,
+                                      <= 2e-5 GEMM, relative vs fp64) or ``exact`` (fp32 MFMA /
+                                      library fp32 GEMM, ~5e-7); profiles/r3_fp32_split.md
 ``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
                                       1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
 ``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
@@ -48,6 +49,8 @@ variable                    default   effect
 ``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
 ``XDOT_GEMM_LIB`` (C++)     see doc   plain large products on hipBLASLt instead of the hand-written
                                       MFMA GEMM (``csrc/bindings.cpp``)
+``XDOT_GEMM3`` (C++)        1         16-bit products with M, N >= 256 and beta = 0 run the 8-phase
+                                      16x16x32 kernel (``csrc/gemm3.hip``; 0: the 256x256 v2 kernel)
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
 ==========================  ========  ===========================================================
 
