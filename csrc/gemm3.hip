@@ -35,12 +35,17 @@ namespace xdot {
 namespace g3 {
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+#ifndef G3_FL
+#define G3_FL 1  // whole-line epilogue stores for 16-bit C with k-contiguous B (A/B knob)
+#endif
 #ifndef G3_STORE_AUX
 #define G3_STORE_AUX 0  // cache policy of the output stores (A/B knob of scripts/gemm3_ab.sh)
 #endif
 constexpr int HALF = 16384;       // one half-tile image (128 x 64 x 2 B)
 constexpr int SLOT = 4 * HALF;    // [A 0-127 | A 128-255 | B 0-127 | B 128-255]
-constexpr int LDS = 2 * SLOT;     // 128 KiB: two k-tiles
+constexpr int TAB = 2 * SLOT;     // 128 KiB ring: two k-tiles; then the item table
+constexpr int MAX_ITEMS = 2048;   // items per workgroup (16-byte entries, 32 KiB)
+constexpr int LDS = TAB + 16 * MAX_ITEMS;
 
 template <int DT> __device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
   if constexpr (DT == DT_BF16)
@@ -108,26 +113,36 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   const int64_t lda2 = p.lda * 2, ldb2 = p.ldb * 2;
   // byte steps of one k-tile / one half-tile inside an operand
   const int64_t a_kstep = A_MC ? 64 * lda2 : 128, b_kstep = B_MC ? 64 * ldb2 : 128;
-  const int64_t a_half = A_MC ? 256 : 128 * lda2, b_half = B_MC ? 256 : 128 * ldb2;
+  // FL (16-bit C, k-contiguous B): wave wn owns the 64 contiguous output columns 64 wn .. +63
+  // (its two 32-column n-halves side by side), B half i = columns {64 w + 32 i + c} (image row
+  // 32 w + c), and the epilogue writes whole 128-byte row segments (see store_half).
+  // Otherwise wave wn owns columns 128 i + 32 wn (an mn-contiguous B half is then one
+  // contiguous 256-byte piece of a k row).
+  constexpr bool FL = EPI == 0 && !B_MC && G3_FL;
+  constexpr int WCOL = FL ? 64 : 32;  // column stride of the waves
+  const int64_t a_half = A_MC ? 256 : 128 * lda2, b_half = B_MC ? 256 : (FL ? 32 : 128) * ldb2;
   // byte jump from the last k-tile of a K segment to the first of the next
   const int64_t a_segjump = 2 * p.sAseg - (int64_t)(ktiles - 1) * a_kstep;
   const int64_t b_segjump = 2 * p.sBseg - (int64_t)(ktiles - 1) * b_kstep;
   const int kl_t = p.K - (ktiles - 1) * BK;  // valid k of every segment's last k-tile
 
   struct Item {
-    int m0, n0, mo, no, z, zs, tb, te;
+    int m0, n0, mo, no, z, z1, z2, zs, tb, te;
     const char* a;  // operand bytes at (batch, tile mn origin)
     const char* b;
   };
-  auto item_of = [&](int L) __attribute__((always_inline)) {
-    Item it;
+  // Item table: at launch the workgroup decodes its items (slot0 + k G, k < nitems <= 2048) into
+  // 16-byte LDS entries past the 128 KiB ring -- {tm | tn << 16, z1 | z2 << 16, tb | zs << 24, te}
+  // -- so the loop looks an item up with one broadcast ds_read instead of ~10 integer divisions.
+  // Tile order: super-blocks of SB x SB tiles (row-major over the super-block grid), inside one
+  // super-block groups of GM m-tiles sweeping its n-tiles.  A super-block's panels are re-read
+  // while at most SB^2 x 128 KiB of output streams out (<= 128 MiB: they stay in the 256 MiB
+  // Infinity Cache; a whole-row sweep at N = 75000 wrote 300 MB between two uses).
+  const int nitems = (W - slot0 + G - 1) / G;
+  for (int k = tid; k < nitems; k += NT) {
+    const int L = slot0 + k * G;
     const int zz = L / ntile, tl = L % ntile;
-    it.zs = zz / batches;
-    it.z = zz % batches;
-    // tile order: super-blocks of SB x SB tiles (row-major over the super-block grid), inside
-    // one super-block groups of GM m-tiles sweeping its n-tiles.  A super-block's panels are
-    // re-read while at most SB^2 x 128 KiB of output streams out (<= 128 MiB: they stay in the
-    // 256 MiB Infinity Cache; a whole-row sweep at N = 75000 wrote 300 MB between two uses)
+    const int zs = zz / batches, z = zz % batches;
     const int sbr = tl / (SB * p.tiles_n);
     const int sbm = min(SB, p.tiles_m - sbr * SB);
     const int r1 = tl - sbr * SB * p.tiles_n;
@@ -138,13 +153,29 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     const int gm_n = min(GM, sbm - gi * GM);
     const int r3 = r2 - gi * GM * sbn;
     const int tm = sbr * SB + gi * GM + r3 % gm_n, tn = sbc * SB + r3 / gm_n;
-    it.mo = tm * BM;
-    it.no = tn * BN;
+    const int tb = (int)((unsigned)(zs * ntot) / (unsigned)nsplit);
+    const int te = (int)((unsigned)((zs + 1) * ntot) / (unsigned)nsplit);
+    *reinterpret_cast<u32x4*>(smem + TAB + 16 * k) =
+        u32x4{(uint32_t)tm | ((uint32_t)tn << 16), (uint32_t)(z / p.nb2) | ((uint32_t)(z % p.nb2) << 16),
+              (uint32_t)tb | ((uint32_t)zs << 24), (uint32_t)te};
+  }
+  __syncthreads();
+  auto item_of = [&](int k) __attribute__((always_inline)) {
+    const u32x4 e = *reinterpret_cast<const u32x4*>(smem + TAB + 16 * k);
+    const uint32_t e0 = __builtin_amdgcn_readfirstlane(e[0]), e1 = __builtin_amdgcn_readfirstlane(e[1]);
+    const uint32_t e2 = __builtin_amdgcn_readfirstlane(e[2]), e3 = __builtin_amdgcn_readfirstlane(e[3]);
+    Item it;
+    it.mo = (int)(e0 & 0xFFFFu) * BM;
+    it.no = (int)(e0 >> 16) * BN;
     it.m0 = min(it.mo, p.M - BM);  // (an mn-contiguous operand has M / N % 8 == 0: 16-byte DMA sources)
     it.n0 = min(it.no, p.N - BN);
-    it.tb = __builtin_amdgcn_readfirstlane((int)((unsigned)(it.zs * ntot) / (unsigned)nsplit));
-    it.te = __builtin_amdgcn_readfirstlane((int)((unsigned)((it.zs + 1) * ntot) / (unsigned)nsplit));
-    const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
+    const int z1 = (int)(e1 & 0xFFFFu), z2 = (int)(e1 >> 16);
+    it.z1 = z1;
+    it.z2 = z2;
+    it.z = z1 * p.nb2 + z2;
+    it.zs = (int)(e2 >> 24);
+    it.tb = (int)(e2 & 0xFFFFFFu);
+    it.te = (int)e3;
     it.a = reinterpret_cast<const char*>(p.A) + 2 * (z1 * p.sA1 + z2 * p.sA2 + (A_MC ? (int64_t)it.m0 : (int64_t)it.m0 * p.lda));
     it.b = reinterpret_cast<const char*>(p.B) + 2 * (z1 * p.sB1 + z2 * p.sB2 + (B_MC ? (int64_t)it.n0 : (int64_t)it.n0 * p.ldb));
     return it;
@@ -161,7 +192,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     const char* a;
     const char* b;
   };
-  // k-tile k of item L (k < te2)
+  // k-tile k of the workgroup's item L (table index; k < te2)
   auto cur_at = [&](int L, int k, int te) __attribute__((always_inline)) {
     Cur c;
     const Item it = item_of(L);
@@ -200,9 +231,9 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
       n.kl = 0;
       return n;
     }
-    if (c.L + G < W) {
-      const Item it = item_of(c.L + G);
-      return cur_at(c.L + G, it.tb, it.te);
+    if (c.L + 1 < nitems) {
+      const Item it = item_of(c.L + 1);
+      return cur_at(c.L + 1, it.tb, it.te);
     }
     return c;
   };
@@ -227,7 +258,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
       }
       if (!B_MC) {
         const int r = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-        ob[pp] = (uint32_t)(r * ldb2 + 16 * c);
+        const int rt = FL ? 64 * (r >> 5) + (r & 31) : r;  // tile row (output column) of image row r
+        ob[pp] = (uint32_t)(rt * ldb2 + 16 * c);
         tb_[pp] = 8 * c;
       } else {
         const int k = 4 * pc + (lane >> 4), c = (lane & 15) ^ (2 * (k & 3) + 8 * ((k >> 3) & 1));
@@ -342,13 +374,13 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   // 16 (32 fp32) store instructions per wave spread over 4 phases instead of one burst that the
   // DMA stream queues behind -- then zeroed for the next item.
   auto store_quad = [&](const Item& it, const int j, const int i) __attribute__((always_inline)) {
-    const int z1 = it.z / p.nb2, z2 = it.z % p.nb2;
+    const int z1 = it.z1, z2 = it.z2;
     const float alpha = p.alpha;
     const char* cb;
     if constexpr (EPI == 1)
-      cb = reinterpret_cast<const char*>(ws + ((int64_t)it.zs * batches + it.z) * (int64_t)p.M * p.N + it.n0 + 32 * wn);
+      cb = reinterpret_cast<const char*>(ws + ((int64_t)it.zs * batches + it.z) * (int64_t)p.M * p.N + it.n0 + WCOL * wn);
     else
-      cb = reinterpret_cast<const char*>(p.C) + sizeof(TO) * (z1 * p.sC1 + z2 * p.sC2 + it.n0 + 32 * wn);
+      cb = reinterpret_cast<const char*>(p.C) + sizeof(TO) * (z1 * p.sC1 + z2 * p.sC2 + it.n0 + WCOL * wn);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int r0 = it.m0 + 128 * j + 64 * wm + 16 * mt;
@@ -381,6 +413,53 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
       yr = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
+  // FL epilogue of output row block j (both n-halves final): per 16-row strip two stores of
+  // 8 rows x 128 bytes each (whole cache lines; the plain form writes 16 rows x 64 bytes per
+  // instruction).  After the permlane16 pairing a lane holds 8 columns of its row in each half
+  // (chunk c0 = 2 (g & 1) + (g >> 1) of the 4 16-byte chunks of a 64-byte half); lanes l and
+  // l ^ 8 of a 16-lane row exchange one half (DPP row_ror:8), so the first store carries rows
+  // 0-7 (chunks 0-7) and the second rows 8-15.
+  const bool lo8 = l15 < 8;
+  const int voff_fl = (int)(((l15 & 7) * ldo + 8 * (2 * (g & 1) + (g >> 1) + 4 * (l15 >> 3))) * 2);
+  auto store_half = [&](const Item& it, const int j) __attribute__((always_inline)) {
+    if constexpr (FL) {
+      const float alpha = p.alpha;
+      const char* cb = reinterpret_cast<const char*>(p.C) + sizeof(TO) * (it.z1 * p.sC1 + it.z2 * p.sC2 + it.n0 + WCOL * wn);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int r0 = it.m0 + 128 * j + 64 * wm + 16 * mt;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb + (int64_t)r0 * ldo * 2), 0, 0x7FFFFFF0, 0x00020000);
+        uint32_t d[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const f32x4 x = acc[4 * j + mt][2 * i] * alpha, y = acc[4 * j + mt][2 * i + 1] * alpha;
+          d[i][0] = fa::pack2<DTO>(x[0], x[1]);
+          d[i][1] = fa::pack2<DTO>(x[2], x[3]);
+          d[i][2] = fa::pack2<DTO>(y[0], y[1]);
+          d[i][3] = fa::pack2<DTO>(y[2], y[3]);
+          swap16(d[i][0], d[i][2]);
+          swap16(d[i][1], d[i][3]);
+          acc[4 * j + mt][2 * i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[4 * j + mt][2 * i + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        u32x4 va, vb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t send = lo8 ? d[1][e] : d[0][e];
+          const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xF, 0xF, false);  // row_ror:8
+          va[e] = lo8 ? d[0][e] : recv;
+          vb[e] = lo8 ? recv : d[1][e];
+        }
+#ifndef G3_DIAG_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(va, rs, voff_fl, 0, G3_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(vb, rs, voff_fl + (int)(8 * ldo * 2), 0, G3_STORE_AUX);
+#else
+        if (va[0] == 12345u && vb[1] == 7u) __builtin_amdgcn_raw_buffer_store_b128(va, rs, voff_fl, 0, 0);
+#endif
+      }
+    }
+  };
   // store instructions of one quadrant per lane (exact: the vmcnt waits around an item boundary
   // count them)
 #ifdef G3_DIAG_NOSTORE
@@ -388,6 +467,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
 #else
   constexpr int SPQ = EPI == 0 ? 4 : 8;
 #endif
+  // FL: 8 stores per row block j: j = 0 in the last k-tile's q2, j = 1 after it
+  constexpr int SPH = 2 * SPQ;
 
   // ---- prologue: k-tiles 0 (slot 0) and 1 (slot 1) in the steady-state issue order ----
   // steady state, k-tile v (slot v & 1, quadrant order by parity P = v & 1):
@@ -398,8 +479,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   // waits vmcnt(8) in q0, q1, q3 (after their issue): data waited in phase q is read in q+1.
   Cur c1;
   {
-    const Item it = item_of(slot0);
-    c1 = cur_at(slot0, it.tb, it.te);
+    const Item it = item_of(0);
+    c1 = cur_at(0, it.tb, it.te);
   }
   issue(c1, 0, 0);
   issue(c1, 2, 0);
@@ -412,7 +493,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   fa::raw_barrier();
   if (wm == 1) fa::raw_barrier();  // waves 4-7 run one barrier behind
 
-  int cL = slot0;
+  int cL = 0;  // compute side: table index of the item
   // compute side: flattened k index and its end
   int ck, cte;  // cte: the padded end
   {
@@ -432,37 +513,41 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
   auto ktile = [&](auto Pc, auto Lc, const Item& it) __attribute__((always_inline)) {
     constexpr int P = decltype(Pc)::value;
     constexpr bool LAST = decltype(Lc)::value;
+    // stores issued after the DMA each wait is for: see the item loop
+    constexpr int W0F = FL ? 8 + 2 * SPH : 8 + 4 * SPQ, W1F = FL ? 8 + 2 * SPH : 8 + 3 * SPQ, W3F = FL ? 8 + SPH : 8 + SPQ;
+    constexpr int W1L = FL ? 8 : 8 + SPQ, W3L = FL ? 8 + SPH : 8 + 3 * SPQ;
     const char* st = smem + P * SLOT;
     // q0
     read_a(fa_, st, 0);
     read_b(P ? fb1 : fb0, st, P);
     issue(c1, 2 + P, 1 - P);
-    if (!LAST && first) fa::wait_vm<8 + 4 * SPQ>(); else fa::wait_vm<8>();
+    if (!LAST && first) fa::wait_vm<W0F>(); else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb1 : fb0, 0, P);
     fa::raw_barrier();
     // q1
-    if constexpr (LAST) store_quad(it, 0, P);
+    if constexpr (LAST && !FL) store_quad(it, 0, P);
     read_b(P ? fb0 : fb1, st, 1 - P);
     issue(c1, 1, 1 - P);
-    if constexpr (LAST) fa::wait_vm<8 + SPQ>();
-    else if (first) fa::wait_vm<8 + 3 * SPQ>();
+    if constexpr (LAST) fa::wait_vm<W1L>();
+    else if (first) fa::wait_vm<W1F>();
     else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb0 : fb1, 0, 1 - P);
     fa::raw_barrier();
     // q2
-    if constexpr (LAST) store_quad(it, 0, 1 - P);
+    if constexpr (LAST && !FL) store_quad(it, 0, 1 - P);
+    if constexpr (LAST && FL) store_half(it, 0);
     read_a(fa_, st, 1);
     issue(c2, 0, P);
     fa::raw_barrier();
     quad(fa_, P ? fb0 : fb1, 1, 1 - P);
     fa::raw_barrier();
     // q3
-    if constexpr (LAST) store_quad(it, 1, 1 - P);
+    if constexpr (LAST && !FL) store_quad(it, 1, 1 - P);
     issue(c2, 2 + P, P);
-    if constexpr (LAST) fa::wait_vm<8 + 3 * SPQ>();
-    else if (first) fa::wait_vm<8 + SPQ>();
+    if constexpr (LAST) fa::wait_vm<W3L>();
+    else if (first) fa::wait_vm<W3F>();
     else fa::wait_vm<8>();
     fa::raw_barrier();
     quad(fa_, P ? fb1 : fb0, 1, P);
@@ -492,11 +577,11 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
     c2 = next_of(c1);
     const Item it = item_of(cL);
     ktile(I1{}, BT{}, it);
-    store_quad(it, 1, 1);
+    if constexpr (FL) store_half(it, 1);
+    else store_quad(it, 1, 1);
     c1 = c2;
     first = true;
-    cL += G;
-    if (cL >= W) break;
+    if (++cL >= nitems) break;
     const Item nx = item_of(cL);
     ck = nx.tb;
     cte = nx.te + ((nx.te - nx.tb) & 1);
@@ -542,7 +627,12 @@ extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in
   g.tiles_n = (g.N + g3::BN - 1) / g3::BN;
   if (batches == 0 || g.K == 0) return -3;
   if (splits < 1 || (splits > 1 && !ws)) return -2;
+  const int ncu_ = xdot_num_cus();
   if ((int64_t)((g.K + g3::BK - 1) / g3::BK) * g.nseg < splits) return -3;  // every item >= 1 k-tile
+  {
+    const int64_t W = (int64_t)g.tiles_m * g.tiles_n * batches * splits;
+    if ((W + ncu_ - 1) / ncu_ > g3::MAX_ITEMS || g.tiles_m > 65535 || g.tiles_n > 65535) return -3;
+  }
   const int ncu = xdot_num_cus();
 #define G3_DT(I, O) \
   if (dt_in == I && dt_out == O) { launch3_d<I, O>(g, batches, a_mc, b_mc, splits, ws, ncu, st); goto done; }
