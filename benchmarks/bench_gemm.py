@@ -42,11 +42,13 @@ def main():
     path = a.path
     pc = {"auto": 0, "v1": 1, "v2": 2, "v3": 3}[path]
     for case in a.cases.split(","):
-        if case in ("nt", "nt_small", "nt_rank8") or case.startswith("ntk"):
+        if case in ("nt", "nt_small", "nt_rank8", "nt_wide") or case.startswith("ntk"):
             M = N = 75000 if case == "nt" else 25000
             K = int(case[3:]) if case.startswith("ntk") else 768
             if case == "nt_rank8":  # one rank's whole-shard nt at N=8, T=25000
                 M = 3125
+            if case == "nt_wide":  # 25000 x 75000 x 768 (round-2 verdict's fp32 comparison shape)
+                M, N = 25000, 75000
             A = torch.randn(M, K, device=dev, dtype=dt)
             B = torch.randn(N, K, device=dev, dtype=dt)
             C = torch.empty(M, N, device=dev, dtype=dt)

@@ -64,13 +64,14 @@ int64_t avail_elems(const at::Tensor& t) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// XDOT_GEMM_LIB: 1 (default) = plain GEMMs (one uniform batch level, K segments contiguous,
-// output dtype = input dtype) that fill >= 2 rounds of 256x256 tiles go to the library GEMM
-// (at::baddbmm -> hipBLASLt) on in-place strided views; 0 = always the xdot kernels
+// XDOT_GEMM_LIB: 0 (default) = every product on the xdot kernels (gemm3 matches or beats the
+// library GEMM on the plain large products: profiles/r3_gemm3.md); 1 = plain GEMMs (one uniform
+// batch level, K segments contiguous, output dtype = input dtype) that fill >= 2 rounds of
+// 256x256 tiles go to the library GEMM (at::baddbmm -> hipBLASLt) on in-place strided views
 int gemm_lib() {
   static const int v = [] {
     const char* e = std::getenv("XDOT_GEMM_LIB");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
   }();
   return v;
 }

@@ -92,10 +92,11 @@ def test_gemm2_persistent_interior_items(gpu, K, out_dt):
 
 
 def test_gemm_library_route_matches_kernels(gpu):
-    """large plain products take the library route (in-place strided views, one batch level,
-    merged K segments, tn's interleaved column blocks of `left` against one broadcast `right`);
-    the layout it refuses (nt's per-rank column blocks interleaved in one output row) stays on
-    the xdot kernels -- both must agree with torch on the same data"""
+    """large plain products through the op-level helpers (gemm3 by default; with
+    XDOT_GEMM_LIB=1 the library route on in-place strided views, one batch level, merged K
+    segments, tn's interleaved column blocks of `left` against one broadcast `right`); nt's
+    per-rank column blocks interleaved in one output row stay on the xdot kernels either way --
+    all must agree with torch on the same data"""
     from xdot.ops.gemm import all_chunk_into, nt_chunk_into, tn_partials_into
 
     g = torch.Generator(device="cpu").manual_seed(5)

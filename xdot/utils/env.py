@@ -47,8 +47,8 @@ variable                    default   effect
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
 ``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
-``XDOT_GEMM_LIB`` (C++)     see doc   plain large products on hipBLASLt instead of the hand-written
-                                      MFMA GEMM (``csrc/bindings.cpp``)
+``XDOT_GEMM_LIB`` (C++)     0         1: plain large products on hipBLASLt instead of the hand-written
+                                      MFMA GEMMs (``csrc/bindings.cpp``)
 ``XDOT_GEMM3`` (C++)        1         16-bit products with M, N >= 256 and beta = 0 run the 8-phase
                                       16x16x32 kernel (``csrc/gemm3.hip``; 0: the 256x256 v2 kernel)
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
