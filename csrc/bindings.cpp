@@ -265,7 +265,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;
   if (v2 && a_mc) v2 = M % 8 == 0;
   if (v2 && b_mc) v2 = N % 8 == 0;
-  if (v2 && mode != 2 && mode != 3) {
+  if (v2 && mode != 2 && mode != 3 && mode != 5) {
     // auto: enough 256x256 tiles (>= 32 per batch entry or >= 512 overall) -- small outputs
     // batched over K slabs (the split-K weight gradients of xdot.ops.linear) keep the 128x128
     // kernel, which fills the GPU without a second split.  Skinny outputs (one side 64..191,
@@ -287,7 +287,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     if (S > 1) ws = at::empty({S * nb1 * nb2 * M * N}, A.options().dtype(at::kFloat));
     // v3 (8-phase 16x16x32, csrc/gemm3.hip) first: beta = 0, M and N >= 256; it declines
     // (-3) the rest, which the v2 kernel takes
-    if (mode == 3 || (mode == 0 && gemm3_auto())) {
+    if (mode == 3 || mode == 5 || (mode == 0 && gemm3_auto())) {
       const int rc3 = xdot_gemm3_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()),
                                         a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(A));
       TORCH_CHECK(mode != 3 || rc3 == 0, "xdot.gemm: path 3 (gemm3) not eligible for this call (", rc3, ")");

@@ -26,8 +26,9 @@ def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0
     """C[z1, z2](m, n) = alpha * sum_s sum_k opA(m, k) * opB(k, n) + beta * C[z1, z2](m, n)
     (csrc/gemm.hip; 16-bit operands with large outputs run the 256x256 csrc/gemm2.hip).
 
-    ``path``: 0 = automatic kernel choice, 1 = the 128x128 kernel, 2 = the 256x256 kernel, 3 = the 8-phase 16x16x32 kernel
-    whenever its layout rules hold."""
+    ``path``: 0 = automatic kernel choice, 1 = the 128x128 kernel, 2 = the 256x256 kernel, 3 = the 8-phase
+    16x16x32 kernel (raises if it declines), 4 = fp32 as three bf16 products on it, 5 = the 8-phase kernel
+    where it takes the call, else the 256x256 one -- whenever the layout rules hold."""
     _ext.ops().gemm(A, B, C, int(M), int(N), int(K), int(nseg), int(nb1), int(nb2), int(lda),
                     int(ldb), int(ldc), int(sA1), int(sA2), int(sB1), int(sB2), int(sC1), int(sC2),
                     int(sAseg), int(sBseg), bool(a_mc), bool(b_mc), float(alpha),

@@ -28,6 +28,7 @@ __all__ = ["linear", "weight_grad", "LinearFn"]
 
 _SLOTS = 512       # 2 workgroups per CU x 256 CUs
 _MIN_SLAB = 256    # rows of K per split
+_WGRAD_PATH = 5    # gemm3 where it takes the shape (>= 256 x 256), else the 256x256 v2 kernel
 
 
 def _splits(M: int, N: int, K: int) -> int:
@@ -57,7 +58,7 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
         # 256x256 LDS-DMA kernel: it picks the K split itself (fp32 slices, one vectorised
         # in-order reduction that also casts to the parameter dtype)
         out = torch.empty(M, N, dtype=out_dtype, device=dy.device)
-        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True, path=2)
+        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True, path=_WGRAD_PATH)
         return out
     S = _splits(M, N, K)
     slab = K // S
