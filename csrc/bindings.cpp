@@ -217,7 +217,13 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   // hi/lo bf16 copies, three bf16 products in one gemm3 call (csrc/gemm3.hip, split3_kernel)
   if (A.scalar_type() == at::kFloat && (mode == 4 || (mode == 0 && fp32_split() && gemm3_auto()))) {
     const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
-    const bool big = 2.0 * (double)M * N * K * nseg * nb1 * nb2 >= 2e9 && (tpb >= 32 || tpb * nb1 * nb2 >= 512);
+    // worth it when three bf16 products plus the operand copies (read 4 B, write 6 B per
+    // element) beat one exact fp32 product: a product whose operand is far larger than its
+    // output (the materialised P.V: 2.5 GB of P per head) keeps the exact kernel
+    const double flop = 2.0 * (double)M * N * K * nseg * nb1 * nb2;
+    const double elems = (double)nb1 * nb2 * nseg * K * ((double)M + (double)N);
+    const double t_split = 3.0 * flop / 1.1e15 + 10.0 * elems / 5e12, t_exact = flop / 1.15e14;
+    const bool big = flop >= 2e9 && (tpb >= 32 || tpb * nb1 * nb2 >= 512) && t_split < t_exact;
     const bool ok = beta == 0.0 && K > 0 && M >= 256 && N >= 256 && K % 8 == 0 && (!a_mc || M % 8 == 0) &&
                     (!b_mc || N % 8 == 0) && C.scalar_type() == at::kFloat && nb1 * nb2 * 3 * nseg <= 65535;
     TORCH_CHECK(mode != 4 || ok, "xdot.gemm: path 4 (split fp32) not eligible for this call");

@@ -14,6 +14,8 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || e
 timeout -k 10 300 python benchmarks/bench_rank.py --world 2 4 8 --steps 20 --warmup 5 > $O/rank.log 2>&1 || exit $?
 timeout -k 10 300 python benchmarks/bench_rank.py --world 2 4 8 --steps 20 --warmup 5 --link-gbps 300 --p2p-gbps 64 > $O/rank_link.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --dtype fp32 --steps 5 --warmup 2 > $O/bench_fp32.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --impl materialized --steps 5 --warmup 2 > $O/bench_mat.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --impl materialized --dtype fp32 --steps 3 --warmup 1 > $O/bench_mat_fp32.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o prof \
   -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 > $GRAFT_REPO_ROOT/$O/prof.log 2>&1 || exit $?
