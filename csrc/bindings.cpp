@@ -1017,6 +1017,57 @@ void ipc_reduce_scatter(const at::Tensor& inp, at::Tensor& out, at::IntArrayRef 
   check_launch(hipGetLastError(), "ipc_reduce_scatter");
 }
 
+// ---- HIP graph node priorities: diagnostics (benchmarks/micro/graph_prio_probe.py) ----
+// Stream capture records the fork/join topology but not the stream priorities, and on ROCm 7.2
+// hipGraphKernelNodeSetAttribute(.., hipKernelNodeAttributePriority, ..) returns invalid
+// argument, so a captured two-stream backward cannot get its priority back
+// (profiles/r3_graph.md); these two ops let the probe re-check a newer runtime.
+void graph_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) (void)hipGetLastError();  // do not leave the error for the next HIP call
+  TORCH_CHECK(e == hipSuccess, "xdot.", what, ": ", hipGetErrorString(e));
+}
+
+bool is_kernel_node(hipGraphNode_t n) {
+  hipGraphNodeType t;
+  return hipGraphNodeGetType(n, &t) == hipSuccess && t == hipGraphNodeTypeKernel;
+}
+
+// priorities of every kernel node of a graph (diagnostics / tests)
+std::vector<int64_t> graph_kernel_priorities(int64_t raw) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>((uintptr_t)raw);
+  size_t n = 0;
+  graph_ok(hipGraphGetNodes(g, nullptr, &n), "graph_kernel_priorities");
+  std::vector<hipGraphNode_t> nodes(n);
+  graph_ok(hipGraphGetNodes(g, nodes.data(), &n), "graph_kernel_priorities");
+  std::vector<int64_t> out;
+  for (auto nd : nodes) {
+    if (!is_kernel_node(nd)) continue;
+    hipKernelNodeAttrValue v{};
+    graph_ok(hipGraphKernelNodeGetAttribute(nd, hipKernelNodeAttributePriority, &v), "graph_kernel_priorities");
+    out.push_back(v.priority);
+  }
+  return out;
+}
+
+// set the priority attribute of the i-th kernel node of a graph (diagnostics)
+void graph_set_kernel_priority(int64_t raw, int64_t index, int64_t prio) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>((uintptr_t)raw);
+  size_t n = 0;
+  graph_ok(hipGraphGetNodes(g, nullptr, &n), "graph_set_kernel_priority");
+  std::vector<hipGraphNode_t> nodes(n);
+  graph_ok(hipGraphGetNodes(g, nodes.data(), &n), "graph_set_kernel_priority");
+  int64_t k = 0;
+  for (auto nd : nodes) {
+    if (!is_kernel_node(nd)) continue;
+    if (k++ != index) continue;
+    hipKernelNodeAttrValue v{};
+    v.priority = (int)prio;
+    graph_ok(hipGraphKernelNodeSetAttribute(nd, hipKernelNodeAttributePriority, &v), "graph_set_kernel_priority");
+    return;
+  }
+  TORCH_CHECK(false, "xdot.graph_set_kernel_priority: no kernel node ", index);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(xdot, m) {
@@ -1061,9 +1112,13 @@ TORCH_LIBRARY(xdot, m) {
         "int ticks, int nwg) -> ()");
   m.def("ipc_reduce_scatter(Tensor inp, Tensor(a!) out, int[] stage, int[] sig, int status, int rank, int epoch, "
         "int ticks, int nwg) -> ()");
+  m.def("graph_kernel_priorities(int graph) -> int[]");
+  m.def("graph_set_kernel_priority(int graph, int index, int prio) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
+  m.impl("graph_kernel_priorities", &graph_kernel_priorities);
+  m.impl("graph_set_kernel_priority", &graph_set_kernel_priority);
   m.impl("flash_splits", &flash_splits);
   m.impl("ipc_info", &ipc_info);
   m.impl("ipc_alloc", &ipc_alloc);
