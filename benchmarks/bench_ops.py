@@ -48,6 +48,10 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-local", action="store_true", help="skip the single-GPU torch.matmul baseline")
     ap.add_argument("--file", default=None, help="JSON list to append the record to")
+    ap.add_argument("--trials", type=int, default=1,
+                    help="records to append (the reference's files hold 100 trials): record 0 is the "
+                         "summary record above; records 1.. carry one synchronised call each "
+                         "(distributed_time / total_time of that call, max over ranks)")
     ap.add_argument("--p2p-gbps", type=float, default=None, help="emulated ring-hop link rate (GB/s, --emulate)")
     ap.add_argument("--schedule", default=None, choices=["gather", "ring"],
                     help="product schedule (default XDOT_OPS_SCHEDULE / gather); also used by the *_fb modes")
@@ -97,8 +101,10 @@ def timed(fn, args, iters, warmup):
             t0 = time.perf_counter()
             fn(*args)
             ts.append((time.perf_counter() - t0) * 1e3)
+    raw = list(ts)
     ts.sort()
-    return {"ms_p50": statistics.median(ts), "ms_p90": ts[min(len(ts) - 1, int(0.9 * len(ts)))], "ms_min": ts[0]}
+    return {"ms_p50": statistics.median(ts), "ms_p90": ts[min(len(ts) - 1, int(0.9 * len(ts)))], "ms_min": ts[0],
+            "all_ms": raw}
 
 
 def main(argv=None):
@@ -127,6 +133,7 @@ def main(argv=None):
     rec = {"mode": a.mode, "schedule": a.schedule or "gather", "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype,
            "link_gbps": a.link_gbps, "p2p_gbps": a.p2p_gbps}
 
+    local_trials = []
     fb = a.mode.endswith("_fb")
     torch.set_grad_enabled(fb)
     # single-GPU torch baseline on the full problem (reference: rank 0 only)
@@ -144,7 +151,9 @@ def main(argv=None):
         rec["total_time"] = t_cold
         rec["peak_memory"] = pk
         rec["output_memory"] = y.numel() * y.element_size()
-        rec["local_" + "ms_p50"] = timed(torch.matmul, args, max(3, a.iters // 2), 1)["ms_p50"]
+        lt = timed(torch.matmul, args, max(3, a.iters // 2, a.trials - 1), 1)
+        rec["local_" + "ms_p50"] = lt["ms_p50"]
+        local_trials = lt["all_ms"]
         del args, y
         if dev.type == "cuda":
             torch.cuda.empty_cache()
@@ -182,7 +191,7 @@ def main(argv=None):
     y, t_cold, pk = cold_call(fn, left, right)
     out_mem = y.numel() * y.element_size()
     del y
-    stats = timed(fn, (left, right), a.iters, a.warmup)
+    stats = timed(fn, (left, right), max(a.iters, a.trials - 1), a.warmup)
     vals = comm.all_gather_object((din, t_cold, pk, out_mem, stats))
     if rank == 0:
         avg = lambda i: sum(v[i] for v in vals) / n  # noqa: E731
@@ -197,9 +206,19 @@ def main(argv=None):
             "ms_min": max(v[4]["ms_min"] for v in vals),
         })
         print(json.dumps(rec), flush=True)
+        recs = [rec]
+        for i in range(a.trials - 1):  # one record per synchronised call, in call order
+            r = {k: rec[k] for k in ("mode", "schedule", "world_size", "emulated", "T", "D", "offset", "dtype",
+                                     "input_memory", "peak_memory", "output_memory", "distributed_input_memory",
+                                     "distributed_peak_memory", "distributed_output_memory") if k in rec}
+            r["trial"] = i + 1
+            if i < len(local_trials):
+                r["total_time"] = local_trials[i] / 1e3
+            r["distributed_time"] = max(v[4]["all_ms"][i] for v in vals) / 1e3
+            recs.append(r)
         if a.file:
             data = json.load(open(a.file)) if os.path.exists(a.file) else []
-            data.append(rec)
+            data.extend(recs)
             json.dump(data, open(a.file, "w"), indent=1)
     comm.barrier()
     ctx.__exit__(None, None, None)

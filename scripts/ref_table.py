@@ -10,7 +10,8 @@ import statistics
 import sys
 
 ref_dir, ours_dir = sys.argv[1], sys.argv[2]
-print("| file | reference median distributed_time s (cold, unsynced) | xdot cold unsynced s | xdot synced p50 s | speed-up (ref median / xdot p50) |")
+print("| file | reference median distributed_time s, cold, unsynced (records) | xdot cold unsynced s | "
+      "xdot synced median s (records) | speed-up (ref median / xdot median) |")
 print("|---|---|---|---|---|")
 for f in sorted(glob.glob(os.path.join(ours_dir, "*.json"))):
     name = os.path.basename(f)
@@ -18,7 +19,10 @@ for f in sorted(glob.glob(os.path.join(ours_dir, "*.json"))):
     if not os.path.exists(rp):
         continue
     ref = json.load(open(rp))  # plain JSON (safe loader)
-    ours = json.load(open(f))[-1]
+    recs = json.load(open(f))
+    ours = [r for r in recs if "cold_unsynced_s" in r][-1]  # the summary record (trial records follow it)
+    trials = [r["distributed_time"] for r in recs if "trial" in r]
     rm = statistics.median(r["distributed_time"] for r in ref)
-    p50 = ours["ms_p50"] / 1e3
-    print(f"| `{name}` | {rm:.4f} | {ours['cold_unsynced_s']:.4f} | {p50:.5f} | {rm / p50:.0f}x |")
+    p50 = statistics.median(trials) if trials else ours["ms_p50"] / 1e3
+    print(f"| `{name}` | {rm:.4f} ({len(ref)}) | {ours['cold_unsynced_s']:.4f} | {p50:.5f} ({len(trials) or 1}) "
+          f"| {rm / p50:.0f}x |")
