@@ -122,6 +122,19 @@ def test_bench_ops_records_gloo(tmp_path, mode):
     assert rec["ms_p50"] > 0 and rec["distributed_time"] > 0
 
 
+def test_bench_ops_trial_records(tmp_path):
+    """--trials K: the summary record, then K-1 one-call trial records (the reference's files
+    hold 100 trials), each with the reference's timing keys."""
+    f = tmp_path / "nt.json"
+    _run(["benchmarks/bench_ops.py", "--mode", "nt", "--T", "96", "--dim", "16", "--emulate", "3",
+          "--iters", "2", "--warmup", "0", "--trials", "4", "--file", str(f)])
+    data = json.loads(f.read_text())
+    assert len(data) == 4 and "cold_unsynced_s" in data[0]
+    assert [r["trial"] for r in data[1:]] == [1, 2, 3]
+    for r in data[1:]:
+        assert r["distributed_time"] > 0 and r["total_time"] > 0 and r["world_size"] == 3
+
+
 def test_bench_ops_fwd_bwd_mode_emulated():
     out = _run(["benchmarks/bench_ops.py", "--mode", "leftT_fb", "--T", "96", "--dim", "16", "--emulate", "3",
                 "--iters", "1", "--warmup", "0"])
