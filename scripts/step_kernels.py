@@ -26,7 +26,6 @@ def main():
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     ad = [i for i, r in enumerate(rows) if "adamw_kernel" in r["Kernel_Name"]]
-    per = max(1, len(ad) // max(1, len({r["Kernel_Name"] for r in rows if "mse_final" in r["Kernel_Name"]}) or 1))
     # one mse_final per step: steps = number of mse_final launches after the first AdamW
     mse = [i for i, r in enumerate(rows) if "mse_final" in r["Kernel_Name"] and i > ad[0]]
     steps = len(mse)
@@ -38,7 +37,6 @@ def main():
         e[0] += 1
         e[1] += d
     span = (int(rows[hi]["End_Timestamp"]) - int(rows[lo]["End_Timestamp"])) / 1e6
-    del per
     print(f"{steps} steps in the window, {span / steps:.3f} ms/step (timestamps)\n")
     print("| kernel | calls/step | µs/step | avg µs |\n|---|---|---|---|")
     for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
