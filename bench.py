@@ -36,8 +36,9 @@ METRIC = "ms/fwd+bwd DistributedDotProductAttn T=25000 d=768 h=8; scaling 1/2/4/
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first (10: about 1 %% faster timed steps than 3 on the same box, scripts/warm_ab.sh)")
     ap.add_argument("--seq-len", type=int, default=25000, help="global T")
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--heads", type=int, default=8)
