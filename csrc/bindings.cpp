@@ -220,10 +220,19 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     // worth it when three bf16 products plus the operand copies (read 4 B, write 6 B per
     // element) beat one exact fp32 product: a product whose operand is far larger than its
     // output (the materialised P.V: 2.5 GB of P per head) keeps the exact kernel
+    // Both sides are priced at the fraction of the 256 CUs their grid fills: the exact kernel
+    // has no split-K (128x128 tiles), gemm3 splits K (pick_splits), so a product with few
+    // output tiles and a long K (the K = T weight-side products of the autograd ops) goes split.
     const double flop = 2.0 * (double)M * N * K * nseg * nb1 * nb2;
     const double elems = (double)nb1 * nb2 * nseg * K * ((double)M + (double)N);
-    const double t_split = 3.0 * flop / 1.1e15 + 10.0 * elems / 5e12, t_exact = flop / 1.15e14;
-    const bool big = flop >= 2e9 && (tpb >= 32 || tpb * nb1 * nb2 >= 512) && t_split < t_exact;
+    const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * nb1 * nb2;
+    const int64_t s3 = pick_splits(tpb * nb1 * nb2, 3 * nseg * ((K + 63) / 64));
+    const double fill1 = std::min(1.0, (double)t128 / 256.0);
+    const double fill3 = std::min(1.0, (double)(tpb * nb1 * nb2 * s3) / 256.0);
+    const double t_split = 3.0 * flop / (1.1e15 * fill3) + 10.0 * elems / 5e12 +
+                           (s3 > 1 ? 8.0 * (double)s3 * M * N * nb1 * nb2 / 5e12 : 0.0);
+    const double t_exact = flop / (1.15e14 * fill1);
+    const bool big = flop >= 2e9 && t_split < t_exact;
     const bool ok = beta == 0.0 && K > 0 && M >= 256 && N >= 256 && K % 8 == 0 && (!a_mc || M % 8 == 0) &&
                     (!b_mc || N % 8 == 0) && C.scalar_type() == at::kFloat && nb1 * nb2 * 3 * nseg <= 65535;
     TORCH_CHECK(mode != 4 || ok, "xdot.gemm: path 4 (split fp32) not eligible for this call");
