@@ -8,6 +8,8 @@ Synthetic random inputs, random-init weights, bf16 compute, the reference's all-
 boolean mask (``example.py:29``) is passed and honoured.
 
     python bench.py --gpus 1 --steps 10 --warmup 3
+    python bench.py --gpus 8 --steps 20 --warmup 5        # starts the 8-rank torchrun job itself
+    python bench.py --sweep 1,2,4,8                        # one line per N + a scaling summary
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
 
@@ -35,7 +37,12 @@ METRIC = "ms/fwd+bwd DistributedDotProductAttn T=25000 d=768 h=8; scaling 1/2/4/
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU).  Without a launcher in the environment, N > 1 starts the "
+                         "N-rank torchrun job itself")
+    ap.add_argument("--sweep", default=None,
+                    help="comma-separated N list (e.g. 1,2,4,8): run each N in fresh processes, print one "
+                         "JSON line per N and a speed-up / efficiency summary line")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10,
                     help="untimed steps first (10: about 1 %% faster timed steps than 3 on the same box, scripts/warm_ab.sh)")
@@ -86,7 +93,8 @@ def numerics_check(a, comm, dev, dt, impl, T: int = 512, tol: float = 3e-2) -> f
     R = T // n
     torch.manual_seed(4321)  # identical weights on every rank
     m = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, impl=impl, comm=comm).to(dev, dt)
-    ref = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, distributed=False).to(dev, torch.float32)
+    ref = xdot.DistributedDotProductAttn(a.dim, num_heads=a.heads, distributed=False, impl="materialized",
+                                         backend="torch").to(dev, torch.float32)  # plain torch ops
     ref.load_state_dict({k: v.float() for k, v in m.state_dict().items()})
     g = torch.Generator(device=dev).manual_seed(99)  # identical full inputs on every rank
     xf = torch.rand(1, T, a.dim, device=dev, generator=g)
@@ -219,10 +227,98 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
     return ms, (th - t0) * 1e3 / max(1, steps), lossv, impl
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child_argv(argv, gpus: int):
+    """This invocation's arguments with --gpus replaced (and --sweep dropped)."""
+    out, skip = [], False
+    for i, x in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if x in ("--gpus", "--sweep"):
+            skip = True
+            continue
+        if x.startswith("--gpus=") or x.startswith("--sweep="):
+            continue
+        out.append(x)
+    return ["--gpus", str(gpus)] + out
+
+
+def _launch_cmd(argv, gpus: int):
+    """Command that runs this bench as a ``gpus``-rank job: torchrun (one rank per GPU over
+    RCCL, rendezvous on 127.0.0.1) for gpus > 1, a plain child for gpus == 1."""
+    me = os.path.abspath(__file__)
+    if gpus == 1:
+        return [sys.executable, me] + _child_argv(argv, 1)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), me] + _child_argv(argv, gpus)
+
+
+def _check_gpu_count(a) -> None:
+    # torch.cuda.device_count() does not initialise HIP on this image: safe before a launch
+    if a.device == "cuda":
+        have = torch.cuda.device_count()
+        if have and a.gpus > have:
+            print(f"bench.py: --gpus {a.gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            raise SystemExit(2)
+
+
+def self_launch(argv, a) -> int:
+    """``python bench.py --gpus N`` without a launcher (no WORLD_SIZE in the environment):
+    start the N-rank job ourselves, BEFORE any GPU call in this process, as a torchrun child
+    (the reference's equivalent is ``horovodrun -np N``, README.md:77).  The child's rank 0
+    prints the one JSON line on our stdout; its exit code is ours."""
+    import subprocess
+
+    _check_gpu_count(a)
+    return subprocess.call(_launch_cmd(argv, a.gpus))
+
+
+def sweep(argv, ns) -> int:
+    """``--sweep 1,2,4,8``: each N in fresh processes, one JSON line per N (rank 0's record),
+    then one summary line with the speed-up and strong-scaling efficiency against the N=1 run."""
+    import subprocess
+
+    recs = {}
+    rc_all = 0
+    for n in ns:
+        p = subprocess.run(_launch_cmd(argv, n), stdout=subprocess.PIPE, text=True)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode != 0 or not lines:
+            print(json.dumps({"sweep_n": n, "error": f"exit {p.returncode}"}), flush=True)
+            rc_all = rc_all or (p.returncode or 1)
+            continue
+        rec = json.loads(lines[-1])
+        recs[n] = rec
+        print(json.dumps(rec), flush=True)
+    if recs:
+        base_n = min(recs)
+        base = recs[base_n]["ms_per_step"] * base_n
+        summ = {"sweep": sorted(recs), "ms_per_step": {n: recs[n]["ms_per_step"] for n in sorted(recs)},
+                "speedup_vs_n1": {n: round(recs[base_n]["ms_per_step"] / recs[n]["ms_per_step"], 3) for n in sorted(recs)}
+                if base_n == 1 else None,
+                "strong_scaling_efficiency": {n: round(base / (n * recs[n]["ms_per_step"]), 3) for n in sorted(recs)},
+                "metric": recs[base_n]["metric"]}
+        print(json.dumps(summ), flush=True)
+    return rc_all
+
+
 def main(argv=None, comm=None):
     """``comm``: optional communicator override (``benchmarks/bench_rank.py`` passes an
     :class:`xdot.utils.comm.EmulatedComm` to run one rank of an N-GPU step on one GPU)."""
+    raw = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    if comm is None and a.sweep:
+        raise SystemExit(sweep(raw, [int(x) for x in a.sweep.split(",") if x.strip()]))
+    if comm is None and a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(raw, a))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from xdot.utils import comm as C
     from xdot.utils.env import FLAGS

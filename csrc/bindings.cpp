@@ -96,16 +96,6 @@ int64_t pick_splits(int64_t tiles, int64_t kt64) {
   return S;
 }
 
-// XDOT_FP32_MODE: split (default) = large fp32 products run as three bf16 products (hi/lo
-// halves) on gemm3; exact = the exact-fp32 MFMA kernel / library GEMM
-int fp32_split() {
-  static const int v = [] {
-    const char* e = std::getenv("XDOT_FP32_MODE");
-    return (e && e[0] == 'e') ? 0 : 1;
-  }();
-  return v;
-}
-
 // XDOT_GEMM3: 1 (default) = the automatic path tries the 8-phase kernel first (csrc/gemm3.hip)
 int gemm3_auto() {
   static const int v = [] {
@@ -212,10 +202,12 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
   // v2 (256x256 tiles, LDS-DMA, csrc/gemm2.hip) for 16-bit operands whose layout meets its
   // alignment rules and whose output fills 256-wide tiles; split-K when the tiles alone would
   // leave CUs idle.  path: 0 = auto, 1 = v1, 2 = v2 whenever its layout rules hold (per call)
-  const int mode = (int)path;
-  // fp32 operands on the bf16 matrix pipe (XDOT_FP32_MODE=split, the default; path 4 forces it):
-  // hi/lo bf16 copies, three bf16 products in one gemm3 call (csrc/gemm3.hip, split3_kernel)
-  if (A.scalar_type() == at::kFloat && (mode == 4 || (mode == 0 && fp32_split() && gemm3_auto()))) {
+  int mode = (int)path;
+  // fp32 operands on the bf16 matrix pipe (path 6 = automatic with split allowed, which Python
+  // passes under XDOT_FP32_MODE=split; path 4 forces it): hi/lo bf16 copies, three bf16 products
+  // in one gemm3 call (csrc/gemm3.hip, split3_kernel).  The mode is decided in Python only
+  // (xdot.ops.gemm.strided_gemm reads FLAGS.fp32_mode per call): no second source of truth here.
+  if (A.scalar_type() == at::kFloat && (mode == 4 || (mode == 6 && gemm3_auto()))) {
     const int64_t tpb = ((M + 255) / 256) * ((N + 255) / 256);
     // worth it when three bf16 products plus the operand copies (read 4 B, write 6 B per
     // element) beat one exact fp32 product: a product whose operand is far larger than its
@@ -232,7 +224,15 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     const double t_split = 3.0 * flop / (1.1e15 * fill3) + 10.0 * elems / 5e12 +
                            (s3 > 1 ? 8.0 * (double)s3 * M * N * nb1 * nb2 / 5e12 : 0.0);
     const double t_exact = flop / (1.15e14 * fill1);
-    const bool big = flop >= 2e9 && t_split < t_exact;
+    // the hi/lo copies are transient HBM (6 B per operand element): never more than a quarter of
+    // what is free, else the exact kernel (no extra memory) runs
+    const double copy_bytes = 6.0 * elems;
+    bool fits = copy_bytes < 1e9;
+    if (!fits) {
+      size_t fr = 0, tot = 0;
+      fits = hipMemGetInfo(&fr, &tot) == hipSuccess && copy_bytes < 0.25 * (double)fr;
+    }
+    const bool big = flop >= 2e9 && t_split < t_exact && fits;
     const bool ok = beta == 0.0 && K > 0 && M >= 256 && N >= 256 && K % 8 == 0 && (!a_mc || M % 8 == 0) &&
                     (!b_mc || N % 8 == 0) && C.scalar_type() == at::kFloat && nb1 * nb2 * 3 * nseg <= 65535;
     TORCH_CHECK(mode != 4 || ok, "xdot.gemm: path 4 (split fp32) not eligible for this call");
@@ -271,6 +271,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
       return;
     }
   }
+  if (mode == 6) mode = 0;
   if (mode == 0 && gemm_lib() &&
       gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
                    b_mc, alpha, beta))

@@ -389,9 +389,6 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
       f32x4& xr = acc[4 * j + mt][2 * i];
       f32x4& yr = acc[4 * j + mt][2 * i + 1];
       f32x4 x = xr, y = yr;
-#ifdef G3_DIAG_NOSTORE
-      if (x[0] == 12345.f && y[1] == -7.f) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff, 0, 0);
-#else
       if constexpr (EPI == 0) {
         x *= alpha;
         y *= alpha;
@@ -408,7 +405,6 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rs, voff + 512 * i, 0, G3_STORE_AUX);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, voff + 512 * i + 64, 0, G3_STORE_AUX);
       }
-#endif
       xr = f32x4{0.f, 0.f, 0.f, 0.f};
       yr = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -451,22 +447,14 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs p, float* __restric
           va[e] = lo8 ? d[0][e] : recv;
           vb[e] = lo8 ? recv : d[1][e];
         }
-#ifndef G3_DIAG_NOSTORE
         __builtin_amdgcn_raw_buffer_store_b128(va, rs, voff_fl, 0, G3_STORE_AUX);
         __builtin_amdgcn_raw_buffer_store_b128(vb, rs, voff_fl + (int)(8 * ldo * 2), 0, G3_STORE_AUX);
-#else
-        if (va[0] == 12345u && vb[1] == 7u) __builtin_amdgcn_raw_buffer_store_b128(va, rs, voff_fl, 0, 0);
-#endif
       }
     }
   };
   // store instructions of one quadrant per lane (exact: the vmcnt waits around an item boundary
   // count them)
-#ifdef G3_DIAG_NOSTORE
-  constexpr int SPQ = 0;
-#else
   constexpr int SPQ = EPI == 0 ? 4 : 8;
-#endif
   // FL: 8 stores per row block j: j = 0 in the last k-tile's q2, j = 1 after it
   constexpr int SPH = 2 * SPQ;
 
@@ -670,8 +658,16 @@ __global__ __launch_bounds__(256) void split3_kernel(Split3Args a) {
   const int z2 = (int)(t % a.nb2);
   const int z1 = (int)(t / a.nb2);
   const float x = a.src[z1 * a.s1 + z2 * a.s2 + seg * a.sseg + (int64_t)r * a.ld + c];
-  const __bf16 hi = (__bf16)x;
-  const __bf16 lo = (__bf16)(x - (float)hi);
+  __bf16 hi = (__bf16)x;
+  __bf16 lo = (__bf16)(x - (float)hi);
+  if (!__builtin_isfinite(x)) {
+    lo = (__bf16)0.f;  // inf / NaN: hi carries it (inf - inf would make lo a NaN)
+  } else if (!__builtin_isfinite((float)hi)) {
+    // |x| near FLT_MAX rounds up to inf in bf16: truncate toward zero instead, the residual stays finite
+    const float ht = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & 0xFFFF0000u);
+    hi = (__bf16)ht;
+    lo = (__bf16)(x - ht);
+  }
   const int64_t RC = (int64_t)a.R * a.C;
   __bf16* d = a.dst + ((int64_t)(z1 * a.nb2 + z2) * 3 * a.nseg + seg) * RC + (int64_t)r * a.C + c;
 #pragma unroll

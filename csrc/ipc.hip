@@ -110,11 +110,19 @@ __global__ __launch_bounds__(256) void all_gather_kernel(Args a) {
   uint32_t* done = a.sig[a.rank] + MAXR * MAXG;
   int64_t v0, v1;
   range_of(a, w, v0, v1);
-  // 1. our slot is free once every peer finished reading it two collectives ago (an expired
-  //    wait here only delays the peer that stopped; the error word is set)
+  // 1. our slot is free once every peer finished reading it two collectives ago.  If that wait
+  //    expires, a (merely slow) peer may still be reading the old epoch's bytes: overwriting the
+  //    slot and raising our flag would hand it the new bytes as the old ones.  So this range is
+  //    neither staged nor published (the peers' waits expire and poison theirs: loud on every
+  //    rank) and our own output range is poisoned.
+  bool busy = false;
   if (a.epoch > 2)
     for (int p = 0; p < a.n; ++p)
-      if (p != a.rank) wait_ge(done + p * MAXG + w, (uint32_t)(a.epoch - 2), a);
+      if (p != a.rank) busy |= wait_ge(done + p * MAXG + w, (uint32_t)(a.epoch - 2), a);
+  if (busy) {
+    for (int p = 0; p < a.n; ++p) poison_units(a.out + p * a.shard, v0, v1);
+    return;
+  }
   // 2. stage range w (and our own output block), publish
   copy_units(a.stage[a.rank], a.src, v0, v1);
   copy_units(a.out + a.rank * a.shard, a.src, v0, v1);
@@ -169,9 +177,14 @@ __global__ __launch_bounds__(256) void reduce_scatter_kernel(Args a) {
   uint32_t* done = a.sig[a.rank] + MAXR * MAXG;
   int64_t v0, v1;
   range_of(a, w, v0, v1);
+  bool busy = false;  // slot still being read by a peer: no stage / publish (see all_gather_kernel)
   if (a.epoch > 2)
     for (int p = 0; p < a.n; ++p)
-      if (p != a.rank) wait_ge(done + p * MAXG + w, (uint32_t)(a.epoch - 2), a);
+      if (p != a.rank) busy |= wait_ge(done + p * MAXG + w, (uint32_t)(a.epoch - 2), a);
+  if (busy) {
+    poison_units(a.out, v0, v1);
+    return;
+  }
   // stage range w of every block (peer p reads block p)
   for (int p = 0; p < a.n; ++p)
     if (p != a.rank) copy_units(a.stage[a.rank] + p * a.shard, a.src + p * a.shard, v0, v1);

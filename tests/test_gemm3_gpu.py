@@ -130,3 +130,48 @@ def test_gemm3_split_fp32_split_k(gpu):
     strided_gemm(A.float().to(gpu), B.float().to(gpu), C, M=256, N=256, K=4104, lda=4104, ldb=4104, ldc=256, path=4)
     ref = A.float().double() @ B.float().double().t()
     assert _rel_fro(C.cpu(), ref) <= 2e-5
+
+
+def test_fp32_default_is_exact_non_integer(gpu):
+    """the distributed products' fp32 GEMMs run EXACT fp32 by default (XDOT_FP32_MODE
+    unset), checked on non-integer data against fp64 at torch-fp32 tolerance -- a split-bf16
+    route (~1e-5) would fail this bound; split runs only when asked for."""
+    from xdot.ops.gemm import strided_gemm
+    from xdot.utils.env import FLAGS
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    M, N, K = 1024, 1024, 2048
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(N, K, generator=g, dtype=torch.float64)
+    ref = A.float().double() @ B.float().double().t()
+    old = FLAGS.fp32_mode
+    try:
+        FLAGS.fp32_mode = "exact"
+        C = torch.empty(M, N, device=gpu)
+        strided_gemm(A.float().to(gpu), B.float().to(gpu), C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N)
+        assert _rel_fro(C.cpu(), ref) <= 2e-6
+        FLAGS.fp32_mode = "split"
+        C2 = torch.empty(M, N, device=gpu)
+        strided_gemm(A.float().to(gpu), B.float().to(gpu), C2, M=M, N=N, K=K, lda=K, ldb=K, ldc=N)
+        assert _rel_fro(C2.cpu(), ref) <= 2e-5
+    finally:
+        FLAGS.fp32_mode = old
+
+
+def test_split_fp32_non_finite_inputs(gpu):
+    """split3: an inf operand gives inf (not NaN) products; |x| near FLT_MAX stays finite in hi/lo."""
+    from xdot.ops.gemm import strided_gemm
+
+    M = N = 256
+    K = 64
+    A = torch.ones(M, K, device=gpu)
+    B = torch.full((N, K), 1e-3, device=gpu)
+    A[3, 5] = float("inf")
+    A[7, 9] = 3.3e38  # rounds to +inf in bf16: hi must be truncated instead
+    C = torch.empty(M, N, device=gpu)
+    strided_gemm(A, B, C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, path=4)
+    ref = (A.double().cpu() @ B.double().cpu().t())
+    assert torch.isinf(C[3]).all() and not torch.isnan(C).any()
+    ok = torch.ones(M, dtype=torch.bool)
+    ok[3] = False
+    assert torch.allclose(C.cpu().double()[ok], ref[ok], rtol=2e-5, atol=1e-6)

@@ -36,8 +36,9 @@ def _module_case(rank, ws, impl, masked, dtype="bf16"):
     mask_full[..., torch.arange(T), torch.arange(T)] = False
     mask_full = mask_full.to(dev)
     rdt = torch.float32 if dtype == "bf16" else torch.float64
+    # ground truth: plain torch ops only (no xdot kernel anywhere in the reference)
     ref = xdot.DistributedDotProductAttn(D, num_heads=H, distributed=False, impl="materialized",
-                                         add_bias=True).to(dev, rdt)
+                                         add_bias=True, backend="torch").to(dev, rdt)
     ref.load_state_dict({k: v.to(rdt) for k, v in m.state_dict().items()})
     xf = x_full.to(rdt).clone().requires_grad_(True)
     ref_out = ref(xf, xf, xf, mask_full)
@@ -143,7 +144,8 @@ def test_module_materialized_fp32_default_offset(gpu):
     with use_comm(LocalComm()):
         m = xdot.DistributedDotProductAttn(D, num_heads=H, impl="materialized").to(gpu)
         assert m.offset == 32
-        ref = xdot.DistributedDotProductAttn(D, num_heads=H, distributed=False, impl="materialized").to(gpu, torch.float64)
+        ref = xdot.DistributedDotProductAttn(D, num_heads=H, distributed=False, impl="materialized",
+                                             backend="torch").to(gpu, torch.float64)
         ref.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
         x = torch.rand(1, T, D, device=gpu, requires_grad=True)
         mask = torch.rand(1, T, T, device=gpu) < 0.3

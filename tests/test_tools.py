@@ -65,12 +65,34 @@ def test_bench_contract_cpu():
 
 
 def test_bench_rejects_wrong_world_size():
-    """--gpus 2 under a 1-rank launch exits non-zero instead of timing the wrong job."""
-    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--seq-len", "64", "--dim", "32",
-                        "--heads", "2", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=_env(), capture_output=True,
-                       text=True, timeout=240)
+    """--gpus 2 under a 1-rank LAUNCHER exits 2 instead of timing the wrong job."""
+    p = subprocess.run([sys.executable] + _torchrun(1) + ["bench.py", "--gpus", "2", "--device", "cpu", "--backend",
+                       "gloo", "--seq-len", "64", "--dim", "32", "--heads", "2", "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
     assert p.returncode != 0 and "rank(s)" in p.stderr, (p.returncode, p.stderr[-2000:])
     assert not _json_lines(p.stdout)
+
+
+def test_bench_self_launch_two_ranks():
+    """``python bench.py --gpus 2`` with no launcher starts the 2-rank job itself (VERDICT r3
+    item 2; reference launch: ``horovodrun -np N``, README.md:77): ONE record, world_size 2."""
+    out = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--dtype", "fp32",
+                "--seq-len", "128", "--dim", "64", "--heads", "4", "--steps", "2", "--warmup", "1"])
+    recs = _json_lines(out)
+    assert len(recs) == 1, out
+    assert recs[0]["world_size"] == 2 and recs[0]["n_gpus"] == 2 and recs[0]["config"]["parallelism"] == "sp2"
+
+
+def test_bench_sweep():
+    """``--sweep 1,2``: one record per N from fresh processes, then the scaling summary."""
+    out = _run(["bench.py", "--sweep", "1,2", "--device", "cpu", "--backend", "gloo", "--dtype", "fp32",
+                "--seq-len", "128", "--dim", "64", "--heads", "4", "--steps", "2", "--warmup", "1", "--no-check"])
+    recs = _json_lines(out)
+    assert len(recs) == 3, out
+    assert [r["n_gpus"] for r in recs[:2]] == [1, 2]
+    summ = recs[2]
+    assert summ["sweep"] == [1, 2] and set(summ["strong_scaling_efficiency"]) == {"1", "2"}
+    assert summ["strong_scaling_efficiency"]["1"] == 1.0
 
 
 @pytest.mark.parametrize("impl", ["auto", "ring"])

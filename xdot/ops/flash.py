@@ -193,9 +193,9 @@ FP32_MODES = {"exact": 0, "split": 1}
 
 
 def fp32_code(dtype: torch.dtype, mode: Optional[str] = None) -> int:
-    """Kernel family of fp32 operands: 1 split-bf16 (``csrc/flash_x3.hip``, default: 3 bf16 MFMAs
-    per product, <= 9e-6 relative error vs fp64), 0 exact fp32 (``csrc/flash_f32.hip``, ~5e-7;
-    profiles/r3_fp32_split.md).  ``mode`` None: ``XDOT_FP32_MODE``.  0 for 16-bit dtypes."""
+    """Kernel family of fp32 operands: 0 exact fp32 (``csrc/flash_f32.hip``, the default: ~5e-7
+    relative error vs fp64, the reference's precision), 1 split-bf16 (``csrc/flash_x3.hip``,
+    opt-in: 3 bf16 MFMAs per product, <= 9e-6; profiles/r3_fp32_split.md).  ``mode`` None: ``XDOT_FP32_MODE``.  0 for 16-bit dtypes."""
     if dtype != torch.float32:
         return 0
     mode = FLAGS.fp32_mode if mode is None else mode

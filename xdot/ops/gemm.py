@@ -12,6 +12,7 @@ from typing import Optional
 import torch
 
 from .. import _ext
+from ..utils.env import FLAGS
 
 _HIP_IN = (torch.bfloat16, torch.float16, torch.float32)
 
@@ -28,7 +29,12 @@ def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0
 
     ``path``: 0 = automatic kernel choice, 1 = the 128x128 kernel, 2 = the 256x256 kernel, 3 = the 8-phase
     16x16x32 kernel (raises if it declines), 4 = fp32 as three bf16 products on it, 5 = the 8-phase kernel
-    where it takes the call, else the 256x256 one -- whenever the layout rules hold."""
+    where it takes the call, else the 256x256 one -- whenever the layout rules hold; 6 = automatic
+    with the split-fp32 route allowed (what path 0 becomes for fp32 operands under
+    ``XDOT_FP32_MODE=split``; the default ``exact`` keeps fp32 products on the exact fp32 MFMA kernel).
+    ``FLAGS.fp32_mode`` is read here on every call: the one source of truth for the GEMMs too."""
+    if path == 0 and A.dtype == torch.float32 and FLAGS.fp32_mode == "split":
+        path = 6
     _ext.ops().gemm(A, B, C, int(M), int(N), int(K), int(nseg), int(nb1), int(nb2), int(lda),
                     int(ldb), int(ldc), int(sA1), int(sA2), int(sB1), int(sB2), int(sC1), int(sC2),
                     int(sAseg), int(sBseg), bool(a_mc), bool(b_mc), float(alpha),

@@ -31,15 +31,16 @@ variable                    default   effect
                                       (default: rounded once to bf16/fp16 in the kernel)  [collective]
 ``XDOT_IPC``                0         all-gathers / reduce-scatters as native xGMI pull kernels over
                                       HIP IPC (``csrc/ipc.hip``)  [collective]
-``XDOT_IPC_MB``             512       IPC staging MiB per slot
+``XDOT_IPC_MB``             512       IPC staging MiB per slot (routes IPC vs RCCL by size)  [collective]
 ``XDOT_IPC_WGS``            64        workgroups (byte ranges) per IPC collective
 ``XDOT_IPC_TIMEOUT_S``      (comm)    bound of every IPC device-side wait
 ``XDOT_PRESCALE``           1         pre-multiply the row side by scale·log2 e once per forward
                                       (seeded score accumulators; forward 2.11 -> 1.98 ms)
-``XDOT_FP32_MODE``          split     fp32 flash kernels and large fp32 GEMMs (read by Python and C++):
-                                      ``split`` (hi/lo bf16 halves, 3 bf16 products: <= 9e-6 flash,
-                                      <= 2e-5 GEMM, relative vs fp64) or ``exact`` (fp32 MFMA /
-                                      library fp32 GEMM, ~5e-7); profiles/r3_fp32_split.md
+``XDOT_FP32_MODE``          exact     fp32 flash kernels and fp32 GEMMs (read by Python only, per
+                                      call; passed to the kernels): ``exact`` (fp32 MFMA, ~5e-7
+                                      relative vs fp64: the reference's precision) or ``split``
+                                      (opt-in, like TF32: hi/lo bf16 halves, 3 bf16 products:
+                                      <= 9e-6 flash, <= 2e-5 GEMM; profiles/r3_fp32_split.md)
 ``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
                                       1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
 ``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
@@ -103,7 +104,7 @@ class _Flags:
         self.ipc_wgs = _num("XDOT_IPC_WGS", 64, int)
         self.ipc_timeout_s = _num("XDOT_IPC_TIMEOUT_S", self.comm_timeout_s)
         self.prescale = _flag("XDOT_PRESCALE", default="1")
-        self.fp32_mode = _str("XDOT_FP32_MODE", "split")
+        self.fp32_mode = _str("XDOT_FP32_MODE", "exact")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
@@ -114,7 +115,7 @@ FLAGS = _Flags()
 
 # flags that change the number (or dtype) of the collectives an op issues
 COLLECTIVE_KNOBS = ("check", "chunk_budget_mb", "ops_schedule", "gather_chunks", "local_first", "grad_fp32",
-                    "ipc", "ipc_wgs")
+                    "ipc", "ipc_mb", "ipc_wgs")
 
 
 def collective_knobs() -> dict:

@@ -26,8 +26,9 @@ attention's local block) while the pull runs, and ``Handle.wait()`` orders it af
 Every device wait is bounded (``XDOT_IPC_TIMEOUT_S``, default: the process-group timeout
 ``XDOT_COMM_TIMEOUT_S``, 600 s, so a peer busy with host work such as checkpointing is not
 mistaken for a dead one): on expiry the kernel writes NaN over the output range that peer
-should have supplied (the result is unusable, never silently stale), sets a host-mapped error
-word and drains; the host raises at the next collective (and ``Handle.wait()`` checks too).
+should have supplied (the result is unusable), sets a host-mapped error word and drains; the
+host raises at the next collective (``Handle.wait()`` raises for earlier collectives, and for
+its own one only under ``XDOT_CHECK=1``, which synchronises on the kernel first).
 
 Enable with ``XDOT_IPC=1`` (``xdot.utils.comm.init`` wraps its RCCL communicator) or build one
 explicitly: ``IpcComm(comm)``.  The staging buffers hold ``XDOT_IPC_MB`` MiB per slot (two
@@ -58,13 +59,14 @@ class IpcError(RuntimeError):
 class _EventWork:
     """``wait()`` orders the caller's current stream after a recorded event (device-side)."""
 
-    __slots__ = ("ev",)
+    __slots__ = ("ev", "device")
 
-    def __init__(self, ev):
+    def __init__(self, ev, device):
         self.ev = ev
+        self.device = device
 
     def wait(self):
-        torch.cuda.current_stream().wait_event(self.ev)
+        torch.cuda.current_stream(self.device).wait_event(self.ev)
 
     def is_completed(self) -> bool:
         return self.ev.query()
@@ -99,11 +101,20 @@ class IpcComm(Communicator):
             self._sig = ops.ipc_alloc(int(sig_bytes), True)
             self._host, self._status = ops.ipc_host_word()
             mine = (ops.ipc_get_handle(self._stage).tolist(), ops.ipc_get_handle(self._sig).tolist(),
-                    os.getpid())
+                    os.getpid(), self.capacity, self.nwg)
             allh = base.all_gather_object(mine)
+            # routing (IPC vs the wrapped communicator) and the peers' stage offsets follow from
+            # the capacity, the flag partition from nwg: ranks that disagree would hang or read
+            # past a peer's staging allocation
+            shapes = {(c, w) for (_hs, _hg, _pid, c, w) in allh}
+            if len(shapes) != 1:
+                ops.ipc_free(self._stage)
+                ops.ipc_free(self._sig)
+                raise IpcError(f"IpcComm: ranks disagree on (staging bytes, workgroups): {sorted(shapes)} "
+                               f"(XDOT_IPC_MB / XDOT_IPC_WGS must match on every rank)")
             self._opened: List[int] = []
             self.stage_ptrs, self.sig_ptrs = [], []
-            for p, (hs, hg, _pid) in enumerate(allh):
+            for p, (hs, hg, _pid, _c, _w) in enumerate(allh):
                 if p == self.rank:
                     self.stage_ptrs.append(self._stage)
                     self.sig_ptrs.append(self._sig)
@@ -137,6 +148,14 @@ class IpcComm(Communicator):
             raise IpcError(f"rank {self.rank}: an xGMI pull collective timed out waiting for a peer "
                            f"(XDOT_IPC_TIMEOUT_S); its output is invalid")
 
+    def _post(self, ev) -> None:
+        """After ``Handle.wait()``: a timeout of THIS collective is only known once its kernel has
+        finished, so it surfaces at the next collective (``_next``) or, under ``XDOT_CHECK=1``,
+        here after synchronising on the kernel; earlier timeouts raise here either way."""
+        if FLAGS.check:
+            ev.synchronize()
+        self.check()
+
     def _next(self):
         self.check()
         self.epoch += 1
@@ -159,7 +178,7 @@ class IpcComm(Communicator):
         for t in tensors:  # the caching allocator must not recycle them while the kernel runs
             t.record_stream(cs)
         if async_op:
-            return Handle(work=_EventWork(ev), out=out, post=self.check)
+            return Handle(work=_EventWork(ev, self.device), out=out, post=lambda: self._post(ev))
         cur.wait_event(ev)
         return None
 
