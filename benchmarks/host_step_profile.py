@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--inline-backward", action="store_true",
+                    help="run backward on the calling thread (torch.autograd.set_multithreading_enabled(False)) "
+                         "so cProfile sees the Python backward functions too")
     a = ap.parse_args()
     import torch
 
@@ -28,6 +31,13 @@ def main():
     comm = EmulatedComm(a.world)
     dev = torch.device("cuda", 0)
     bench.time_step(args, comm, dev, torch.bfloat16, 5, 5)  # warm everything (kernels, caches, allocator)
+    ms0, host0, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)
+    print(f"world {a.world}: {ms0:.3f} ms/step, host enqueue {host0:.3f} ms/step (unprofiled, engine thread)")
+    if a.inline_backward:
+        torch.autograd.set_multithreading_enabled(False)
+        bench.time_step(args, comm, dev, torch.bfloat16, 5, 5)
+        ms0, host0, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)
+        print(f"world {a.world}: {ms0:.3f} ms/step, host enqueue {host0:.3f} ms/step (unprofiled, inline backward)")
     pr = cProfile.Profile()
     pr.enable()
     ms, host_ms, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)

@@ -64,14 +64,18 @@ int64_t avail_elems(const at::Tensor& t) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// XDOT_GEMM_LIB: 0 (default) = every product on the xdot kernels (gemm3 matches or beats the
-// library GEMM on the plain large products: profiles/r3_gemm3.md); 1 = plain GEMMs (one uniform
-// batch level, K segments contiguous, output dtype = input dtype) that fill >= 2 rounds of
-// 256x256 tiles go to the library GEMM (at::baddbmm -> hipBLASLt) on in-place strided views
+// XDOT_GEMM_LIB: which plain large products may take the library GEMM (at::baddbmm ->
+// hipBLASLt) on in-place strided views.  fp32 (default) = exact-fp32 products only: the
+// library's fp32 GEMM runs at ~140 TF/s on the big square products vs 115 TF/s for the 128x128
+// exact kernel (profiles/r3_gemm3.md), and plain GEMMs are what the library is for; every
+// 16-bit product stays on the xdot kernels (gemm3 matches or beats the library there).
+// 0 = never (every product on the xdot kernels); 1 = 16-bit products too (round-2 route).
 int gemm_lib() {
   static const int v = [] {
     const char* e = std::getenv("XDOT_GEMM_LIB");
-    return (e && e[0] == '1') ? 1 : 0;
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == '1') return 2;
+    return 1;  // fp32 only
   }();
   return v;
 }
@@ -272,7 +276,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     }
   }
   if (mode == 6) mode = 0;
-  if (mode == 0 && gemm_lib() &&
+  if (mode == 0 && (gemm_lib() == 2 || (gemm_lib() == 1 && A.scalar_type() == at::kFloat)) &&
       gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
                    b_mc, alpha, beta))
     return;
@@ -317,6 +321,52 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     if (rc2 == 0) {
       check_launch(hipGetLastError(), "gemm2");
       return;
+    }
+  }
+  // K slabs for the 128x128 kernel (the exact-fp32 path): a product with few output tiles and a
+  // long K (the K = T weight-side products of the autograd ops: e.g. 1562 x 768 x 12496 = 78
+  // tiles) would leave most CUs idle.  Slab s of every (batch, segment) is one outer batch entry
+  // writing an fp32 partial; one ordered sum (gemm2_reduce) applies alpha / beta / the cast.
+  if (mode == 0 && nb1 == 1 && K >= 1024) {
+    const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128) * nb2;
+    if (tiles < 384) {
+      int64_t S = std::min<int64_t>(std::min<int64_t>((768 + tiles - 1) / tiles, K / 256), 32);
+      S = std::min<int64_t>(S, (int64_t)(64 << 20) / std::max<int64_t>(1, nb2 * M * N));  // partials <= 256 MB
+      int64_t Ks = ((K + S - 1) / S + 15) / 16 * 16;
+      S = (K + Ks - 1) / Ks;
+      if (S >= 2) {
+        at::Tensor ws = at::empty({S * nb2 * M * N}, A.options().dtype(at::kFloat));
+        xdot::GemmArgs gs = g;
+        gs.C = ws.data_ptr();
+        gs.ldc = N;
+        gs.sC2 = M * N;
+        gs.sC1 = nb2 * M * N;
+        gs.alpha = 1.f;
+        gs.beta = 0.f;
+        gs.sA1 = a_mc ? Ks * lda : Ks;
+        gs.sB1 = b_mc ? Ks * ldb : Ks;
+        gs.K = (int)Ks;
+        const int full = (int)(K / Ks) == S ? (int)S : (int)S - 1;
+        const bool vs = vec && (Ks * (a_mc ? lda : 1)) % eps == 0 && (Ks * (b_mc ? ldb : 1)) % eps == 0;
+        int rc1 = xdot_gemm_launch(&gs, full * (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vs,
+                                   cur_stream(A));
+        if (rc1 == 0 && full < S) {  // the short last slab
+          xdot::GemmArgs gl = gs;
+          const int64_t k0 = (int64_t)full * Ks;
+          gl.A = static_cast<const char*>(A.data_ptr()) + A.element_size() * (a_mc ? k0 * lda : k0);
+          gl.B = static_cast<const char*>(B.data_ptr()) + B.element_size() * (b_mc ? k0 * ldb : k0);
+          gl.C = ws.data_ptr<float>() + (int64_t)full * nb2 * M * N;
+          gl.K = (int)(K - k0);
+          const bool vl = vs && (a_mc ? k0 * lda : k0) % eps == 0 && (b_mc ? k0 * ldb : k0) % eps == 0;
+          rc1 = xdot_gemm_launch(&gl, (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vl, cur_stream(A));
+        }
+        TORCH_CHECK(rc1 == 0, "xdot.gemm: unsupported dtype combination ", A.scalar_type(), " -> fp32 slabs");
+        check_launch(hipGetLastError(), "gemm (K slabs)");
+        TORCH_CHECK(xdot_gemm_reduce_launch(&g, ws.data_ptr<float>(), (int)S, (int)nb2, dt_code(C.scalar_type()),
+                                            cur_stream(A)) == 0, "xdot.gemm: slab reduce dtype");
+        check_launch(hipGetLastError(), "gemm slab reduce");
+        return;
+      }
     }
   }
   const int rc = xdot_gemm_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()),

@@ -192,12 +192,20 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     sel_bits16(s[0], (uint32_t)w, NINF_BITS);
     sel_bits16(s[1], (uint32_t)(w >> 32), NINF_BITS);
   };
+  // four independent v_max3 chains of 8 scores, then their max: dependency depth 6 instead of
+  // one 16-deep chain (this runs between the PV MFMAs and the tile barrier, outside any MFMA gap)
   auto row_max = [&](const f32x16 (&s)[2]) {
-    float mx = NEG_INF;
+    float mc[4];
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[tt][r]);
+    for (int c = 0; c < 4; ++c) {
+      const f32x16& v = s[c >> 1];
+      const int o = (c & 1) * 8;
+      float m = fmaxf(fmaxf(v[o], v[o + 1]), v[o + 2]);
+      m = fmaxf(fmaxf(m, v[o + 3]), v[o + 4]);
+      m = fmaxf(fmaxf(m, v[o + 5]), v[o + 6]);
+      mc[c] = fmaxf(m, v[o + 7]);
+    }
+    const float mx = fmaxf(fmaxf(mc[0], mc[1]), fmaxf(mc[2], mc[3]));
     return PS ? pair_max(mx) + m_seed : pair_max(mx) * c2;
   };
   // s: the tile whose max is mx (exponentiated next; PS: corrected to the new m)

@@ -139,6 +139,9 @@ int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out
 // 256x256 LDS-DMA 16-bit GEMM (csrc/gemm2.hip); splits > 1 needs ws: splits*batches*M*N fp32
 int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);
+// C = alpha * (ordered sum of `splits` fp32 partials ws[s][z][M][N]) + beta * C  (csrc/gemm2.hip)
+int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws, int splits, int batches, int dt_out,
+                            hipStream_t st);
 // 8-phase 16x16x32 16-bit GEMM (csrc/gemm3.hip): M, N >= 256, K % 8 == 0; -3 = not eligible
 int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);

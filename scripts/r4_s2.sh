@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-4 session 2: forward row-max A/B (tree vs chain), host profile with the backward inline,
+# HEAD PMC table of the flash kernels, exact-fp32 BASELINE config 4, headline bench.
+set -o pipefail
+O=gpurun_out/${1:-r4s2}
+mkdir -p $O
+for i in 1 2 3; do
+  timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 >> $O/fwd_tree.log 2>&1 || exit $?
+  XDOT_EXT_PATH=xdot/_C_chainmax.so timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 >> $O/fwd_chain.log 2>&1 || exit $?
+  timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 --R 3125 >> $O/fwd_tree8.log 2>&1 || exit $?
+  XDOT_EXT_PATH=xdot/_C_chainmax.so timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 --R 3125 >> $O/fwd_chain8.log 2>&1 || exit $?
+done
+timeout -k 10 300 python benchmarks/host_step_profile.py --world 8 --steps 40 --inline-backward > $O/host8_inline.log 2>&1 || exit $?
+timeout -k 10 200 python benchmarks/bench_ops.py --mode leftT_fb --T 12500 --emulate 8 --dtype fp32 --iters 5 > $O/c4_leftT_fp32.log 2>&1 || exit $?
+timeout -k 10 200 python benchmarks/bench_ops.py --mode nt --T 25000 --offset 32 --emulate 8 --dtype fp32 --iters 5 > $O/c3_nt_fp32.log 2>&1 || exit $?
+timeout -k 10 200 python benchmarks/bench_ops.py --mode all --T 25000 --offset 32 --emulate 8 --dtype fp32 --iters 5 > $O/c3_all_fp32.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || exit $?
+bash scripts/pmc_head.sh ${1:-r4s2}/pmc || exit $?
+echo s2-ok

@@ -175,3 +175,33 @@ def test_split_fp32_non_finite_inputs(gpu):
     ok = torch.ones(M, dtype=torch.bool)
     ok[3] = False
     assert torch.allclose(C.cpu().double()[ok], ref[ok], rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("a_mc,b_mc", LAYOUTS)
+@pytest.mark.parametrize("K", [4096, 5000])
+def test_exact_fp32_k_slabs(gpu, a_mc, b_mc, K):
+    """Exact fp32 with few output tiles and a long K runs as K slabs of the 128x128 kernel
+    (fp32 partials + one ordered sum; a short last slab when the slab length does not divide
+    K): exact-fp32 accuracy vs fp64, alpha / beta applied once."""
+    from xdot.ops.gemm import strided_gemm
+    from xdot.utils.env import FLAGS
+
+    g = torch.Generator(device="cpu").manual_seed(K)
+    M, N, nb = 300, 200, 2
+    A = torch.randn(nb, *((K, M) if a_mc else (M, K)), generator=g, dtype=torch.float64)
+    B = torch.randn(nb, *((K, N) if b_mc else (N, K)), generator=g, dtype=torch.float64)
+    C0 = torch.randn(nb, M, N, generator=g, dtype=torch.float64)
+    C = C0.float().to(gpu)
+    old = FLAGS.fp32_mode
+    try:
+        FLAGS.fp32_mode = "exact"
+        strided_gemm(A.float().to(gpu), B.float().to(gpu), C, M=M, N=N, K=K, nb2=nb, lda=(M if a_mc else K),
+                     ldb=(N if b_mc else K), ldc=N, sA2=M * K, sB2=N * K, sC2=M * N, a_mc=a_mc, b_mc=b_mc,
+                     alpha=0.5, beta=2.0)
+    finally:
+        FLAGS.fp32_mode = old
+    Af, Bf = A.float().double(), B.float().double()
+    opA = Af.transpose(-1, -2) if a_mc else Af
+    opB = Bf if b_mc else Bf.transpose(-1, -2)
+    ref = 0.5 * torch.matmul(opA, opB) + 2.0 * C0.float().double()
+    assert _rel_fro(C.cpu(), ref) <= 2e-6
