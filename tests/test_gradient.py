@@ -80,6 +80,16 @@ def test_module_unmasked_float32_reference_config():
                                                 dtype=torch.float32, tol=1e-5))
 
 
+@pytest.mark.parametrize("ws", [3, 4])
+@pytest.mark.parametrize("bidir", ["1", "0"])
+def test_ring_bidirectional_gloo(ws, bidir, monkeypatch):
+    """The bidirectional ring (half of every block each way, grouped two-link hops, 16-bit
+    accumulators on the wire for bf16) against the dense module, fp32 and bf16, over gloo."""
+    monkeypatch.setenv("XDOT_RING_BIDIR", bidir)
+    run_gloo(_module_parity, ws, 4, "ring", None, True)
+    run_gloo(_module_parity, ws, 4, "ring", None, True, torch.bfloat16, 0.08)
+
+
 @pytest.mark.parametrize("impl", ["flash", "ring"])
 def test_module_bf16_gloo(impl):
     """bf16 end to end over real gloo collectives (half-precision gathers / reductions / ring hops)."""

@@ -23,8 +23,12 @@ backward  the blocks circulate again.  Per step: the row-side partial ``dk`` (su
           travels WITH the block one hop behind it; after N steps plus one hop every rank holds
           the full gradient of its own block — no reduce-scatter.
 
-Per hop one link carries ``R·2C`` bf16 (block) and ``R·2C`` fp32 (accumulator), so a ring is
-link-bound where the all-gather is mesh-bound: it is selected explicitly
+Bidirectional (``XDOT_RING_BIDIR``, default on, N >= 3): rows ``[0, R/2)`` of every block travel
+one way round the ring and rows ``[R/2, R)`` the other, so each hop drives two xGMI links (to
+rank+1 and rank-1) with half the bytes each, and the backward accumulators travel in the compute
+dtype (bf16: the same per-hop rounding as the fused path's reduce-scatter).  Per hop each of the
+two links carries ``R/2·2C`` 16-bit elements (block) and as many again (accumulator).  A ring is
+still link-bound where the all-gather is mesh-bound: it is selected explicitly
 (``DistributedDotProductAttn(impl="ring")`` / :func:`ring_attention`), never by ``auto``.
 CPU tensors (and dtypes the kernels do not take) run the same schedule with torch math.
 """
@@ -80,34 +84,68 @@ def _ref_block_bwd(do, k, blk, lse, delta, mask, H, scale):
 
 
 class _Ring:
-    """Double-buffered block ring: ``cur`` is consumed while ``nxt`` is being received.  The
-    caller's ``first`` block is only ever sent, never received into (it is a saved tensor)."""
+    """Double-buffered block ring of one direction (``d`` = +1: to rank+1 / from rank-1, -1: the
+    other way): ``cur`` is consumed while ``nxt`` is being received.  The caller's ``first``
+    block is only ever sent, never received into (it is a saved tensor)."""
 
-    def __init__(self, comm, first: Tensor):
-        self.comm, self.n, self.rank = comm, comm.world_size, comm.rank
+    def __init__(self, comm, first: Tensor, d: int = 1):
+        self.comm, self.n, self.rank, self.d = comm, comm.world_size, comm.rank, d
         self.first = first
         self.cur = first
         self.nxt = torch.empty_like(first) if self.n > 1 else None
-        self.h = None
 
     def src(self, s: int) -> int:
-        return (self.rank - s) % self.n
+        """the rank whose block this ring holds at step s"""
+        return (self.rank - self.d * s) % self.n
+
+    def pair(self):
+        return (self.cur, self.nxt, (self.rank + self.d) % self.n, (self.rank - self.d) % self.n)
+
+    def rotate(self):
+        old, self.cur = self.cur, self.nxt
+        self.nxt = torch.empty_like(old) if old is self.first else old
+
+
+class _Rings:
+    """The lanes of one ring schedule, hopped together (one grouped exchange per step).
+
+    With ``N >= 3`` ranks the block is split by rows: rows ``[0, R/2)`` travel one way round the
+    ring and rows ``[R/2, R)`` the other, so every hop drives TWO xGMI links (to rank+1 and to
+    rank-1) with half the bytes each: the hop takes half the time of a one-way ring.  Lane i is
+    ``(d, a, b)``: direction and the block rows it carries."""
+
+    def __init__(self, comm, blk: Tensor, bidir: bool):
+        R = blk.shape[1]
+        n = comm.world_size
+        self.comm = comm
+        if bidir and n >= 3 and R >= 2:
+            h = R // 2
+            self.lanes = [(1, 0, h), (-1, h, R)]
+        else:
+            self.lanes = [(1, 0, R)]
+        self.rings = [_Ring(comm, blk[:, a:b].contiguous() if len(self.lanes) > 1 else blk, d)
+                      for (d, a, b) in self.lanes]
+        self.h = None
 
     def start(self, s: int):
-        if s < self.n - 1:
-            self.h = self.comm.sendrecv(self.cur, self.nxt, (self.rank + 1) % self.n, (self.rank - 1) % self.n,
-                                        async_op=True)
+        if s < self.comm.world_size - 1:
+            self.h = self.comm.sendrecv_multi([r.pair() for r in self.rings], async_op=True)
 
     def advance(self):
         if self.h is not None:
             self.h.wait()
             self.h = None
-            old, self.cur = self.cur, self.nxt
-            self.nxt = torch.empty_like(old) if old is self.first else old
+            for r in self.rings:
+                r.rotate()
 
 
-def _block_mask(mask: Optional[Tensor], src: int, R: int) -> Optional[Tensor]:
-    return None if mask is None else mask[..., src * R:(src + 1) * R]
+def _block_mask(mask: Optional[Tensor], src: int, R: int, a: int = 0, b: Optional[int] = None) -> Optional[Tensor]:
+    b = R if b is None else b
+    return None if mask is None else mask[..., src * R + a:src * R + b]
+
+
+def _bidir() -> bool:
+    return FLAGS.ring_bidir
 
 
 class RingAttention(torch.autograd.Function):
@@ -124,8 +162,9 @@ class RingAttention(torch.autograd.Function):
         use_hip = (_ext.use_hip(k) and k.dtype in FLASH_DTYPES and qv.shape[-1] == 2 * C
                    and C // H in FLASH_HEAD_DIMS)
         qv = qv.contiguous()
-        ring = _Ring(comm, qv)
-        mks: List = []
+        rings = _Rings(comm, qv, _bidir())
+        L = len(rings.lanes)
+        mks: List = []  # per step, per lane
         prescaled = False
         fm = 0
         if use_hip:
@@ -135,28 +174,31 @@ class RingAttention(torch.autograd.Function):
             fm = flash.fp32_code(k.dtype)
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
             kk = flash.prescale(k, scale) if prescaled else k.contiguous()
-            ns = int(ops.flash_splits(B, R, R, H, False))
-            # slot 0: the running (O, LSE) of the blocks seen so far (fp32), slots 1..ns: the
-            # arriving block's split partials, merged into slot 0 after each step — resident
-            # partials stay (1 + ns) slots whatever the ring length
-            opart = torch.empty(1 + ns, B, R, C, dtype=torch.float32, device=k.device)
-            lpart = torch.empty(1 + ns, B, H, R, dtype=torch.float32, device=k.device)
+            ns = int(ops.flash_splits(B, R, max(b - a for _, a, b in rings.lanes), H, False))
+            # slot 0: the running (O, LSE) of the blocks seen so far (fp32), then ns slots per lane
+            # for the arriving pieces' split partials, merged into slot 0 after each step -- resident
+            # partials stay (1 + L ns) slots whatever the ring length
+            opart = torch.empty(1 + L * ns, B, R, C, dtype=torch.float32, device=k.device)
+            lpart = torch.empty(1 + L * ns, B, H, R, dtype=torch.float32, device=k.device)
             lpart[0].fill_(-float("inf"))
             lrun = torch.empty(B, H, R, dtype=torch.float32, device=k.device)
             for s in range(n):
-                ring.start(s)
-                src = ring.src(s)
-                mk = flash.prepare_mask_cached(mask, B, R, R, tag=("ring", src, R),
-                                               view=lambda m, src=src: _block_mask(m, src, R))
-                mks.append(mk)
-                bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
-                g = ring.cur
-                ops.flash_fwd_partial(kk, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                      float(scale), opart, lpart, 1, ns, prescaled, fm)
+                rings.start(s)
+                step = []
+                for li, ((_d, a, b), ring) in enumerate(zip(rings.lanes, rings.rings)):
+                    src = ring.src(s)
+                    mk = flash.prepare_mask_cached(mask, B, R, b - a, tag=("ring", src, a, b, R),
+                                                   view=lambda m, src=src, a=a, b=b: _block_mask(m, src, R, a, b))
+                    step.append(mk)
+                    bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
+                    g = ring.cur
+                    ops.flash_fwd_partial(kk, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
+                                          float(scale), opart, lpart, 1 + li * ns, ns, prescaled, fm)
+                mks.append(step)
                 if s < n - 1:
                     ops.flash_fwd_merge(opart, lpart, lrun, int(H))
                     lpart[0].copy_(lrun)
-                ring.advance()
+                rings.advance()
             o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
             ctx.save_for_backward(kk, qv, o, lse)
         else:
@@ -164,23 +206,26 @@ class RingAttention(torch.autograd.Function):
             acc = torch.zeros(B, H, R, (qv.shape[-1] - C) // H, dtype=cdt, device=k.device)
             lse = torch.full((B, H, R), -float("inf"), dtype=cdt, device=k.device)
             for s in range(n):
-                ring.start(s)
-                m = _block_mask(mask, ring.src(s), R)
-                mks.append(m)
-                ob, lb = _ref_block_fwd(k, ring.cur, m, H, scale)
-                new = torch.logaddexp(lse, lb)
-                live = torch.isfinite(new).unsqueeze(-1)
-                w_old = torch.where(live, torch.exp(lse - new).unsqueeze(-1), torch.zeros_like(acc[..., :1]))
-                w_new = torch.where(torch.isfinite(lb).unsqueeze(-1), torch.exp(lb - new).unsqueeze(-1),
-                                    torch.zeros_like(acc[..., :1]))
-                acc = acc * w_old + torch.nan_to_num(ob, nan=0.0) * w_new
-                lse = new
-                ring.advance()
+                rings.start(s)
+                step = []
+                for (_d, a, b), ring in zip(rings.lanes, rings.rings):
+                    m = _block_mask(mask, ring.src(s), R, a, b)
+                    step.append(m)
+                    ob, lb = _ref_block_fwd(k, ring.cur, m, H, scale)
+                    new = torch.logaddexp(lse, lb)
+                    live = torch.isfinite(new).unsqueeze(-1)
+                    w_old = torch.where(live, torch.exp(lse - new).unsqueeze(-1), torch.zeros_like(acc[..., :1]))
+                    w_new = torch.where(torch.isfinite(lb).unsqueeze(-1), torch.exp(lb - new).unsqueeze(-1),
+                                        torch.zeros_like(acc[..., :1]))
+                    acc = acc * w_old + torch.nan_to_num(ob, nan=0.0) * w_new
+                    lse = new
+                mks.append(step)
+                rings.advance()
             acc = torch.where(torch.isfinite(lse).unsqueeze(-1), acc, torch.full_like(acc, float("nan")))
             o = acc.transpose(1, 2).reshape(B, R, -1).to(k.dtype)
             ctx.save_for_backward(k, qv, o, lse)
         ctx.mks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip, ctx.prescaled = mks, H, scale, comm, use_hip, prescaled
-        ctx.fp32_mode = fm
+        ctx.fp32_mode, ctx.bidir = fm, L > 1
         return o
 
     @staticmethod
@@ -188,14 +233,20 @@ class RingAttention(torch.autograd.Function):
     def backward(ctx, do):
         k, qv, o, lse = ctx.saved_tensors
         comm, H, scale = ctx.comm, ctx.H, ctx.scale
-        n, rank = comm.world_size, comm.rank
+        n = comm.world_size
         B, R, C = k.shape
         do = do.contiguous()
-        ring = _Ring(comm, qv)
-        acc_in = torch.empty(B, R, qv.shape[-1], dtype=torch.float32 if k.dtype != torch.float64 else k.dtype,
-                             device=k.device) if n > 1 else None
+        rings = _Rings(comm, qv, ctx.bidir)
+        lanes = rings.lanes
+        # the [dq | dv] accumulators travel one hop behind their blocks, in the compute dtype (as
+        # the fused path's reduce-scatter; XDOT_GRAD_FP32=1 keeps fp32 on the wire) -- each rank
+        # adds its fp32 contribution to the arriving partial sum before forwarding it
+        wdt = k.dtype if (k.dtype in (torch.bfloat16, torch.float16) and not FLAGS.grad_fp32) else (
+            torch.float32 if k.dtype != torch.float64 else k.dtype)
+        acc_in = [torch.empty(B, b - a, qv.shape[-1], dtype=wdt, device=k.device) for (_d, a, b) in lanes] \
+            if n > 1 else None
         acc_h = None
-        acc = None
+        accs = None
         if ctx.use_hip:
             from ..ops import flash
 
@@ -207,52 +258,63 @@ class RingAttention(torch.autograd.Function):
             two = ov not in ("0", "false", "off", "no") and (ov != "auto" or -(-R // 128) * B * H >= 1024)
             hi = _side_stream(do.device) if two else cur  # XDOT_RING_OVERLAP (utils/env.py)
             delta = flash.bwd_delta(do, o, H)
-            nsr = int(ops.flash_splits(B, R, R, H, True))
-            # slot 0: running fp32 dk, slots 1..nsr: this step's column-split partials
-            dpart = torch.empty(1 + nsr, B, R, C, dtype=torch.float32, device=k.device)
+            nsr = int(ops.flash_splits(B, R, max(b - a for _, a, b in lanes), H, True))
+            L = len(lanes)
+            # slot 0: running fp32 dk, then nsr column-split partial slots per lane
+            dpart = torch.empty(1 + L * nsr, B, R, C, dtype=torch.float32, device=k.device)
             dpart[0].zero_()
         else:
             cdt = lse.dtype
             delta = (_heads(do, H, cdt) * _heads(o, H, cdt)).sum(-1)
             dk = torch.zeros(B, R, C, dtype=cdt, device=k.device)
         for s in range(n):
-            ring.start(s)
-            g = ring.cur
-            mk = ctx.mks[s]
+            rings.start(s)
+            contribs = []
             if ctx.use_hip:
-                # the gathered-side kernel runs on the high-priority side stream, concurrently
-                # with the row-side partial here, when a block is big enough for that to pay
+                # the gathered-side kernels run on the high-priority side stream, concurrently with
+                # the row-side partials here, when a block is big enough for that to pay
                 # (``hi is cur`` otherwise)
                 hi.wait_stream(cur)
                 with torch.cuda.stream(hi):
-                    contrib, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mk, H, scale, delta,
-                                                fp32_out=True, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
-                bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
-                ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                           flags, int(H), float(scale), dpart, 1, nsr, ctx.prescaled,
-                                           ctx.fp32_mode)
+                    for li, ring in enumerate(rings.rings):
+                        g = ring.cur
+                        c_, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[s][li], H, scale, delta,
+                                               fp32_out=True, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
+                        contribs.append(c_)
+                for li, ring in enumerate(rings.rings):
+                    g = ring.cur
+                    mk = ctx.mks[s][li]
+                    bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
+                    ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
+                                               flags, int(H), float(scale), dpart, 1 + li * nsr, nsr, ctx.prescaled,
+                                               ctx.fp32_mode)
                 if s < n - 1:
                     ops.sum_partials_into(dpart, dpart[0])
                 cur.wait_stream(hi)
-                contrib.record_stream(cur)
+                for c_ in contribs:
+                    c_.record_stream(cur)
             else:
-                dkb, contrib = _ref_block_bwd(do, k, g, lse, delta, mk, H, scale)
-                dk += dkb
-                contrib = contrib.to(acc_in.dtype if acc_in is not None else contrib.dtype)
-            # the accumulator of this block arrives from rank-1 one hop behind the block itself
+                for li, ring in enumerate(rings.rings):
+                    dkb, c_ = _ref_block_bwd(do, k, ring.cur, lse, delta, ctx.mks[s][li], H, scale)
+                    dk += dkb
+                    contribs.append(c_)
+            # each accumulator arrives from the previous rank of its lane one hop behind its block
             if acc_h is not None:
                 acc_h.wait()
-                contrib += acc_in
-            acc = contrib
+                for c_, ai in zip(contribs, acc_in):
+                    c_ += ai
+            accs = [c_.to(wdt) for c_ in contribs]
             if n > 1:  # acc_in was consumed above (stream-ordered before the receive overwrites it)
-                acc_h = comm.sendrecv(acc, acc_in, (rank + 1) % n, (rank - 1) % n, async_op=True)
-            ring.advance()
+                acc_h = comm.sendrecv_multi([(a_, ai, (comm.rank + d) % n, (comm.rank - d) % n)
+                                             for a_, ai, (d, _a, _b) in zip(accs, acc_in, lanes)], async_op=True)
+            rings.advance()
         if acc_h is not None:
             acc_h.wait()
-            acc = acc_in
+            accs = acc_in
+        dqv = accs[0] if len(accs) == 1 else torch.cat(accs, dim=1)
         if ctx.use_hip:
             dk = ops.flash_bwd_rows_sum(dpart, int(H), k)
-        return dk.to(k.dtype), acc.to(k.dtype), None, None, None, None
+        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None
 
 
 def ring_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,

@@ -110,6 +110,17 @@ class Communicator:
         same order (one hop of :mod:`xdot.parallel.ring`)."""
         raise NotImplementedError
 
+    def sendrecv_multi(self, pairs, async_op: bool = False):
+        """Several point-to-point exchanges issued together: ``pairs`` = ``[(send, recv, dst,
+        src), ...]``, each as :meth:`sendrecv`; backends that can run them as one group (one
+        RCCL group: both directions of a bidirectional ring hop on two xGMI links at once) do."""
+        hs = [self.sendrecv(s_, r_, d_, src_, async_op=True) for (s_, r_, d_, src_) in pairs]
+        h = Handle(work=hs, out=[p[1] for p in pairs])
+        if async_op:
+            return h
+        h.wait()
+        return None
+
     @property
     def backend(self) -> str:
         return "local"
@@ -293,6 +304,22 @@ class EmulatedComm(LocalComm):
                 recv.copy_(send)
         return self._transfer(recv, send.nbytes, self.p2p_gbps, hop, async_op, (send,))
 
+    def sendrecv_multi(self, pairs, async_op=False):
+        # the exchanges go to different peers (different xGMI links): one transfer as long as
+        # the largest of them
+        def hops():
+            for s_, r_, _d, _s in pairs:
+                if r_.data_ptr() != s_.data_ptr():
+                    r_.copy_(s_)
+        nbytes = max(p[0].nbytes for p in pairs)
+        keep = tuple(p[0] for p in pairs) + tuple(p[1] for p in pairs[1:])
+        h = self._transfer(pairs[0][1], nbytes, self.p2p_gbps, hops, True, keep)
+        h._out = [p[1] for p in pairs]
+        if async_op:
+            return h
+        h.wait()
+        return None
+
     def all_gather_object(self, obj):
         return [obj] * self.world_size
 
@@ -416,6 +443,19 @@ class TorchDistComm(Communicator):
             works = [dist.isend(send, self._global(dst), group=self.group),
                      dist.irecv(recv, self._global(src), group=self.group)]
         h = Handle(list(works), recv)
+        if async_op:
+            return h
+        h.wait()
+        return None
+
+    def sendrecv_multi(self, pairs, async_op=False):
+        if self._backend != "nccl" or any(self._staged(p[0], p[1]) for p in pairs):
+            return super().sendrecv_multi(pairs, async_op)
+        ops = []
+        for s_, r_, d_, src_ in pairs:  # ONE RCCL group: every send / receive progresses together
+            ops.append(dist.P2POp(dist.isend, s_.contiguous(), self._global(d_), self.group))
+            ops.append(dist.P2POp(dist.irecv, r_, self._global(src_), self.group))
+        h = Handle(list(dist.batch_isend_irecv(ops)), [p[1] for p in pairs])
         if async_op:
             return h
         h.wait()

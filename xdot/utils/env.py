@@ -47,6 +47,8 @@ variable                    default   effect
                                       stream as soon as the gathered-side gradient lands
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
+``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
+                                      (two xGMI links per hop), 16-bit accumulators  [collective]
 ``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
 ``XDOT_GEMM_LIB`` (C++)     0         1: plain large products on hipBLASLt instead of the hand-written
                                       MFMA GEMMs (``csrc/bindings.cpp``)
@@ -108,6 +110,7 @@ class _Flags:
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
+        self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
         self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
 
 
@@ -115,7 +118,7 @@ FLAGS = _Flags()
 
 # flags that change the number (or dtype) of the collectives an op issues
 COLLECTIVE_KNOBS = ("check", "chunk_budget_mb", "ops_schedule", "gather_chunks", "local_first", "grad_fp32",
-                    "ipc", "ipc_mb", "ipc_wgs")
+                    "ipc", "ipc_mb", "ipc_wgs", "ring_bidir")
 
 
 def collective_knobs() -> dict:

@@ -230,6 +230,9 @@ class IpcComm(Communicator):
     def sendrecv(self, send, recv, dst, src, async_op=False):
         return self.base.sendrecv(send, recv, dst, src, async_op)
 
+    def sendrecv_multi(self, pairs, async_op=False):
+        return self.base.sendrecv_multi(pairs, async_op)
+
     def close(self) -> None:
         """Unmap the peers' pages and free this rank's (after a device sync and a barrier, so
         no peer is still reading them)."""
