@@ -57,6 +57,46 @@ from ..utils.env import FLAGS
 __all__ = ["DistributedDotProductAttn"]
 
 
+def _adjacent(a: Tensor, b: Tensor) -> bool:
+    return (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.device == b.device
+            and tuple(a.shape[1:]) == tuple(b.shape[1:])
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel())
+
+
+class _RowsView(torch.autograd.Function):
+    """``cat([a, b], 0)`` as a no-copy view of the storage ``a`` and ``b`` share (``b`` stored
+    right after ``a``); the gradient splits back into two row views."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.n = a.shape[0]
+        return a.detach().as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(),
+                                     a.storage_offset())
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:ctx.n], g[ctx.n:]
+
+
+def _stacked_rows(a: Tensor, b: Tensor) -> Tensor:
+    """``cat([a, b], 0)`` for two parameters.  First use (or after ``.to()`` gave them separate
+    storages): both are moved into ONE contiguous buffer (``.data`` rebound: the Parameter
+    objects, their optimizer state and ``state_dict`` keys are unchanged); every later call is a
+    view of it."""
+    if not _adjacent(a, b):
+        if not (isinstance(a, nn.Parameter) and isinstance(b, nn.Parameter) and a.dtype == b.dtype
+                and a.device == b.device and tuple(a.shape[1:]) == tuple(b.shape[1:])):
+            return torch.cat([a, b], 0)
+        with torch.no_grad():
+            packed = torch.empty((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
+            packed[:a.shape[0]].copy_(a)
+            packed[a.shape[0]:].copy_(b)
+            a.data = packed[:a.shape[0]]
+            b.data = packed[a.shape[0]:]
+    return _RowsView.apply(a, b)
+
+
 class DistributedDotProductAttn(nn.Module):
     def __init__(self, key_dim: int, value_dim: Optional[int] = None, query_dim: Optional[int] = None,
                  num_heads: int = 1, add_bias: bool = False, offset: Optional[int] = 32,
@@ -163,12 +203,14 @@ class DistributedDotProductAttn(nn.Module):
 
     def _project_qv(self, queries: Tensor, values: Tensor) -> Tensor:
         """[q | v] packed (B, R, 2C): ONE GEMM when ``queries is values`` (self-attention), so
-        the gathered side travels in one all-gather and its grads in one reduce-scatter."""
+        the gathered side travels in one all-gather and its grads in one reduce-scatter.  The
+        ``queries`` / ``values`` parameters share one storage (re-packed once after a ``.to()``),
+        so the packed weight is a view: no concatenation kernel and no autograd node per step."""
         if queries is values and self.queries.in_features == self.values.in_features:
-            w = self._w(torch.cat([self.queries.weight, self.values.weight], 0))
+            w = self._w(_stacked_rows(self.queries.weight, self.values.weight))
             b = None
             if self.queries.bias is not None:
-                b = self._w(torch.cat([self.queries.bias, self.values.bias], 0))
+                b = self._w(_stacked_rows(self.queries.bias, self.values.bias))
             return linear(queries, w, b)
         return torch.cat([self._proj(self.queries, queries), self._proj(self.values, values)], dim=-1)
 
