@@ -15,15 +15,16 @@ LENGTH = 18
 DIM = 64
 
 
-def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, tol=1e-9):
+def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, tol=1e-9, call="kqk", bias=False):
     import xdot
     from xdot import DistributedDotProductAttn
     from xdot.parallel import broadcast_parameters, allreduce_gradients, gather_sequence
 
     torch.manual_seed(100 + rank)  # different init per rank: broadcast must fix it
-    model = DistributedDotProductAttn(DIM, DIM, DIM, num_heads=heads, offset=offset, impl=impl).to(dtype)
+    model = DistributedDotProductAttn(DIM, DIM, DIM, num_heads=heads, offset=offset, impl=impl,
+                                      add_bias=bias).to(dtype)
     gt_model = DistributedDotProductAttn(DIM, DIM, DIM, num_heads=heads, distributed=False,
-                                         impl="materialized").to(dtype)
+                                         impl="materialized", add_bias=bias).to(dtype)
     broadcast_parameters(model)
     gt_model.load_state_dict(model.state_dict())
 
@@ -40,20 +41,27 @@ def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, t
     sl = slice(rank * LENGTH, (rank + 1) * LENGTH)
     k = k_full[:, sl].clone().requires_grad_(True)
     q = q_full[:, sl].clone().requires_grad_(True)
-    out = model(k, q, k, mask_full[:, sl])
+    # call: which tensors go in as (keys, queries, values); "kqq" / "xxx" (queries is values) take
+    # the single-node fused module path (xdot.models.fused) on the flash impl
+    pick = {"kqk": lambda a, b: (a, b, a), "kqq": lambda a, b: (a, b, b), "xxx": lambda a, b: (a, a, a)}[call]
+    out = model(*pick(k, q), mask_full[:, sl])
     out.sum().backward()
 
     kg = k_full.clone().requires_grad_(True)
     qg = q_full.clone().requires_grad_(True)
-    gt_out = gt_model(kg, qg, kg, mask_full)
+    gt_out = gt_model(*pick(kg, qg), mask_full)
     gt_out.sum().backward()
 
     torch.testing.assert_close(gather_sequence(out.detach(), -2), gt_out.detach(), atol=tol, rtol=tol)
     torch.testing.assert_close(gather_sequence(k.grad, -2), kg.grad, atol=tol, rtol=tol)
-    torch.testing.assert_close(gather_sequence(q.grad, -2), qg.grad, atol=tol, rtol=tol)
+    if call != "xxx":
+        torch.testing.assert_close(gather_sequence(q.grad, -2), qg.grad, atol=tol, rtol=tol)
     allreduce_gradients(model)
     for (n1, p1), (n2, p2) in zip(gt_model.named_parameters(), model.named_parameters()):
         assert n1 == n2
+        if n1 == "queries.bias":  # exactly 0 in exact arithmetic (softmax shift invariance): noise only
+            assert p2.grad.abs().max() <= 1e-6 * max(1.0, p1.grad.abs().max().item()) + 1e3 * tol
+            continue
         torch.testing.assert_close(p2.grad, p1.grad, atol=tol * 10, rtol=tol * 10)
 
 
@@ -78,6 +86,24 @@ def test_module_unmasked_float32_reference_config():
 
     ThreadGroup(2).run(lambda r: _module_parity(r, 2, 4, "materialized", 32, False,
                                                 dtype=torch.float32, tol=1e-5))
+
+
+@pytest.mark.parametrize("ws", [1, 3])
+@pytest.mark.parametrize("call", ["kqq", "xxx"])
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_module_fused_node_threads(ws, call, fused, monkeypatch):
+    """queries is values: the flash path runs as ONE autograd node (XDOT_FUSED_MODULE=1) or one
+    node per op (0); both match the dense module (outputs, input and all 8 parameter grads)."""
+    from xdot.utils.comm import ThreadGroup
+    from xdot.utils.env import FLAGS
+
+    monkeypatch.setattr(FLAGS, "fused_module", fused == "1")
+    ThreadGroup(ws).run(lambda r: _module_parity(r, ws, 4, "flash", None, True, call=call, bias=True))
+
+
+def test_module_fused_node_gloo():
+    run_gloo(_module_parity, 2, 4, "flash", None, True, torch.float64, 1e-9, "xxx", True)
+    run_gloo(_module_parity, 2, 4, "flash", None, True, torch.bfloat16, 0.08, "kqq", True)
 
 
 @pytest.mark.parametrize("ws", [3, 4])

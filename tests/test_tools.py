@@ -141,6 +141,8 @@ def test_bench_ops_records_gloo(tmp_path, mode):
     for k in REF_KEYS:
         assert k in rec, k
     assert rec["world_size"] == 2 and rec["T"] == 256 and rec["D"] == 64 and rec["offset"] == 32
+    # fp32 records say which fp32 family ran (exact by default: the reference's precision)
+    assert rec["dtype"] != "fp32" or rec["fp32_mode"] == "exact"
     assert rec["ms_p50"] > 0 and rec["distributed_time"] > 0
 
 

@@ -178,6 +178,21 @@ class DistributedDotProductAttn(nn.Module):
 
                 attn_mask = flash.prepare_mask_async(attn_mask.to(torch.bool), attn_mask.shape[0],
                                                      attn_mask.shape[1], attn_mask.shape[2])
+            if (FLAGS.fused_module and queries is values and self.queries.in_features == self.values.in_features
+                    and (self.compute_dtype is None or self.keys.weight.dtype == self.compute_dtype)):
+                # the whole module as ONE autograd node (xdot.models.fused): same kernels, streams
+                # and numerics, a fraction of the per-op host work
+                from .fused import AttnBlockFn
+
+                wq, wv = self.queries.weight, self.values.weight
+                bq, bv = self.queries.bias, self.values.bias
+                if isinstance(wq, nn.Parameter) and isinstance(wv, nn.Parameter):
+                    _stacked_rows(wq, wv)  # (re)pack the two parameters into one storage once
+                    if bq is not None:
+                        _stacked_rows(bq, bv)
+                return AttnBlockFn.apply(keys, queries, attn_mask, self.keys.weight, self.keys.bias, wq, bq, wv, bv,
+                                         self.composition.weight, self.composition.bias, self.num_heads, scale, comm,
+                                         self.chunk_plan)
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
             pending = start_gather(qv, comm, chunks=self.chunk_plan)

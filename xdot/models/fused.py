@@ -1,0 +1,91 @@
+"""The whole module on the fused (flash) path as ONE autograd node.
+
+Reference structure (``distributed_dot_product/module.py:41-76``): three input projections,
+``RightTransposeMultiplication`` -> scale / mask / softmax -> ``FullMultiplication``, the
+output projection -- each an autograd node whose backward the engine schedules separately
+(``multiplication/ops.py:29-37, :49-54``).  On the flash path the per-node host work (Python
+``Function.apply`` / ``backward`` dispatch, argument flattening, saved-tensor bookkeeping) is a
+large share of the per-rank step's host time at N=8 (``profiles/r3_rank_host.md``), where the
+GPU step is only ~1.4 ms.  :class:`AttnBlockFn` runs
+
+    forward   [q|v] = x_qv Wqvᵀ (+b)  ->  all-gather issued  ->  k = x_k Wkᵀ (+b)
+              ->  seq-parallel flash attention  ->  out = o Wcᵀ (+b)
+    backward  do = dout Wc, dWc  ->  attention backward (both kernels, reduce-scatter)
+              ->  dk: dx_k, dWk  ->  d[q|v]: dx_qv, dW[q|v] (on the priority stream)
+
+with the same kernels, streams and numerics as the per-op graph (``XDOT_FUSED_MODULE=0``
+restores it), and hands back the eight parameter gradients and the input gradients in one go.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from ..ops.linear import linear_backward
+from ..parallel.attention import SeqParallelAttention, start_gather
+
+__all__ = ["AttnBlockFn"]
+
+
+class _Ctx:
+    """Stand-in ``ctx`` for calling :class:`SeqParallelAttention`'s forward / backward inline."""
+
+    def save_for_backward(self, *ts):
+        self._saved = ts
+
+    @property
+    def saved_tensors(self):
+        return self._saved
+
+
+def _rows(a, b):
+    """``cat([a, b], 0)``: a view when ``b`` is stored right after ``a`` (the module keeps the
+    ``queries`` / ``values`` parameters in one storage), else a copy."""
+    from .attention import _adjacent
+
+    if _adjacent(a, b):
+        return a.detach().as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(), a.storage_offset())
+    return torch.cat([a, b], 0)
+
+
+class AttnBlockFn(torch.autograd.Function):
+    @staticmethod
+    @_ext.pinned
+    def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan):
+        wqv = _rows(wq, wv)
+        bqv = _rows(bq, bv) if bq is not None else None
+        qv = F.linear(xqv, wqv, bqv)
+        pending = start_gather(qv, comm, chunks=chunk_plan)  # in flight under the row-side GEMM
+        k = F.linear(xk, wk, bk)
+        actx = _Ctx()
+        o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending)
+        out = F.linear(o, wc, bc)
+        ctx.actx = actx
+        ctx.nq = wq.shape[0]
+        ctx.has_b = (bk is not None, bq is not None, bc is not None)
+        ctx.save_for_backward(xk, xqv, wk, wqv, wc, o)
+        return out
+
+    @staticmethod
+    @_ext.pinned
+    def backward(ctx, dout):
+        xk, xqv, wk, wqv, wc, o = ctx.saved_tensors
+        ng = ctx.needs_input_grad
+        hk, hq, hc = ctx.has_b
+        dout = dout.contiguous()
+        # output projection: d(o) for the attention, its weight / bias gradients
+        do, dwc, dbc = linear_backward(dout, o, wc, True, ng[9], hc and ng[10])
+        dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
+        ctx.actx = None
+        dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], ng[3], hk and ng[4])
+        # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
+        # gradient runs there, under the row-side kernel (linear_backward)
+        dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], ng[5] or ng[7], hq and (ng[6] or ng[8]))
+        n = ctx.nq
+        dwq = dwv = dbq = dbv = None
+        if dwqv is not None:
+            dwq, dwv = dwqv[:n], dwqv[n:]
+        if dbqv is not None:
+            dbq, dbv = dbqv[:n], dbqv[n:]
+        return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None)

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 from .. import _ext
 from .gemm import strided_gemm
 
-__all__ = ["linear", "weight_grad", "LinearFn"]
+__all__ = ["linear", "linear_backward", "weight_grad", "LinearFn"]
 
 _SLOTS = 512       # 2 workgroups per CU x 256 CUs
 _MIN_SLAB = 256    # rows of K per split
@@ -48,7 +48,8 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
     N = x.shape[1]
     out_dtype = out_dtype or dy.dtype
     if not (_ext.use_hip(dy, x) and dy.dtype == x.dtype and dy.dtype in (torch.bfloat16, torch.float16)):
-        return (dy.float().t() @ x.float()).to(out_dtype)
+        ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else torch.promote_types(dy.dtype, x.dtype)
+        return (dy.to(ct).t() @ x.to(ct)).to(out_dtype)
     dy = dy.contiguous()
     x = x.contiguous()
     # 256x256 kernel.  K slabs of the 128x128 kernel are faster in isolation at short K (K = 3125:
@@ -75,6 +76,35 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
     return part.sum(0).to(out_dtype)
 
 
+def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, need_dx: bool, need_dw: bool,
+                    need_db: bool):
+    """Gradients of ``F.linear(x, weight, bias)``: (dx, dw, db), each None when not needed.  dw is
+    the split-K MFMA weight gradient (fp32 accumulation)."""
+    dx = dw = db = None
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if need_dx:
+        dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+    side = getattr(dy, "_xdot_ready_on", None)  # dy is complete on this stream (see below)
+    cur = torch.cuda.current_stream(dy.device) if side is not None else None
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        if need_dw:
+            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
+        if need_db:
+            ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else dy.dtype
+            db = dy2.sum(0, dtype=ct).to(dy.dtype)
+    if side is not None:
+        # the fused attention backward produced dy on its priority stream while its row-side
+        # kernel still runs on `cur`: the weight / bias gradients run there too, overlapping
+        # that kernel, and `cur` is ordered after them before they are handed on
+        x.record_stream(side)
+        dy.record_stream(side)
+        for t in (dw, db):
+            if t is not None:
+                t.record_stream(cur)
+        cur.wait_stream(side)
+    return dx, dw, db
+
+
 class LinearFn(torch.autograd.Function):
     @staticmethod
     @_ext.pinned
@@ -87,28 +117,8 @@ class LinearFn(torch.autograd.Function):
     @_ext.pinned
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        dx = dw = db = None
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        if ctx.needs_input_grad[0]:
-            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
-        side = getattr(dy, "_xdot_ready_on", None)  # dy is complete on this stream (see below)
-        cur = torch.cuda.current_stream(dy.device) if side is not None else None
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            if ctx.needs_input_grad[1]:
-                dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
-            if ctx.has_bias and ctx.needs_input_grad[2]:
-                db = dy2.float().sum(0).to(dy.dtype)
-        if side is not None:
-            # the fused attention backward produced dy on its priority stream while its row-side
-            # kernel still runs on `cur`: the weight / bias gradients run there too, overlapping
-            # that kernel, and `cur` is ordered after them before they are handed on
-            x.record_stream(side)
-            dy.record_stream(side)
-            for t in (dw, db):
-                if t is not None:
-                    t.record_stream(cur)
-            cur.wait_stream(side)
-        return dx, dw, db
+        return linear_backward(dy, x, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               ctx.has_bias and ctx.needs_input_grad[2])
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -41,6 +41,9 @@ variable                    default   effect
                                       relative vs fp64: the reference's precision) or ``split``
                                       (opt-in, like TF32: hi/lo bf16 halves, 3 bf16 products:
                                       <= 9e-6 flash, <= 2e-5 GEMM; profiles/r3_fp32_split.md)
+``XDOT_FUSED_MODULE``       1         the module's flash path as ONE autograd node (projections +
+                                      attention + output projection, xdot/models/fused.py; 0: one
+                                      node per op)
 ``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
                                       1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
 ``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
@@ -108,6 +111,7 @@ class _Flags:
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.fp32_mode = _str("XDOT_FP32_MODE", "exact")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
+        self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
