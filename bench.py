@@ -263,7 +263,7 @@ def _launch_cmd(argv, gpus: int):
 
 def _check_gpu_count(a) -> None:
     # torch.cuda.device_count() does not initialise HIP on this image: safe before a launch
-    if a.device == "cuda":
+    if a.device == "cuda" and a.backend != "gloo":  # gloo rehearsals may share one GPU
         have = torch.cuda.device_count()
         if have and a.gpus > have:
             print(f"bench.py: --gpus {a.gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)

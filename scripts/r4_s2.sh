@@ -10,6 +10,7 @@ for i in 1 2 3; do
   timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 --R 3125 >> $O/fwd_tree8.log 2>&1 || exit $?
   XDOT_EXT_PATH=xdot/_C_chainmax.so timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 --R 3125 >> $O/fwd_chain8.log 2>&1 || exit $?
 done
+bash scripts/pmc_head.sh ${1:-r4s2}/pmc || exit $?
 timeout -k 10 300 python benchmarks/host_step_profile.py --world 8 --steps 40 --inline-backward > $O/host8_inline.log 2>&1 || exit $?
 XDOT_FUSED_MODULE=0 timeout -k 10 300 python benchmarks/host_step_profile.py --world 8 --steps 40 --inline-backward > $O/host8_inline_nofuse.log 2>&1 || exit $?
 for i in 1 2; do
@@ -24,5 +25,5 @@ timeout -k 10 200 python benchmarks/bench_ops.py --mode all --T 25000 --offset 3
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || exit $?
 timeout -k 10 300 python benchmarks/bench_rank.py --world 8 --steps 10 --warmup 3 --impl ring --link-gbps 300 --p2p-gbps 64 --fp32-steps 0 > $O/ring8.log 2>&1 || exit $?
 XDOT_RING_BIDIR=0 timeout -k 10 300 python benchmarks/bench_rank.py --world 8 --steps 10 --warmup 3 --impl ring --link-gbps 300 --p2p-gbps 64 --fp32-steps 0 > $O/ring8_uni.log 2>&1 || exit $?
-bash scripts/pmc_head.sh ${1:-r4s2}/pmc || exit $?
+bash scripts/gpu_multirank.sh ${1:-r4s2}/mr || exit $?
 echo s2-ok

@@ -10,8 +10,11 @@ GPU step is only ~1.4 ms.  :class:`AttnBlockFn` runs
 
     forward   [q|v] = x_qv Wqvᵀ (+b)  ->  all-gather issued  ->  k = x_k Wkᵀ (+b)
               ->  seq-parallel flash attention  ->  out = o Wcᵀ (+b)
-    backward  do = dout Wc, dWc  ->  attention backward (both kernels, reduce-scatter)
-              ->  dk: dx_k, dWk  ->  d[q|v]: dx_qv, dW[q|v] (on the priority stream)
+    backward  do = dout Wc  ->  attention backward (both kernels, reduce-scatter)
+              ->  dx_k  ->  dx_qv
+              beside it: dWc / dbc on a second stream, under the attention backward; dWk / dbk
+              there too, under the input-gradient GEMMs; dW[q|v] on the attention backward's
+              priority stream as soon as the reduce-scatter lands (under the row-side kernel)
 
 with the same kernels, streams and numerics as the per-op graph (``XDOT_FUSED_MODULE=0``
 restores it), and hands back the eight parameter gradients and the input gradients in one go.
@@ -23,6 +26,7 @@ import torch.nn.functional as F
 
 from .. import _ext
 from ..ops.linear import linear_backward
+from ..utils.env import FLAGS
 from ..parallel.attention import SeqParallelAttention, start_gather
 
 __all__ = ["AttnBlockFn"]
@@ -47,6 +51,22 @@ def _rows(a, b):
     if _adjacent(a, b):
         return a.detach().as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride(), a.storage_offset())
     return torch.cat([a, b], 0)
+
+
+def _wgrad_stream(t):
+    """Second compute stream for the weight gradients that only the optimizer needs (None on
+    the CPU, under HIP-graph capture or with ``XDOT_WGRAD_SIDE=0``)."""
+    if not (t.is_cuda and FLAGS.wgrad_side and _ext.use_hip(t)) or torch.cuda.is_current_stream_capturing():
+        return None
+    from ..parallel.attention import _side_stream
+
+    return _side_stream(t.device, 0)
+
+
+def _ready_on(t, side):
+    """``side`` ordered after the current stream's work so far (``t`` is complete there)."""
+    side.wait_stream(torch.cuda.current_stream(t.device))
+    return side
 
 
 class AttnBlockFn(torch.autograd.Function):
@@ -74,11 +94,20 @@ class AttnBlockFn(torch.autograd.Function):
         ng = ctx.needs_input_grad
         hk, hq, hc = ctx.has_b
         dout = dout.contiguous()
-        # output projection: d(o) for the attention, its weight / bias gradients
-        do, dwc, dbc = linear_backward(dout, o, wc, True, ng[9], hc and ng[10])
+        # output projection: d(o) for the attention on this stream; its weight / bias gradients
+        # (only needed by the optimizer) on a second stream, under the attention backward
+        do, _, _ = linear_backward(dout, o, wc, True, False, False)
+        side = _wgrad_stream(dout)
+        if side is not None:
+            dout._xdot_ready_on = _ready_on(dout, side)
+        _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=side is None)
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
         ctx.actx = None
-        dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], ng[3], hk and ng[4])
+        # the row-side weight gradient also runs beside the input-gradient GEMMs that follow
+        if side is not None:
+            dk._xdot_ready_on = _ready_on(dk, side)
+        dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
+        _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=side is None)
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
         dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], ng[5] or ng[7], hq and (ng[6] or ng[8]))
@@ -88,4 +117,10 @@ class AttnBlockFn(torch.autograd.Function):
             dwq, dwv = dwqv[:n], dwqv[n:]
         if dbqv is not None:
             dbq, dbv = dbqv[:n], dbqv[n:]
+        if side is not None:  # the gradients handed on are complete on this stream
+            cur = torch.cuda.current_stream(dout.device)
+            cur.wait_stream(side)
+            for t in (dwc, dbc, dwk, dbk):
+                if t is not None:
+                    t.record_stream(cur)
         return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None)

@@ -77,9 +77,11 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
 
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, need_dx: bool, need_dw: bool,
-                    need_db: bool):
+                    need_db: bool, join: bool = True):
     """Gradients of ``F.linear(x, weight, bias)``: (dx, dw, db), each None when not needed.  dw is
-    the split-K MFMA weight gradient (fp32 accumulation)."""
+    the split-K MFMA weight gradient (fp32 accumulation).  When ``dy._xdot_ready_on`` names a
+    stream, dw / db are computed there; ``join=False`` leaves ordering the current stream after
+    them (and ``record_stream`` of dw / db on it) to the caller."""
     dx = dw = db = None
     dy2 = dy.reshape(-1, dy.shape[-1])
     if need_dx:
@@ -92,16 +94,17 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, nee
         if need_db:
             ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else dy.dtype
             db = dy2.sum(0, dtype=ct).to(dy.dtype)
-    if side is not None:
+    if side is not None and (need_dw or need_db):
         # the fused attention backward produced dy on its priority stream while its row-side
         # kernel still runs on `cur`: the weight / bias gradients run there too, overlapping
         # that kernel, and `cur` is ordered after them before they are handed on
         x.record_stream(side)
         dy.record_stream(side)
-        for t in (dw, db):
-            if t is not None:
-                t.record_stream(cur)
-        cur.wait_stream(side)
+        if join:
+            for t in (dw, db):
+                if t is not None:
+                    t.record_stream(cur)
+            cur.wait_stream(side)
     return dx, dw, db
 
 
