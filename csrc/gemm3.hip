@@ -28,7 +28,8 @@
 //   * K tails: operands stream through buffer_load ... lds; the tail k-tile's dead 16-byte
 //     chunks / k rows get an out-of-range offset, so the DMA writes zeros (K % 8 == 0).
 // Eligibility (checked by xdot_gemm3_launch): 16-bit A/B, beta = 0, M >= 256, N >= 256, 16-byte aligned
-// operand bases, lda/ldb/batch/segment strides multiples of 8 elements, K % 8 == 0.
+// operand bases, lda/ldb/batch/segment strides multiples of 8 elements, K % 8 == 0 unless both
+// operands are mn-contiguous.
 #include "flash_common.h"
 
 namespace xdot {
@@ -610,7 +611,9 @@ extern "C" int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in
                                  int splits, float* ws, hipStream_t st) {
   using namespace xdot;
   GemmArgs g = *a;
-  if (g.M < g3::BM || g.N < g3::BN || (g.K % 8) != 0 || g.beta != 0.f) return -3;
+  // K % 8: a k-contiguous operand's K tail is zero-filled per 16-byte chunk; two mn-contiguous
+  // operands (the weight gradients dYᵀ·X, K = the sequence rows) are tail-filled per k row, any K
+  if (g.M < g3::BM || g.N < g3::BN || ((g.K % 8) != 0 && !(a_mc && b_mc)) || g.beta != 0.f) return -3;
   g.tiles_m = (g.M + g3::BM - 1) / g3::BM;
   g.tiles_n = (g.N + g3::BN - 1) / g3::BN;
   if (batches == 0 || g.K == 0) return -3;

@@ -4,6 +4,7 @@
 set -o pipefail
 O=gpurun_out/${1:-r4s2}
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gemm3_gpu.py tests/test_module_gpu.py tests/test_graphs_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_sel.log 2>&1 || exit $?
 for i in 1 2 3; do
   timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 >> $O/fwd_tree.log 2>&1 || exit $?
   XDOT_EXT_PATH=xdot/_C_chainmax.so timeout -k 10 120 python benchmarks/bench_flash.py --only fwd --iters 20 >> $O/fwd_chain.log 2>&1 || exit $?

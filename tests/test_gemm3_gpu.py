@@ -70,6 +70,27 @@ def test_gemm3_persistent_many_items(gpu, a_mc, b_mc):
     _run(gpu, torch.bfloat16, a_mc, b_mc, 2056, 2056, 200, nseg=2, batches=5, alpha=0.5, out_dt=torch.bfloat16)
 
 
+@pytest.mark.parametrize("K", [3125, 77, 1562, 12503])
+@pytest.mark.parametrize("out_dt", [torch.bfloat16, torch.float32])
+def test_gemm3_odd_k_both_mn_contiguous(gpu, K, out_dt):
+    """K % 8 != 0 with both operands mn-contiguous (the weight gradients dYᵀ·X at T/N = 3125 rows):
+    the K tail is zero-filled per k row, so gemm3 takes these shapes; split-K included."""
+    _run(gpu, torch.bfloat16, True, True, 768, 768, K, batches=1, out_dt=out_dt)
+    _run(gpu, torch.bfloat16, True, True, 1536, 768, K, batches=1, out_dt=out_dt, alpha=0.5)
+
+
+def test_weight_grad_odd_rows(gpu):
+    """xdot.ops.linear.weight_grad at the N=8 rank shape (K = 3125 rows) against fp32 torch."""
+    from xdot.ops.linear import weight_grad
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dy = torch.randn(3125, 1536, generator=g).to(gpu, torch.bfloat16)
+    x = torch.randn(3125, 768, generator=g).to(gpu, torch.bfloat16)
+    w = weight_grad(dy, x)
+    ref = dy.float().t() @ x.float()
+    assert ((w.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
 def test_gemm3_odd_n_kc(gpu):
     """k-contiguous B with N % 8 != 0 (nt's per-rank column count at T/N = 3125): the last
     column tile is shifted by a non-multiple of 8 and stored through unaligned 16-byte stores"""
