@@ -125,7 +125,8 @@ __global__ __launch_bounds__(256) void all_gather_kernel(Args a) {
   }
   // 2. stage range w (and our own output block), publish
   copy_units(a.stage[a.rank], a.src, v0, v1);
-  copy_units(a.out + a.rank * a.shard, a.src, v0, v1);
+  if (a.src != a.out + a.rank * a.shard)  // in place (the producer wrote out[rank]): no own-block copy
+    copy_units(a.out + a.rank * a.shard, a.src, v0, v1);
   release_all();
   if (threadIdx.x < a.n && threadIdx.x != a.rank)
     st_flag(a.sig[threadIdx.x] + a.rank * MAXG + w, (uint32_t)a.epoch);

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from .. import _ext
 from ..ops.linear import linear_backward
 from ..utils.env import FLAGS
-from ..parallel.attention import SeqParallelAttention, start_gather
+from ..parallel.attention import SeqParallelAttention, gather_plan, start_gather
 
 __all__ = ["AttnBlockFn"]
 
@@ -75,8 +75,24 @@ class AttnBlockFn(torch.autograd.Function):
     def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan):
         wqv = _rows(wq, wv)
         bqv = _rows(bq, bv) if bq is not None else None
-        qv = F.linear(xqv, wqv, bqv)
-        pending = start_gather(qv, comm, chunks=chunk_plan)  # in flight under the row-side GEMM
+        n = comm.world_size
+        B, R = xqv.shape[0], xqv.shape[1]
+        gbuf = None
+        if n > 1 and comm.inplace_gather and xqv.is_cuda and \
+                len(gather_plan((B, R), xqv, comm, chunk_plan)) == 1:
+            # the projection writes this rank's block of the gather output directly: the
+            # all-gather runs in place (no copy of the own block; RCCL: sendbuff = recvbuff +
+            # rank block, the xGMI pull kernel skips its own-block copy)
+            gbuf = torch.empty((n, B, R, wqv.shape[0]), dtype=xqv.dtype, device=xqv.device)
+            qv = gbuf[comm.rank]
+            x2 = xqv.reshape(-1, xqv.shape[-1])
+            if bqv is None:
+                torch.mm(x2, wqv.t(), out=qv.view(-1, qv.shape[-1]))
+            else:
+                torch.addmm(bqv, x2, wqv.t(), out=qv.view(-1, qv.shape[-1]))
+        else:
+            qv = F.linear(xqv, wqv, bqv)
+        pending = start_gather(qv, comm, chunks=chunk_plan, out=gbuf)  # in flight under the row-side GEMM
         k = F.linear(xk, wk, bk)
         actx = _Ctx()
         o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending)

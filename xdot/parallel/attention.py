@@ -66,13 +66,15 @@ def _hip_ok(k: Tensor, qv: Tensor, H: int) -> bool:
 # ----------------------------------------------------------------------------------------
 # gather helpers
 # ----------------------------------------------------------------------------------------
-def _gather_rows(comm, x: Tensor, async_op: bool = True):
-    """(B, R, C) -> (N, B, R, C) rank-major (row t = j*R + i of batch b at [j, b, i])."""
+def _gather_rows(comm, x: Tensor, async_op: bool = True, out: Optional[Tensor] = None):
+    """(B, R, C) -> (N, B, R, C) rank-major (row t = j*R + i of batch b at [j, b, i]).  ``out``:
+    the (N, B, R, C) output, whose block ``rank`` may already hold ``x`` (in-place gather)."""
     n = comm.world_size
     x = x.contiguous()
     if n == 1:
         return _comm.Handle(out=x.unsqueeze(0)) if async_op else x.unsqueeze(0)
-    out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    if out is None:
+        out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
     h = comm.all_gather_into(out, x, async_op=async_op)
     return h if async_op else out
 
@@ -109,7 +111,7 @@ class _PendingGather:
     permutation of the rank-major order that attention does not see (the mask columns are
     permuted to match, :func:`_perm_cols`), and the backward runs ONE kernel pair over it."""
 
-    def __init__(self, comm, x: Tensor, chunks: List[Tuple[int, int]]):
+    def __init__(self, comm, x: Tensor, chunks: List[Tuple[int, int]], out: Optional[Tensor] = None):
         self.chunks = chunks
         self.n = n = comm.world_size
         x = x.contiguous()
@@ -121,7 +123,7 @@ class _PendingGather:
         for r0, rc in chunks:
             xc = x[:, r0:r0 + rc]
             if self.flat is None:
-                self.handles.append(_gather_rows(comm, xc))
+                self.handles.append(_gather_rows(comm, xc, out=out))
                 continue
             out = self.flat[off:off + n * xc.numel()].view((n,) + tuple(xc.shape))
             off += out.numel()
@@ -527,14 +529,24 @@ class SeqParallelAttention(torch.autograd.Function):
         return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None
 
 
+def gather_plan(qv_shape, qv: Tensor, comm: _comm.Communicator, chunks: Optional[int] = None):
+    """Row chunks of the gathered side's pipeline for a (B, R, C) ``qv`` of this rank."""
+    hip = _ext.use_hip(qv) and qv.dtype in FLASH_DTYPES
+    return _row_chunks(comm.world_size, qv_shape[1], hip, chunks)
+
+
 def start_gather(qv: Tensor, comm: Optional[_comm.Communicator] = None,
-                 chunks: Optional[int] = None) -> "_PendingGather":
+                 chunks: Optional[int] = None, out: Optional[Tensor] = None) -> "_PendingGather":
     """Issue the all-gather(s) of the packed gathered side early (e.g. before the row-side
     projection GEMM) and hand the result to :func:`seq_parallel_attention_packed`.
-    ``chunks``: row chunks of the pipeline (default ``XDOT_GATHER_CHUNKS``)."""
+    ``chunks``: row chunks of the pipeline (default ``XDOT_GATHER_CHUNKS``).  ``out``: the
+    (N, B, R, C) gather output whose block ``rank`` IS ``qv`` (the projection wrote it in place;
+    one-chunk plans only)."""
     comm = comm or _comm.get_comm()
-    hip = _ext.use_hip(qv) and qv.dtype in FLASH_DTYPES
-    return _PendingGather(comm, qv.detach(), _row_chunks(comm.world_size, qv.shape[1], hip, chunks))
+    plan = gather_plan(qv.shape, qv, comm, chunks)
+    if out is not None and len(plan) != 1:
+        raise ValueError("start_gather: an in-place output needs a one-chunk plan")
+    return _PendingGather(comm, qv.detach(), plan, out=out)
 
 
 def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor], num_heads: int, scale: float,

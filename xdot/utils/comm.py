@@ -69,6 +69,9 @@ class Communicator:
 
     world_size: int = 1
     rank: int = 0
+    # all_gather_into(out, out[rank]) (the input already in place in the output) is supported
+    # without a staging copy of the own block
+    inplace_gather: bool = False
 
     # -- collectives ------------------------------------------------------------------
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -269,11 +272,22 @@ class EmulatedComm(LocalComm):
         h.wait()
         return None
 
+    inplace_gather = True
+
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
-        n = self.world_size
-        return self._transfer(out, out.nbytes * (n - 1) // n, self.link_gbps,
-                              lambda: out.view(n, -1).copy_(inp.reshape(1, -1).expand(n, -1)), async_op, (inp,))
+        n, r = self.world_size, self.rank
+
+        def fill():
+            ov, src = out.view(n, -1), inp.reshape(1, -1)
+            if inp.data_ptr() == ov[r].data_ptr():  # in place: replicate into the other blocks only
+                if r > 0:
+                    ov[:r].copy_(src.expand(r, -1))
+                if r < n - 1:
+                    ov[r + 1:].copy_(src.expand(n - r - 1, -1))
+            else:
+                ov.copy_(src.expand(n, -1))
+        return self._transfer(out, out.nbytes * (n - 1) // n, self.link_gbps, fill, async_op, (inp,))
 
     def all_gather_chunks(self, raw, inp, sizes, async_op=False):
         n = self.world_size
@@ -346,8 +360,14 @@ class TorchDistComm(Communicator):
         host (used to emulate several ranks on one GPU in tests; never on the RCCL path)."""
         return self._backend == "gloo" and any(t.is_cuda for t in ts)
 
+    @property
+    def inplace_gather(self) -> bool:
+        return self._backend == "nccl"  # RCCL all-gather in place: sendbuff = recvbuff + rank block
+
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
+        if self._backend != "nccl" and inp.data_ptr() == out.view(self.world_size, -1)[self.rank].data_ptr():
+            inp = inp.clone()  # gloo: no aliasing between the input and the output
         if self._staged(out, inp):
             o = torch.empty(out.shape, dtype=out.dtype)
             self.all_gather_into(o, inp.detach().cpu())

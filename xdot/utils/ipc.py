@@ -126,6 +126,8 @@ class IpcComm(Communicator):
                 self.sig_ptrs.append(g)
         base.barrier()  # every rank mapped every page before the first pull
 
+    inplace_gather = True  # the pull kernel skips the own-block copy when inp is out[rank]
+
     @property
     def backend(self) -> str:
         return f"ipc+{self.base.backend}"
