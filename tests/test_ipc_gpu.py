@@ -46,6 +46,16 @@ def _collectives_case(rank, ws):
             exp = torch.stack([_data(r, shape, dtype, salt) for r in range(ws)])
             torch.cuda.synchronize()
             assert torch.equal(out.cpu(), exp), (rep, dtype, shape)
+        # in place: the input is this rank's block of the output (the fused module's [q|v]
+        # projection writes it there); the kernel skips its own-block copy
+        salt += 1
+        shape = (1000, 768)
+        out = torch.full((ws,) + shape, float("nan"), dtype=torch.bfloat16, device=dev)
+        out[rank].copy_(_data(rank, shape, torch.bfloat16, salt).to(dev))
+        comm.all_gather_into(out, out[rank])
+        exp = torch.stack([_data(r, shape, torch.bfloat16, salt) for r in range(ws)])
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), exp), (rep, "in place")
         # misaligned input and output views (offset by one element)
         salt += 1
         n = 4096
