@@ -29,12 +29,16 @@ def main():
     ap.add_argument("--link-gbps", type=float, default=None,
                     help="emulated collective bus bandwidth per rank (GB/s); default: no transfer time")
     ap.add_argument("--p2p-gbps", type=float, default=None, help="emulated ring-hop link rate (GB/s)")
+    ap.add_argument("--rank", type=int, default=0,
+                    help="which rank to emulate (the segmented forward launches one partial per peer range: "
+                         "a middle rank has two ranges per gather chunk, rank 0 one)")
     a, rest = ap.parse_known_args()
     import bench
     from xdot.utils.comm import EmulatedComm
 
     for n in a.world:
-        bench.main(["--gpus", str(n)] + rest, comm=EmulatedComm(n, link_gbps=a.link_gbps, p2p_gbps=a.p2p_gbps))
+        bench.main(["--gpus", str(n)] + rest, comm=EmulatedComm(n, rank=min(a.rank, n - 1), link_gbps=a.link_gbps,
+                                                                  p2p_gbps=a.p2p_gbps))
 
 
 if __name__ == "__main__":
