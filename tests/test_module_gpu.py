@@ -84,6 +84,12 @@ def test_module_multi_rank(gpu, impl, ws):
     run_gloo(_module_case, ws, impl, True, timeout=400)
 
 
+def test_module_multi_rank_unmasked_middle_ranks(gpu):
+    """4 ranks, no mask: the middle ranks' gathered chunks run as ONE partial each with their own
+    columns masked out by a synthetic packed mask (rank 0 / 3: one peer range, no mask)."""
+    run_gloo(_module_case, 4, "flash", False, timeout=400)
+
+
 @pytest.mark.parametrize("impl", ["flash", "ring"])
 def test_module_multi_rank_fp32(gpu, impl):
     """fp32 on the fused paths (split-bf16 flash kernels) with 2 ranks, against an fp64 dense

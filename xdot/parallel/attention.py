@@ -279,7 +279,12 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
         from ..ops import flash
 
         ops = _ext.ops()
-        widths = ([R] if local_first else []) + [(j1 - j0) * chunks[c][1] for c, j0, j1 in plan]
+        if local_first and 0 < rank < n - 1:
+            # a middle rank's peers sit on both sides of its own block in every chunk: ONE partial
+            # over the whole chunk with the own columns masked out (their tiles are skipped whole,
+            # two boundary tiles per row block take the masked path) instead of two launches
+            plan = [(c, 0, -1) for c in range(len(chunks))]
+        widths = ([R] if local_first else []) + [(n if j1 == -1 else j1 - j0) * chunks[c][1] for c, j0, j1 in plan]
         ns = [int(ops.flash_splits(B, R, w, H, False)) for w in widths]
         opart = torch.empty(sum(ns), B, R, C, dtype=torch.float32, device=k.device)
         lpart = torch.empty(sum(ns), B, H, R, dtype=torch.float32, device=k.device)
@@ -301,6 +306,10 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
             g = flash.gathered_to_btc(pending.wait(c))          # (B, N*rc, 2C)
             bufs.append(g)
             for _, j0, j1 in (p for p in plan if p[0] == c):
+                if j1 == -1:  # merged: every rank of the chunk, the own columns masked out
+                    mk = _own_excluded_mask(mask, B, R, n, rank, r0, rc, k.device)
+                    run(g[..., :C], g[..., C:], mk)
+                    continue
                 mk = flash.prepare_mask_cached(mask, B, R, (j1 - j0) * rc, tag=("seg", r0, rc, n, j0, j1),
                                                view=_mask_cols(B, R, n, j0, j1, r0, rc))
                 seg = g[:, j0 * rc:j1 * rc]
@@ -321,6 +330,34 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
             parts.append(_ref_fwd_partial(k, seg[..., :C], seg[..., C:], m, H, scale))
     o, lse = _ref_combine(parts, k.dtype)
     return o, lse, [torch.cat(gs, dim=2) if len(gs) > 1 else gs[0]]
+
+
+_OWN_EX = {}
+
+
+def _own_excluded_mask(mask, B: int, R: int, n: int, rank: int, r0: int, rc: int, dev):
+    """Packed (B, R, n*rc) mask of one gather chunk with this rank's own columns masked (they
+    ran first, under the all-gather), OR-ed with the user mask's columns of the chunk.  Cached:
+    on the user mask (MASK_CACHE) or, without one, per shape."""
+    from ..ops import flash
+
+    def own_cols(m):
+        m = m.clone()
+        m[..., rank * rc:(rank + 1) * rc] = True
+        return m
+
+    if mask is not None:
+        packed = flash.prepare_mask_cached(mask, B, R, n * rc, tag=("segx", r0, rc, n, rank),
+                                           view=lambda m: own_cols(_mask_cols(B, R, n, 0, n, r0, rc)(m)))
+        if packed is not None:
+            return packed
+    key = (B, R, n, rank, rc, dev)
+    if key not in _OWN_EX:
+        if len(_OWN_EX) >= 8:
+            _OWN_EX.pop(next(iter(_OWN_EX)))
+        _OWN_EX[key] = flash.prepare_mask(own_cols(torch.zeros(B, R, n * rc, dtype=torch.bool, device=dev)),
+                                          B, R, n * rc)
+    return _OWN_EX[key]
 
 
 _SIDE = {}
