@@ -32,7 +32,13 @@ def main():
     ap.add_argument("--rank", type=int, default=0,
                     help="which rank to emulate (the segmented forward launches one partial per peer range: "
                          "a middle rank has two ranges per gather chunk, rank 0 one)")
+    ap.add_argument("--no-seg-merge", action="store_true",
+                    help="(A/B) a middle rank runs one forward partial per peer range instead of one per chunk")
     a, rest = ap.parse_known_args()
+    if a.no_seg_merge:
+        import xdot.parallel.attention as pa
+
+        pa.SEGMENT_MERGE = False
     import bench
     from xdot.utils.comm import EmulatedComm
 

@@ -279,7 +279,7 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
         from ..ops import flash
 
         ops = _ext.ops()
-        if local_first and 0 < rank < n - 1:
+        if local_first and 0 < rank < n - 1 and SEGMENT_MERGE:
             # a middle rank's peers sit on both sides of its own block in every chunk: ONE partial
             # over the whole chunk with the own columns masked out (their tiles are skipped whole,
             # two boundary tiles per row block take the masked path) instead of two launches
@@ -333,6 +333,8 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
 
 
 _OWN_EX = {}
+# False: a middle rank launches one partial per peer range (A/B diagnostics: bench_rank.py --no-seg-merge)
+SEGMENT_MERGE = True
 
 
 def _own_excluded_mask(mask, B: int, R: int, n: int, rank: int, r0: int, rc: int, dev):
