@@ -136,6 +136,9 @@ class DistributedDotProductAttn(nn.Module):
         self.queries = nn.Linear(query_dim, key_dim, bias=add_bias)
         self.values = nn.Linear(value_dim, value_dim, bias=add_bias)
         self.composition = nn.Linear(value_dim, value_dim, bias=add_bias)
+        # weakref to an attached xdot.parallel.GradSync (set by it): the fused node hands it the
+        # parameter gradients as they are computed (early all-reduce)
+        self._xdot_grad_sync = None
 
     # ------------------------------------------------------------------------------------
     def _pick_impl(self, x: Tensor) -> str:
@@ -190,9 +193,10 @@ class DistributedDotProductAttn(nn.Module):
                     _stacked_rows(wq, wv)  # (re)pack the two parameters into one storage once
                     if bq is not None:
                         _stacked_rows(bq, bv)
+                sync = self._xdot_grad_sync() if self._xdot_grad_sync is not None else None
                 return AttnBlockFn.apply(keys, queries, attn_mask, self.keys.weight, self.keys.bias, wq, bq, wv, bv,
                                          self.composition.weight, self.composition.bias, self.num_heads, scale, comm,
-                                         self.chunk_plan)
+                                         self.chunk_plan, sync)
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
             pending = start_gather(qv, comm, chunks=self.chunk_plan)

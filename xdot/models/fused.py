@@ -72,7 +72,7 @@ def _ready_on(t, side):
 class AttnBlockFn(torch.autograd.Function):
     @staticmethod
     @_ext.pinned
-    def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan):
+    def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan, sync=None):
         wqv = _rows(wq, wv)
         bqv = _rows(bq, bv) if bq is not None else None
         n = comm.world_size
@@ -98,6 +98,8 @@ class AttnBlockFn(torch.autograd.Function):
         o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending)
         out = F.linear(o, wc, bc)
         ctx.actx = actx
+        ctx.sync = sync
+        ctx.params = (wk, bk, wq, bq, wv, bv, wc, bc)
         ctx.nq = wq.shape[0]
         ctx.has_b = (bk is not None, bq is not None, bc is not None)
         ctx.save_for_backward(xk, xqv, wk, wqv, wc, o)
@@ -117,6 +119,13 @@ class AttnBlockFn(torch.autograd.Function):
         if side is not None:
             dout._xdot_ready_on = _ready_on(dout, side)
         _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=side is None)
+        wk_, bk_, wq_, bq_, wv_, bv_, wc_, bc_ = ctx.params
+        sync = ctx.sync
+        cur = torch.cuda.current_stream(dout.device) if dout.is_cuda else None
+        if sync is not None:  # hand the output projection's gradients to GradSync now: their
+            # all-reduce runs under the attention backward
+            sync.deliver([(wc_, dwc), (bc_, dbc)], stream=side or cur)
+            dwc = dbc = None
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
         ctx.actx = None
         # the row-side weight gradient also runs beside the input-gradient GEMMs that follow
@@ -126,6 +135,7 @@ class AttnBlockFn(torch.autograd.Function):
         _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=side is None)
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
+        qv_on = getattr(dqv, "_xdot_ready_on", None) or cur
         dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], ng[5] or ng[7], hq and (ng[6] or ng[8]))
         n = ctx.nq
         dwq = dwv = dbq = dbv = None
@@ -133,10 +143,14 @@ class AttnBlockFn(torch.autograd.Function):
             dwq, dwv = dwqv[:n], dwqv[n:]
         if dbqv is not None:
             dbq, dbv = dbqv[:n], dbqv[n:]
+        if sync is not None:
+            sync.deliver([(wq_, dwq), (bq_, dbq), (wv_, dwv), (bv_, dbv)], stream=qv_on)
+            sync.deliver([(wk_, dwk), (bk_, dbk)], stream=side or cur)
+            dwq = dbq = dwv = dbv = dwk = dbk = None
         if side is not None:  # the gradients handed on are complete on this stream
-            cur = torch.cuda.current_stream(dout.device)
             cur.wait_stream(side)
-            for t in (dwc, dbc, dwk, dbk):
+            for t in (dwc, dbc, dwk, dbk) + tuple(p.grad for p in ctx.params if p is not None and sync is not None):
                 if t is not None:
                     t.record_stream(cur)
-        return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None)
+        ctx.params = ctx.sync = None
+        return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None, None)

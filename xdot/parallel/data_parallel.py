@@ -138,9 +138,20 @@ class GradSync:
         self._muted = False
         self._rest_key = None
         self._rest: List[torch.Tensor] = []
+        self._attached = []
+        self._dlv = set()  # ids of parameters whose gradient was delivered this round
         if self.comm.world_size > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            # modules whose backward computes several parameter gradients in one autograd node
+            # (xdot.models.fused.AttnBlockFn) hand each one over as soon as it exists (deliver),
+            # so its all-reduce overlaps the rest of that node's backward
+            import weakref
+
+            for m in module.modules():
+                if hasattr(m, "_xdot_grad_sync"):
+                    m._xdot_grad_sync = weakref.ref(self)
+                    self._attached.append(m)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -151,8 +162,32 @@ class GradSync:
         finally:
             self._muted = prev
 
-    def _on_grad(self, p):
+    @torch.no_grad()
+    def deliver(self, pairs, stream=None) -> None:
+        """Gradients computed early inside a multi-parameter backward node: accumulate each
+        into ``p.grad`` (as autograd's AccumulateGrad would) and count it for its bucket, the
+        bucket's all-reduce ordered after ``stream`` (where the gradients were computed).  The
+        node then returns None for these parameters."""
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            for p, g in pairs:
+                if g is None:
+                    continue
+                if p.grad is None:
+                    p.grad = g.detach()
+                else:
+                    p.grad.add_(g)
+            for p, g in pairs:
+                if g is not None:
+                    self._dlv.add(id(p))
+                    self._on_grad(p, delivered=True)
+
+    def _on_grad(self, p, delivered: bool = False):
         if self._muted:
+            return
+        if not delivered and id(p) in self._dlv:
+            # autograd's AccumulateGrad still runs (with no gradient) for a parameter whose
+            # gradient the node delivered itself, and its post-accumulate hook fires: ignore it
             return
         i = self._index[id(p)]
         if self._launched[i] or id(p) in self._seen[i]:
@@ -235,6 +270,7 @@ class GradSync:
 
     def _reset(self):
         self._handles.clear()
+        self._dlv = set()
         self._seen = [set() for _ in self.buckets]
         self._launched = [False] * len(self.buckets)
 
@@ -242,3 +278,6 @@ class GradSync:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+        for m in self._attached:
+            m._xdot_grad_sync = None
+        self._attached.clear()
