@@ -76,3 +76,36 @@ def test_compute_dtype_policy(impl):
     for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
         assert p.dtype == torch.float32 and p.grad is not None and p.grad.dtype == torch.float32, n
         torch.testing.assert_close(p.grad, q.grad.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_packed_qv_parameters_share_storage():
+    """queries / values weights live in ONE storage after the first forward (the packed [q|v]
+    weight is a view, no per-step cat); state_dict keys, .to() and load_state_dict keep working
+    (a .to() re-packs on the next forward) and the gradients match the unpacked materialised path."""
+    import copy
+
+    from xdot import DistributedDotProductAttn
+    from xdot.models.attention import _adjacent
+
+    torch.manual_seed(0)
+    m = DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash", distributed=False).double()
+    ref = copy.deepcopy(m)
+    ref.impl = "materialized"  # separate q / v projections, no packing
+    x = torch.randn(1, 7, 32, dtype=torch.float64)
+    out = m(x, x, x, None)
+    assert _adjacent(m.queries.weight, m.values.weight) and _adjacent(m.queries.bias, m.values.bias)
+    assert not _adjacent(ref.queries.weight, ref.values.weight)
+    out.square().sum().backward()
+    ref(x, x, x, None).square().sum().backward()
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        if n == "queries.bias":
+            continue  # exactly zero up to rounding (softmax shift invariance)
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-9, atol=1e-11, msg=n)
+    m2 = m.to(torch.float32)
+    x32 = x.float()
+    m2(x32, x32, x32, None)
+    assert _adjacent(m2.queries.weight, m2.values.weight)
+    sd = m2.state_dict()
+    assert {"queries.weight", "values.weight", "queries.bias", "values.bias"} <= set(sd)
+    m2.load_state_dict(sd)
+    assert _adjacent(m2.queries.weight, m2.values.weight)
