@@ -15,7 +15,8 @@ LENGTH = 18
 DIM = 64
 
 
-def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, tol=1e-9, call="kqk", bias=False):
+def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, tol=1e-9, call="kqk", bias=False,
+                   length=LENGTH):
     import xdot
     from xdot import DistributedDotProductAttn
     from xdot.parallel import broadcast_parameters, allreduce_gradients, gather_sequence
@@ -29,7 +30,7 @@ def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, t
     gt_model.load_state_dict(model.state_dict())
 
     g = torch.Generator().manual_seed(7)
-    T = LENGTH * ws
+    T = length * ws
     k_full = torch.rand(1, T, DIM, generator=g, dtype=dtype)
     q_full = torch.rand(1, T, DIM, generator=g, dtype=dtype)
     if masked:
@@ -38,7 +39,7 @@ def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, t
     else:
         mask_full = torch.zeros(1, T, T, dtype=torch.bool)
 
-    sl = slice(rank * LENGTH, (rank + 1) * LENGTH)
+    sl = slice(rank * length, (rank + 1) * length)
     k = k_full[:, sl].clone().requires_grad_(True)
     q = q_full[:, sl].clone().requires_grad_(True)
     # call: which tensors go in as (keys, queries, values); "kqq" / "xxx" (queries is values) take
@@ -104,6 +105,15 @@ def test_module_fused_node_threads(ws, call, fused, monkeypatch):
 def test_module_fused_node_gloo():
     run_gloo(_module_parity, 2, 4, "flash", None, True, torch.float64, 1e-9, "xxx", True)
     run_gloo(_module_parity, 2, 4, "flash", None, True, torch.bfloat16, 0.08, "kqq", True)
+
+
+@pytest.mark.parametrize("ws", [3, 5])
+def test_ring_bidirectional_odd_rows_threads(ws):
+    """Bidirectional ring with an odd row count per rank: the two lanes carry R//2 and R - R//2
+    rows (exchanges of different sizes in one group), masked, with q != v inputs."""
+    from xdot.utils.comm import ThreadGroup
+
+    ThreadGroup(ws).run(lambda r: _module_parity(r, ws, 4, "ring", None, True, length=7))
 
 
 @pytest.mark.parametrize("ws", [3, 4])
