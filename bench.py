@@ -72,10 +72,20 @@ def parse(argv=None):
                     help="also time this many steps of the same step in fp32 (the reference's precision; "
                          "0 = skip); reported as fp32_ms_per_step")
     ap.add_argument("--fp32-warmup", type=int, default=2)
+    ap.add_argument("--trace", action="store_true",
+                    help="print stage / step progress with timestamps to stderr (diagnostics)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (fwd+bwd+grad sync+AdamW) in a HIP graph and replay it "
                          "(xdot.utils.graphs.GraphedStep; single-GPU / emulated communicators)")
     return ap.parse_args(argv)
+
+
+_T0 = time.perf_counter()
+
+
+def _trace(a, msg):
+    if getattr(a, "trace", False):
+        print(f"[bench {time.perf_counter() - _T0:8.2f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def numerics_check(a, comm, dev, dt, impl, T: int = 512, tol: float = 3e-2) -> float:
@@ -188,8 +198,11 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
         step = GraphedStep(body, zero_grad=opt.zero_grad, warmup=max(1, warmup), optimizer=opt)
         step()  # warmup steps + capture + one replay
     else:
-        for _ in range(warmup):
+        for i in range(warmup):
             step()
+            if dev.type == "cuda" and getattr(a, "trace", False):
+                torch.cuda.synchronize()
+            _trace(a, f"{dt} warmup step {i} done")
     impl = model._pick_impl(x)
 
     def sync_all():
@@ -343,8 +356,10 @@ def main(argv=None, comm=None):
     R = T // n
 
     check_err = None
+    _trace(a, "init done")
     if not emulated and not a.no_check:
         check_err = numerics_check(a, comm, dev, dt, a.impl)
+    _trace(a, "numerics check done")
     ms, host_ms, lossv, impl = time_step(a, comm, dev, dt, a.steps, a.warmup, graph=a.graph,
                                          profile_dir=a.profile_dir)
     fp32 = {}
@@ -355,7 +370,9 @@ def main(argv=None, comm=None):
         try:
             for mode in [default_mode] + [m for m in ("split", "exact") if m != default_mode]:
                 FLAGS.fp32_mode = mode
+                _trace(a, f"fp32 {mode} start")
                 fp32[mode] = time_step(a, comm, dev, torch.float32, a.fp32_steps, a.fp32_warmup)
+                _trace(a, f"fp32 {mode} done: {fp32[mode][0]:.2f} ms")
         finally:
             FLAGS.fp32_mode = default_mode
     if rank == 0:
