@@ -109,3 +109,21 @@ def test_packed_qv_parameters_share_storage():
     assert {"queries.weight", "values.weight", "queries.bias", "values.bias"} <= set(sd)
     m2.load_state_dict(sd)
     assert _adjacent(m2.queries.weight, m2.values.weight)
+
+
+def test_library_weight_gradient_stays_on_current_stream():
+    """A weight gradient that falls back to a library GEMM (fp32 / fp64, CPU) ignores the
+    ``_xdot_ready_on`` side-stream hint: two library GEMMs in flight on two streams can deadlock
+    (stream-K kernels spinning on each other's unscheduled workgroups), so only the xdot MFMA
+    weight gradient may run beside other work (``xdot.ops.linear.native_wgrad``)."""
+    from xdot.ops.linear import linear_backward, native_wgrad
+
+    x = torch.randn(6, 5, dtype=torch.float64)
+    w = torch.randn(4, 5, dtype=torch.float64)
+    dy = torch.randn(6, 4, dtype=torch.float64)
+    assert not native_wgrad(dy, x) and not native_wgrad(dy.float(), x.float())
+    dy._xdot_ready_on = object()  # would fail as a stream context if it were used
+    dx, dw, db = linear_backward(dy, x, w, True, True, True)
+    torch.testing.assert_close(dx, dy @ w)
+    torch.testing.assert_close(dw, dy.t() @ x)
+    torch.testing.assert_close(db, dy.sum(0))

@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
-from ..ops.linear import linear_backward
+from ..ops.linear import linear_backward, native_wgrad
 from ..utils.env import FLAGS
 from ..parallel.attention import SeqParallelAttention, gather_plan, start_gather
 
@@ -55,8 +55,9 @@ def _rows(a, b):
 
 def _wgrad_stream(t):
     """Second compute stream for the weight gradients that only the optimizer needs (None on
-    the CPU, under HIP-graph capture or with ``XDOT_WGRAD_SIDE=0``)."""
-    if not (t.is_cuda and FLAGS.wgrad_side and _ext.use_hip(t)) or torch.cuda.is_current_stream_capturing():
+    the CPU, under HIP-graph capture, with ``XDOT_WGRAD_SIDE=0`` and when the weight gradients
+    are library GEMMs: ``xdot.ops.linear.native_wgrad``)."""
+    if not (t.is_cuda and FLAGS.wgrad_side and native_wgrad(t, t)) or torch.cuda.is_current_stream_capturing():
         return None
     from ..parallel.attention import _side_stream
 

@@ -42,12 +42,24 @@ def _splits(M: int, N: int, K: int) -> int:
     return s
 
 
+def native_wgrad(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """True when :func:`weight_grad` runs on the xdot MFMA kernels (16-bit GPU operands), False
+    when it falls back to a library GEMM.
+
+    Only the native path may run on a second stream beside other GEMMs: a library GEMM may pick
+    a stream-K kernel whose workgroups spin on partial-tile flags and assume the grid is
+    co-resident, and two such kernels in flight on two streams can hold every CU slot while
+    waiting for each other's unscheduled producers (the fp32 module step stalled this way with
+    the output-projection dW and dx GEMMs on two streams)."""
+    return _ext.use_hip(dy, x) and dy.dtype == x.dtype and dy.dtype in (torch.bfloat16, torch.float16)
+
+
 def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """``dyᵀ·x`` for 2-D ``dy`` (K, M) and ``x`` (K, N) -> (M, N), fp32 accumulation."""
     K, M = dy.shape
     N = x.shape[1]
     out_dtype = out_dtype or dy.dtype
-    if not (_ext.use_hip(dy, x) and dy.dtype == x.dtype and dy.dtype in (torch.bfloat16, torch.float16)):
+    if not native_wgrad(dy, x):
         ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else torch.promote_types(dy.dtype, x.dtype)
         return (dy.to(ct).t() @ x.to(ct)).to(out_dtype)
     dy = dy.contiguous()
@@ -87,6 +99,8 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, nee
     if need_dx:
         dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
     side = getattr(dy, "_xdot_ready_on", None)  # dy is complete on this stream (see below)
+    if side is not None and need_dw and not native_wgrad(dy, x):
+        side = None  # a library GEMM stays on the current stream (native_wgrad)
     cur = torch.cuda.current_stream(dy.device) if side is not None else None
     with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
         if need_dw:
