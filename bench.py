@@ -365,7 +365,7 @@ def main(argv=None, comm=None):
     fp32 = {}
     if a.fp32_steps > 0 and dt != torch.float32 and dev.type == "cuda":
         # the reference computes in fp32 only (module.py:60-71): time the same step in fp32 too,
-        # under both fp32 kernel families (XDOT_FP32_MODE: split-bf16 default, exact fp32 MFMA)
+        # under both fp32 kernel families (XDOT_FP32_MODE: exact fp32 MFMA default, split-bf16)
         default_mode = FLAGS.fp32_mode
         try:
             for mode in [default_mode] + [m for m in ("split", "exact") if m != default_mode]:
@@ -375,7 +375,7 @@ def main(argv=None, comm=None):
                 _trace(a, f"fp32 {mode} done: {fp32[mode][0]:.2f} ms")
         finally:
             FLAGS.fp32_mode = default_mode
-    if rank == 0:
+    if rank == 0 or emulated:  # an emulated rank is the only process: it reports
         metric = METRIC
         if (T, a.dim, a.heads) != (25000, 768, 8):  # not the headline config: say what was run
             metric = f"ms/fwd+bwd DistributedDotProductAttn T={T} d={a.dim} h={a.heads}"
@@ -410,6 +410,7 @@ def main(argv=None, comm=None):
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "loss": lossv,
             "world_size": n,
+            "rank": rank,
             "transport": transport,
             "rccl_version": rccl,
             "gather_chunks": len(_row_chunks(n, R, impl == "flash")),

@@ -5,14 +5,16 @@
 For each shape (T/N = 3125 rows, D = 768; [q|v] = 1536 outputs) and route, prints
   host_us   wall time to ENQUEUE one call (GPU kept busy first, so the host never waits),
   gpu_us    GPU time per call (events around `calls` calls queued behind busy work).
-Routes: torch F.linear on hipBLASLt (the default), on rocBLAS ("hipblas") and CK
-(`torch.backends.cuda.preferred_blas_library`), and `xdot.gemm.strided_gemm` (path 0 = xdot's
-automatic kernel choice, 1 = 128x128, 2 = 256x256 v2, 3 = gemm3; the library route of the extension when XDOT_GEMM_LIB=1).
+Routes: torch F.linear / matmul on hipBLASLt (the default) and rocBLAS ("hipblas"), the projection
+kernel (`torch.ops.xdot.proj`, csrc/gemm_proj.hip: forward NT and input-gradient NN), and
+`xdot.gemm.strided_gemm` (path 1 = 128x128, 3 = gemm3).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
@@ -52,31 +54,52 @@ def measure(fn, calls: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=200)
+    ap.add_argument("--quick", action="store_true", help="hipBLASLt vs the projection kernel only")
     args = ap.parse_args()
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
     from xdot.ops.gemm import strided_gemm
     dt = torch.bfloat16
     R, D = 3125, 768
-    cases = {  # name: (x rows, in, out)
-        "qv_fwd": (R, D, 2 * D),
-        "k_fwd": (R, D, D),
-        "qv_dgrad": (R, 2 * D, D),
+    ops = xdot_ops()
+    cases = {  # name: (kind, rows, in, out); nt = forward x Wᵀ + b, nn = input gradient dy W
+        "qv_fwd": ("nt", R, D, 2 * D),
+        "k_fwd": ("nt", R, D, D),
+        "qv_dgrad": ("nn", R, 2 * D, D),
+        "k_dgrad": ("nn", R, D, D),
+        "qv_fwd_n1": ("nt", 8 * R, D, 2 * D),
+        "qv_dgrad_n1": ("nn", 8 * R, 2 * D, D),
     }
-    for name, (m, k, n) in cases.items():
+    for name, (kind, m, k, n) in cases.items():
         x = torch.randn(m, k, device="cuda", dtype=dt)
-        w = torch.randn(n, k, device="cuda", dtype=dt) * 0.03
-        b = torch.randn(n, device="cuda", dtype=dt)
-        out = torch.empty(m, n, device="cuda", dtype=dt)
         res = {}
-        for lib in ("hipblaslt", "hipblas", "ck"):
-            torch.backends.cuda.preferred_blas_library(lib)
-            res[f"torch_{lib}"] = measure(lambda: F.linear(x, w, b), args.calls)
-            res[f"torch_{lib}_nobias"] = measure(lambda: F.linear(x, w), args.calls)
-        torch.backends.cuda.preferred_blas_library("hipblaslt")
-        for path in (0, 1, 2, 3):
-            res[f"xdot_path{path}"] = measure(
-                lambda: strided_gemm(x, w, out, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, path=path), args.calls)
+        if kind == "nt":
+            w = torch.randn(n, k, device="cuda", dtype=dt) * 0.03
+            b = torch.randn(n, device="cuda", dtype=dt)
+            out = torch.empty(m, n, device="cuda", dtype=dt)
+            for lib in ("hipblaslt", "hipblas") if not args.quick else ("hipblaslt",):
+                torch.backends.cuda.preferred_blas_library(lib)
+                res[f"torch_{lib}"] = measure(lambda: F.linear(x, w, b), args.calls)
+                res[f"torch_{lib}_nobias"] = measure(lambda: F.linear(x, w), args.calls)
+            torch.backends.cuda.preferred_blas_library("hipblaslt")
+            res["xdot_proj"] = measure(lambda: ops.proj(x, w, b, False, None), args.calls)
+            res["xdot_proj_nobias"] = measure(lambda: ops.proj(x, w, None, False, None), args.calls)
+            for path in (1, 3) if not args.quick else ():
+                res[f"xdot_path{path}"] = measure(
+                    lambda: strided_gemm(x, w, out, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, path=path), args.calls)
+        else:
+            w = torch.randn(k, n, device="cuda", dtype=dt) * 0.03  # Linear(n -> k) weight: dx = dy W
+            res["torch_hipblaslt"] = measure(lambda: x @ w, args.calls)
+            res["xdot_proj"] = measure(lambda: ops.proj(x, w, None, True, None), args.calls)
         for r, (h, g) in res.items():
-            print(json.dumps({"case": name, "route": r, "host_us": round(h, 2), "gpu_us": round(g, 2)}), flush=True)
+            print(json.dumps({"case": name, "M": m, "N": n, "K": k, "route": r, "host_us": round(h, 2),
+                              "gpu_us": round(g, 2)}), flush=True)
+
+
+def xdot_ops():
+    import xdot._ext as ext
+
+    assert ext.load(), "xdot/_C.so missing"
+    return ext.ops()
 
 
 if __name__ == "__main__":

@@ -682,6 +682,65 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
   return out;
 }
 
+// Projection GEMM (csrc/gemm_proj.hip): nn = false: y = x Wᵀ (+ bias), W (N, K); nn = true:
+// dx = dy W, W (K, N) (the input gradient of the same Linear).  x: (..., K) with unit last
+// stride; out (optional): an (M, N) row-major view to write (e.g. this rank's block of the
+// all-gather buffer).  Shapes / layouts the kernel does not take run on the library GEMM.
+at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool nn,
+                const c10::optional<at::Tensor>& out) {
+  Range rr_("xdot.proj");
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && w.dim() == 2 && x.dim() >= 1 && x.scalar_type() == w.scalar_type(),
+              "xdot.proj: device tensors of one dtype, 2-D weight");
+  const int64_t K = x.size(-1);
+  const int64_t N = nn ? w.size(1) : w.size(0);
+  TORCH_CHECK((nn ? w.size(0) : w.size(1)) == K, "xdot.proj: weight ", w.sizes(), " does not match input features ", K);
+  at::Tensor a = x.dim() == 2 ? x : x.reshape({-1, K});
+  if (a.stride(1) != 1) a = a.contiguous();
+  const int64_t M = a.size(0);
+  std::vector<int64_t> oshape(x.sizes().begin(), x.sizes().end() - 1);
+  oshape.push_back(N);
+  at::Tensor c;
+  if (out.has_value()) {
+    c = *out;
+    TORCH_CHECK(c.is_cuda() && c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 &&
+                    c.scalar_type() == x.scalar_type(),
+                "xdot.proj: out must be an (M, N) row-major view of the input dtype");
+  } else {
+    c = at::empty({M, N}, x.options());
+  }
+  const bool has_b = bias.has_value() && bias->defined();
+  TORCH_CHECK(!has_b || (!nn && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == x.scalar_type()),
+              "xdot.proj: bias must be a contiguous (N,) tensor of the input dtype (forward only)");
+  int rc = -3;
+  if (M > 0 && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && w.stride(1) == 1 &&
+      M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX) {
+    xdot::ProjArgs p{};
+    p.A = a.data_ptr();
+    p.B = w.data_ptr();
+    p.bias = has_b ? bias->data_ptr() : nullptr;
+    p.C = c.data_ptr();
+    p.M = (int)M;
+    p.N = (int)N;
+    p.K = (int)K;
+    p.lda = a.stride(0);
+    p.ldb = w.stride(0);
+    p.ldc = c.stride(0);
+    // every address the kernel can touch lies inside the operands' storage
+    TORCH_CHECK((M - 1) * p.lda + K <= avail_elems(a) && (nn ? (K - 1) * p.ldb + N : (N - 1) * p.ldb + K) <= avail_elems(w) &&
+                    (M - 1) * p.ldc + N <= avail_elems(c),
+                "xdot.proj: operand extents exceed their storage");
+    c10::DeviceGuard guard(x.device());
+    rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, cur_stream(x));
+    if (rc != -3) check_launch((hipError_t)rc, "gemm_proj");
+  }
+  if (rc == -3) {  // library GEMM
+    const at::Tensor wt = nn ? w : w.t();
+    if (has_b) at::addmm_out(c, *bias, a, wt);
+    else at::mm_out(c, a, wt);
+  }
+  return out.has_value() ? c : c.view(oshape);
+}
+
 // fused MSE loss forward: (mean (y - t)^2 in y's dtype, dy = 2 (y - t) / n)
 std::tuple<at::Tensor, at::Tensor> mse_fwd(const at::Tensor& y, const at::Tensor& t) {
   Range rr_("xdot.mse_fwd");
@@ -1159,6 +1218,7 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
+  m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None) -> Tensor");
   m.def("ipc_info() -> int[]");
   m.def("ipc_alloc(int nbytes, bool uncached) -> int");
   m.def("ipc_free(int ptr) -> ()");
@@ -1204,6 +1264,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("sum_partials", &sum_partials);
   m.impl("flash_prescale", &flash_prescale);
   m.impl("mse_fwd", &mse_fwd);
+  m.impl("proj", &proj);
   m.impl("flash_fwd_partial", &flash_fwd_partial);
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);

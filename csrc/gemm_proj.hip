@@ -1,0 +1,243 @@
+// xdot — projection GEMM for gfx950: the module's Linear layers (reference:
+// distributed_dot_product/module.py:43-45 keys / queries / values, :75 composition), forward and
+// input gradient.
+//
+//   NT:  C[M, N] = A[M, K] · B[N, K]ᵀ (+ bias[N])   forward   y  = x · Wᵀ + b
+//   NN:  C[M, N] = A[M, K] · B[K, N]                 backward  dx = dy · W
+//
+// A is k-contiguous (activations / output gradients, row stride lda), C row-major (ldc).  The
+// shapes are the per-rank projections: M = T/N rows (3125 at the N=8 headline rank, 25000 at
+// N=1), N, K = 768 / 1536.  At M = 3125 the 256x256-tile kernels have 78 tiles for 256 CUs
+// (fill-bound: profiles/r3_rank_host.md), so this kernel picks the tile size per shape
+// (128x128, 64x128, 64x64) to put >= 2 workgroups on every CU, and runs the whole K = 768 /
+// 1536 reduction in one workgroup (no split-K partials).
+//
+//   * 256 threads = 2x2 waves, each a (BM/2) x (BN/2) block of v_mfma_f32_16x16x32 tiles;
+//   * k-tiles of 64 through a 2-stage LDS ring filled by global_load_lds_dwordx4 (no VGPRs
+//     hold a tile in flight; the next k-tile's DMA runs under this one's MFMAs, and the
+//     co-resident workgroups cover the rest of its latency);
+//   * k-contiguous images [rows][128 B], 16-byte chunk c of row r at c ^ ((r >> 1) & 7):
+//     conflict-free ds_read_b128 fragments (the gemm3 layout); NN's B is an mn-contiguous
+//     image [64 k][256 B] read with ds_read_b64_tr_b16 (hardware transpose, gemm3's swizzle);
+//   * the MFMA computes Cᵀ tiles (B fragment as its A operand), so each lane ends with 4
+//     consecutive output columns of one row: + bias in fp32, one rounding, 8-byte stores;
+//   * rows past M re-read row M-1 (no bounds branches in the loop) and are not stored.
+#include "flash_common.h"
+
+namespace xdot {
+namespace gp {
+
+constexpr int BK = 64, NTH = 256;
+
+template <int DT> __device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
+  if constexpr (DT == DT_BF16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// N consecutive 1 KiB LDS-DMA pieces of one wave: LDS[lds + 1024 i + 16 lane] <- base + o[i]
+template <int N> __device__ __forceinline__ void dma_run(const void* base, const uint32_t* o, uint32_t lds);
+template <> __device__ __forceinline__ void dma_run<2>(const void* base, const uint32_t* o, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4\n\t"
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %4\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "s"(lds), "s"(base) : "memory", "scc");
+}
+template <> __device__ __forceinline__ void dma_run<4>(const void* base, const uint32_t* o, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %6\n\t"
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %6\n\t"
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %6\n\t"
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %6\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(lds), "s"(base)
+               : "memory", "scc");
+}
+
+template <int BM, int BN, bool NN> struct Cfg {
+  static constexpr int A_BYTES = BM * 128;                 // [BM rows][64 k x 2 B]
+  static constexpr int B_BYTES = NN ? 64 * BN * 2 : BN * 128;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int APW = A_BYTES / 4096, BPW = B_BYTES / 4096;  // 1 KiB pieces per wave
+  static constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
+};
+
+}  // namespace gp
+
+template <int DT, int BM, int BN, bool NN, bool BIAS>
+__global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
+  using namespace gp;
+  using fa::smem;
+  using fa::lds_addr;
+  using CF = Cfg<BM, BN, NN>;
+  using T16 = typename dt_traits<DT>::T;
+  static_assert(!NN || BN == 128, "NN: 256-byte mn-contiguous B rows");
+  constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l15 = lane & 15;
+  const int tiles_n = p.N / BN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tiles_n, tn = lin % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int KT = p.K / BK;
+  const int64_t lda2 = (int64_t)p.lda * 2, ldb2 = (int64_t)p.ldb * 2;
+
+  // ---- per-lane DMA source offsets (constant over k-tiles: the bases advance) ----
+  uint32_t oa[APW], ob[BPW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    const int pc = wave * APW + i;
+    const int r = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    const int rr = min(r, p.M - 1 - m0);  // rows past M re-read row M-1 (never stored)
+    oa[i] = (uint32_t)(rr * lda2 + 16 * c);
+  }
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const int pc = wave * BPW + i;
+    if constexpr (!NN) {
+      const int r = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+      ob[i] = (uint32_t)(r * ldb2 + 16 * c);
+    } else {
+      const int k = 4 * pc + (lane >> 4), c = (lane & 15) ^ (2 * (k & 3) + 8 * ((k >> 3) & 1));
+      ob[i] = (uint32_t)(k * ldb2 + 16 * c);
+    }
+  }
+  const char* a_base = reinterpret_cast<const char*>(p.A) + (int64_t)m0 * lda2;
+  const char* b_base = reinterpret_cast<const char*>(p.B) + (NN ? (int64_t)n0 * 2 : (int64_t)n0 * ldb2);
+  const int64_t b_kstep = NN ? 64 * ldb2 : 128;
+  auto issue = [&](int kt, int s) __attribute__((always_inline)) {
+    char* st = smem + s * CF::STAGE;
+    dma_run<APW>(a_base + (int64_t)kt * 128, oa, lds_addr(st + wave * APW * 1024));
+    dma_run<BPW>(b_base + (int64_t)kt * b_kstep, ob, lds_addr(st + CF::A_BYTES + wave * BPW * 1024));
+  };
+
+  // ---- fragment reads (16x16x32 operand: lane l holds mn = base + (l & 15), k = 8 (l >> 4) .. +7) ----
+  typedef const __attribute__((address_space(3))) char lds_char;
+  const int kcb0 = l15 * 128 + 16 * ((0 + g) ^ (l15 >> 1));
+  const int kcb1 = l15 * 128 + 16 * ((4 + g) ^ (l15 >> 1));
+  auto kfrag = [&](const char* img, int mnb, int ks) __attribute__((always_inline)) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(img + (ks ? kcb1 : kcb0) + mnb * 128);
+  };
+  // mn-contiguous transposed reads (NN's B): lane 4q + p of group g reads k row 8 g + q (+4,
+  // + 32 ks), logical chunk (n base / 8) + (p >> 1) of that row
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  auto mc_base = [&](int cb) __attribute__((always_inline)) {
+    const int c = (tp >> 1) | ((cb ^ (2 * tq + 8 * (g & 1))) & 14);
+    return (8 * g + tq) * 256 + 16 * c + 8 * (tp & 1);
+  };
+  int mcb[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) mcb[nt] = NN ? mc_base((CF::WN * wn + 16 * nt) / 8) : 0;
+  auto bfrag = [&](const char* img, int nt, int ks) __attribute__((always_inline)) -> u32x4 {
+    if constexpr (!NN) {
+      return kfrag(img, CF::WN * wn + 16 * nt, ks);
+    } else {
+      lds_char* b = (lds_char*)img + mcb[nt] + ks * 32 * 256;
+      fa::s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((fa::lds_s16x4*)(b));
+      fa::s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((fa::lds_s16x4*)(b + 4 * 256));
+      union { struct { fa::s16x4 a, b; } s; u32x4 u; } r;
+      r.s.a = lo;
+      r.s.b = hi;
+      return r.u;
+    }
+  };
+
+  // acc[mt][nt]: rows m0 + WM wm + 16 mt + l15, columns n0 + WN wn + 16 nt + 4 g .. +3
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    fa::wait_vm<0>();   // k-tile kt landed
+    fa::raw_barrier();  // ... for every wave; and every wave is done with the other stage
+    if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
+    const char* st = smem + (kt & 1) * CF::STAGE;
+    const char* ai = st;
+    const char* bi = st + CF::A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 fa_[MT], fb_[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) fa_[mt] = kfrag(ai, CF::WM * wm + 16 * mt, ks);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) fb_[nt] = bfrag(bi, nt, ks);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16<DT>(fb_[nt], fa_[mt], acc[mt][nt]);
+    }
+  }
+
+  // ---- epilogue: + bias (fp32), one rounding, 8-byte stores of 4 consecutive columns ----
+  f32x4 bv[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    bv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BIAS) {
+      const T16* bp = reinterpret_cast<const T16*>(p.bias) + n0 + CF::WN * wn + 16 * nt + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[nt][e] = (float)bp[e];
+    }
+  }
+  T16* cp = reinterpret_cast<T16*>(p.C);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = m0 + CF::WM * wm + 16 * mt + l15;
+    if (m < p.M) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const f32x4 v = acc[mt][nt] + bv[nt];
+        u32x2 w;
+        w[0] = fa::pack2<DT>(v[0], v[1]);
+        w[1] = fa::pack2<DT>(v[2], v[3]);
+        *reinterpret_cast<u32x2*>(cp + (int64_t)m * p.ldc + n0 + CF::WN * wn + 16 * nt + 4 * g) = w;
+      }
+    }
+  }
+}
+
+}  // namespace xdot
+
+// Tile choice: the largest tile that still puts >= 2 workgroups on every CU of the 256
+// (NN needs BN = 128).  Returns -3 when the shape / layout is not eligible (the caller falls
+// back to the library GEMM).
+extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hipStream_t st) {
+  using namespace xdot;
+  if (dt != DT_BF16 && dt != DT_F16) return -3;
+  if (a->M < 1 || a->K < gp::BK || a->K % gp::BK || a->N % 64 || a->lda % 8 || a->ldb % 8 || a->ldc % 4) return -3;
+  if ((reinterpret_cast<uintptr_t>(a->A) | reinterpret_cast<uintptr_t>(a->B)) & 15) return -3;
+  if (reinterpret_cast<uintptr_t>(a->C) & 7) return -3;
+  if (nn && a->N % 128) return -3;
+  auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
+  int bm = 64, bn = 64;
+  if (a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
+  else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) bn = 128;
+  const int64_t grid = tiles(bm, bn);
+  if (grid > 0x7FFFFFFF) return -3;
+  const bool bias = a->bias != nullptr;
+#define GPL(DTV, BMV, BNV, NNV, BV)                                                                          \
+  hipLaunchKernelGGL((gemm_proj_kernel<DTV, BMV, BNV, NNV, BV>), dim3((unsigned)grid), dim3(gp::NTH),       \
+                     (gp::Cfg<BMV, BNV, NNV>::LDS), st, *a)
+#define GPB(DTV, BMV, BNV, NNV) \
+  if (bias) GPL(DTV, BMV, BNV, NNV, true); else GPL(DTV, BMV, BNV, NNV, false)
+#define GPD(BMV, BNV, NNV) \
+  if (dt == DT_BF16) { GPB(DT_BF16, BMV, BNV, NNV); } else { GPB(DT_F16, BMV, BNV, NNV); }
+  if (nn) {
+    if (bm == 128) { GPD(128, 128, true); } else { GPD(64, 128, true); }
+  } else {
+    if (bm == 128) { GPD(128, 128, false); }
+    else if (bn == 128) { GPD(64, 128, false); }
+    else { GPD(64, 64, false); }
+  }
+#undef GPD
+#undef GPB
+#undef GPL
+  return (int)hipGetLastError();
+}

@@ -114,6 +114,16 @@ struct AdamArgs {
   const float* step_dev[ADAM_MAX_T];
   const float* lr_dev;
 };
+// projection GEMM (csrc/gemm_proj.hip): C[M, N] = A[M, K] . op(B) (+ bias[N]); A k-contiguous,
+// B = W[N, K] (NT, forward) or W[K, N] (NN, input gradient), 16-bit, C row-major
+struct ProjArgs {
+  const void* A;
+  const void* B;
+  const void* bias;  // nullptr: none
+  void* C;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+};
 namespace ipc {
 constexpr int MAXR = 8;     // ranks of one node
 constexpr int MAXG = 256;   // workgroups (byte ranges) per collective
@@ -145,6 +155,9 @@ int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws, int splits
 // 8-phase 16x16x32 16-bit GEMM (csrc/gemm3.hip): M, N >= 256, K % 8 == 0; -3 = not eligible
 int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);
+// projection GEMM; -3 = not eligible (16-bit, K % 64 == 0, N % 64 == 0 (NN: % 128), 16-byte
+// aligned A / B with lda, ldb % 8 == 0, 8-byte aligned C with ldc % 4 == 0)
+int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hipStream_t st);
 // fp32 operand -> compact bf16 parts [z1][z2][3][seg][R][C] (hi, or lo where lo_mask bit p is set)
 int xdot_split3_launch(const float* src, void* dst, int64_t s1, int64_t s2, int64_t sseg, int64_t ld,
                        int nb1, int nb2, int nseg, int R, int C, int lo_mask, hipStream_t st);

@@ -22,10 +22,9 @@ restores it), and hands back the eight parameter gradients and the input gradien
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from .. import _ext
-from ..ops.linear import linear_backward, native_wgrad
+from ..ops.linear import linear_backward, native_wgrad, proj
 from ..utils.env import FLAGS
 from ..parallel.attention import SeqParallelAttention, gather_plan, start_gather
 
@@ -86,18 +85,14 @@ class AttnBlockFn(torch.autograd.Function):
             # rank block, the xGMI pull kernel skips its own-block copy)
             gbuf = torch.empty((n, B, R, wqv.shape[0]), dtype=xqv.dtype, device=xqv.device)
             qv = gbuf[comm.rank]
-            x2 = xqv.reshape(-1, xqv.shape[-1])
-            if bqv is None:
-                torch.mm(x2, wqv.t(), out=qv.view(-1, qv.shape[-1]))
-            else:
-                torch.addmm(bqv, x2, wqv.t(), out=qv.view(-1, qv.shape[-1]))
+            proj(xqv, wqv, bqv, out=qv.view(-1, qv.shape[-1]))
         else:
-            qv = F.linear(xqv, wqv, bqv)
+            qv = proj(xqv, wqv, bqv)
         pending = start_gather(qv, comm, chunks=chunk_plan, out=gbuf)  # in flight under the row-side GEMM
-        k = F.linear(xk, wk, bk)
+        k = proj(xk, wk, bk)
         actx = _Ctx()
         o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending)
-        out = F.linear(o, wc, bc)
+        out = proj(o, wc, bc)
         ctx.actx = actx
         ctx.sync = sync
         ctx.params = (wk, bk, wq, bq, wv, bv, wc, bc)

@@ -1,9 +1,13 @@
-"""Projection ``Linear`` with a split-K weight gradient on the MFMA GEMM (``csrc/gemm.hip``).
+"""Projection ``Linear`` on xdot MFMA kernels: forward and input gradient on the projection GEMM
+(``csrc/gemm_proj.hip``), split-K weight gradient on the GEMM kernels (``csrc/gemm2.hip``).
 
 The four projections of the module (reference: ``distributed_dot_product/module.py:36-39``,
-applied at ``:43-45`` and ``:75``) are ordinary ``nn.Linear`` layers; their forward and the
-input gradient ``dX = dY·W`` are well served by hipBLASLt.  The weight gradient
-``dW = dYᵀ·X`` is not: its reduction runs over the sequence (K = T/N rows: 25000 at N = 1)
+applied at ``:43-45`` and ``:75``) are ordinary ``nn.Linear`` layers.  Their forward
+``y = x·Wᵀ + b`` and input gradient ``dX = dY·W`` (:func:`proj`, :func:`proj_dx`) pick a tile size
+per shape so the T/N = 3125-row products of an N=8 rank still put >= 2 workgroups on every CU
+(the library's host cost per call, ~19 µs, also exceeded its GPU time there:
+``profiles/r3_rank_host.md``).  The weight gradient
+``dW = dYᵀ·X`` has a reduction over the sequence (K = T/N rows: 25000 at N = 1)
 while the output is only 768 x 768 (9 tiles of 256²) — hipBLASLt runs it at ≈170-330 TF/s
 with most CUs idle.  Here K is split into slices that fill the 256 CUs (the 256x256 kernel of
 ``csrc/gemm2.hip`` chooses the split; other shapes use S slabs of the 128x128 kernel), each
@@ -24,7 +28,7 @@ import torch.nn.functional as F
 from .. import _ext
 from .gemm import strided_gemm
 
-__all__ = ["linear", "linear_backward", "weight_grad", "LinearFn"]
+__all__ = ["linear", "linear_backward", "weight_grad", "LinearFn", "proj", "proj_dx"]
 
 _SLOTS = 512       # 2 workgroups per CU x 256 CUs
 _MIN_SLAB = 256    # rows of K per split
@@ -40,6 +44,35 @@ def _splits(M: int, N: int, K: int) -> int:
         if K % d == 0:
             return d
     return s
+
+
+def _proj_ok(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> bool:
+    from ..utils.env import FLAGS
+
+    return (FLAGS.proj_kernel and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype
+            and (bias is None or bias.dtype == x.dtype) and _ext.use_hip(x, weight))
+
+
+def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear(x, weight, bias)`` on the projection GEMM (16-bit GPU tensors; shapes it does
+    not take run on the library inside the op).  ``out``: an (M, N) row-major view to write,
+    e.g. this rank's block of an all-gather buffer."""
+    if _proj_ok(x, weight, bias):
+        return _ext.ops().proj(x, weight, bias, False, out)
+    if out is None:
+        return F.linear(x, weight, bias)
+    x2 = x.reshape(-1, x.shape[-1])
+    if bias is None:
+        return torch.mm(x2, weight.t(), out=out)
+    return torch.addmm(bias, x2, weight.t(), out=out)
+
+
+def proj_dx(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Input gradient ``dy · weight`` of ``F.linear`` for 2-D ``dy`` (M, N_out) -> (M, N_in)."""
+    if _proj_ok(dy, weight):
+        return _ext.ops().proj(dy, weight, None, True, None)
+    return dy @ weight
 
 
 def native_wgrad(dy: torch.Tensor, x: torch.Tensor) -> bool:
@@ -97,7 +130,7 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, nee
     dx = dw = db = None
     dy2 = dy.reshape(-1, dy.shape[-1])
     if need_dx:
-        dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+        dx = proj_dx(dy2, weight).view(*dy.shape[:-1], weight.shape[1])
     side = getattr(dy, "_xdot_ready_on", None)  # dy is complete on this stream (see below)
     if side is not None and need_dw and not native_wgrad(dy, x):
         side = None  # a library GEMM stays on the current stream (native_wgrad)
@@ -128,7 +161,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        return proj(x, weight, bias)
 
     @staticmethod
     @_ext.pinned
@@ -139,8 +172,11 @@ class LinearFn(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear`` with the split-K MFMA weight gradient for bf16/fp16 GPU tensors."""
+    """``F.linear`` on the projection GEMM with the split-K MFMA weight gradient for bf16/fp16 GPU
+    tensors."""
     if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype \
-            and torch.is_grad_enabled() and _ext.use_hip(x):
-        return LinearFn.apply(x, weight, bias)
+            and _ext.use_hip(x):
+        if torch.is_grad_enabled():
+            return LinearFn.apply(x, weight, bias)
+        return proj(x, weight, bias)
     return F.linear(x, weight, bias)

@@ -113,6 +113,7 @@ class _Flags:
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
+        self.proj_kernel = _flag("XDOT_PROJ", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
         self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
