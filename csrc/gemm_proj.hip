@@ -13,7 +13,7 @@
 // 1536 reduction in one workgroup (no split-K partials).
 //
 //   * 256 threads = 2x2 waves, each a (BM/2) x (BN/2) block of v_mfma_f32_16x16x32 tiles;
-//   * k-tiles of 64 through a 2-stage LDS ring filled by global_load_lds_dwordx4 (no VGPRs
+//   * k-tiles of 64 through a 2- or 3-stage LDS ring filled by global_load_lds_dwordx4 (no VGPRs
 //     hold a tile in flight; the next k-tile's DMA runs under this one's MFMAs, and the
 //     co-resident workgroups cover the rest of its latency);
 //   * k-contiguous images [rows][128 B], 16-byte chunk c of row r at c ^ ((r >> 1) & 7):
@@ -28,6 +28,18 @@ namespace xdot {
 namespace gp {
 
 constexpr int BK = 64, NTH = 256;
+#ifndef GP_PRIO
+#define GP_PRIO 0  // s_setprio 1 around each k-step's MFMAs (A/B knob)
+#endif
+#ifndef GP_NS_BIG
+#define GP_NS_BIG 2  // ring stages of the 128x128 tile (3: 96 KiB, one workgroup per CU)
+#endif
+#ifndef GP_NS_SMALL
+#define GP_NS_SMALL 2  // ring stages of the 64-row tiles
+#endif
+#ifndef GP_BIG
+#define GP_BIG 1  // 0: never the 128x128 tile (64x128 at every M)
+#endif
 
 template <int DT> __device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
   if constexpr (DT == DT_BF16)
@@ -54,11 +66,12 @@ template <> __device__ __forceinline__ void dma_run<4>(const void* base, const u
                : "memory", "scc");
 }
 
-template <int BM, int BN, bool NN> struct Cfg {
+template <int BM, int BN, bool NN, int NS_ = (BM == 128 ? GP_NS_BIG : GP_NS_SMALL)> struct Cfg {
+  static constexpr int NS = NS_;
   static constexpr int A_BYTES = BM * 128;                 // [BM rows][64 k x 2 B]
   static constexpr int B_BYTES = NN ? 64 * BN * 2 : BN * 128;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int LDS = 2 * STAGE;
+  static constexpr int LDS = NS * STAGE;
   static constexpr int APW = A_BYTES / 4096, BPW = B_BYTES / 4096;  // 1 KiB pieces per wave
   static constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
 };
@@ -73,7 +86,8 @@ __global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
   using CF = Cfg<BM, BN, NN>;
   using T16 = typename dt_traits<DT>::T;
   static_assert(!NN || BN == 128, "NN: 256-byte mn-contiguous B rows");
-  constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW;
+  constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW, NS = CF::NS;
+  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -153,12 +167,22 @@ __global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
+  // NS-stage ring: k-tile kt lives in stage kt % NS; NS - 1 k-tiles are in flight while one is
+  // consumed.  The wait at the top of iteration kt leaves the DMAs of k-tiles kt+1 .. kt+NS-2
+  // (NPW instructions each) outstanding.
+  constexpr int NPW = APW + BPW;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < KT) issue(i, i);
   for (int kt = 0; kt < KT; ++kt) {
-    fa::wait_vm<0>();   // k-tile kt landed
-    fa::raw_barrier();  // ... for every wave; and every wave is done with the other stage
-    if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
-    const char* st = smem + (kt & 1) * CF::STAGE;
+    if constexpr (NS == 3) {
+      if (kt + 1 < KT) fa::wait_vm<NPW>(); else fa::wait_vm<0>();
+    } else {
+      fa::wait_vm<0>();
+    }
+    fa::raw_barrier();  // k-tile kt visible to every wave; every wave is done with stage (kt - 1) % NS
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* st = smem + (kt % NS) * CF::STAGE;
     const char* ai = st;
     const char* bi = st + CF::A_BYTES;
 #pragma unroll
@@ -168,10 +192,12 @@ __global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
       for (int mt = 0; mt < MT; ++mt) fa_[mt] = kfrag(ai, CF::WM * wm + 16 * mt, ks);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) fb_[nt] = bfrag(bi, nt, ks);
+      if constexpr (GP_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16<DT>(fb_[nt], fa_[mt], acc[mt][nt]);
+      if constexpr (GP_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -217,7 +243,7 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hi
   if (nn && a->N % 128) return -3;
   auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
   int bm = 64, bn = 64;
-  if (a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
+  if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
   else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) bn = 128;
   const int64_t grid = tiles(bm, bn);
   if (grid > 0x7FFFFFFF) return -3;

@@ -131,6 +131,34 @@ def test_module_flash_deterministic(gpu):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_module_side_stream_weight_gradients_match(gpu, dtype):
+    """XDOT_WGRAD_SIDE=1 (weight gradients on side streams beside the attention backward; off by
+    default) gives bitwise the same outputs and gradients as the one-stream default; in fp32 the
+    library weight gradients stay on the current stream (two library GEMMs on two streams can
+    stall each other: xdot.ops.linear.native_wgrad)."""
+    import xdot
+    from xdot.utils.env import FLAGS
+
+    torch.manual_seed(0)
+    m = xdot.DistributedDotProductAttn(768, num_heads=8, impl="flash").to(gpu, dtype)
+    x = torch.rand(1, 3000, 768, device=gpu, dtype=dtype)
+    res = []
+    old = FLAGS.wgrad_side
+    try:
+        for side in (False, True):
+            FLAGS.wgrad_side = side
+            m.zero_grad(set_to_none=True)
+            y = m(x, x, x, None)
+            y.float().square().mean().backward()
+            torch.cuda.synchronize()
+            res.append([y.detach().clone()] + [p.grad.clone() for p in m.parameters()])
+    finally:
+        FLAGS.wgrad_side = old
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("chunks", [2, 3])
 def test_module_multi_rank_gather_chunks(gpu, monkeypatch, chunks):
     """The chunked all-gather / reduce-scatter pipeline (XDOT_GATHER_CHUNKS) gives the same

@@ -46,8 +46,9 @@ variable                    default   effect
                                       node per op)
 ``XDOT_MASK_ASYNC``         0         pack the attention mask on a side stream (neutral at N=1,
                                       1.7 % slower at the N=8 rank: profiles/r1_s7_mask_async_ab.md)
-``XDOT_WGRAD_SIDE``         1         the [q|v] weight gradient starts on the backward's priority
-                                      stream as soon as the gathered-side gradient lands
+``XDOT_WGRAD_SIDE``         0         weight gradients on side streams beside the attention
+                                      backward (same GPU time, +0.1-0.4 ms host per step: off;
+                                      profiles/r4_s2.md)
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
 ``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
@@ -112,7 +113,7 @@ class _Flags:
         self.fp32_mode = _str("XDOT_FP32_MODE", "exact")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
-        self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="1")
+        self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _flag("XDOT_PROJ", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
