@@ -27,9 +27,12 @@
 namespace xdot {
 namespace gp {
 
-constexpr int BK = 64, NTH = 256;
+constexpr int BK = 64;
 #ifndef GP_PRIO
-#define GP_PRIO 0  // s_setprio 1 around each k-step's MFMAs (A/B knob)
+#define GP_PRIO 1  // s_setprio 1 around each k-step's MFMAs (A/B knob; 0-2 % faster, profiles/r4_s2.md)
+#endif
+#ifndef GP_PRE
+#define GP_PRE 0  // read both k-steps' fragments before the first k-step's MFMAs (A/B knob)
 #endif
 #ifndef GP_NS_BIG
 #define GP_NS_BIG 2  // ring stages of the 128x128 tile (3: 96 KiB, one workgroup per CU)
@@ -39,6 +42,9 @@ constexpr int BK = 64, NTH = 256;
 #endif
 #ifndef GP_BIG
 #define GP_BIG 1  // 0: never the 128x128 tile (64x128 at every M)
+#endif
+#ifndef GP_HUGE
+#define GP_HUGE 0  // 1: 256x128 tiles of 8 waves where they fill >= 4 rounds of the 256 CUs (A/B knob)
 #endif
 
 template <int DT> __device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
@@ -66,20 +72,21 @@ template <> __device__ __forceinline__ void dma_run<4>(const void* base, const u
                : "memory", "scc");
 }
 
-template <int BM, int BN, bool NN, int NS_ = (BM == 128 ? GP_NS_BIG : GP_NS_SMALL)> struct Cfg {
+template <int BM, int BN, bool NN, int NS_ = (BM >= 128 ? GP_NS_BIG : GP_NS_SMALL)> struct Cfg {
   static constexpr int NS = NS_;
+  static constexpr int WGM = BM == 256 ? 4 : 2, NW = 2 * WGM, NTH = 64 * NW;  // waves: WGM x 2
   static constexpr int A_BYTES = BM * 128;                 // [BM rows][64 k x 2 B]
   static constexpr int B_BYTES = NN ? 64 * BN * 2 : BN * 128;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int LDS = NS * STAGE;
-  static constexpr int APW = A_BYTES / 4096, BPW = B_BYTES / 4096;  // 1 KiB pieces per wave
-  static constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
+  static constexpr int APW = A_BYTES / (1024 * NW), BPW = B_BYTES / (1024 * NW);  // 1 KiB pieces per wave
+  static constexpr int WM = BM / WGM, WN = BN / 2, MT = WM / 16, NT = WN / 16;
 };
 
 }  // namespace gp
 
 template <int DT, int BM, int BN, bool NN, bool BIAS>
-__global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
+__global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjArgs p) {
   using namespace gp;
   using fa::smem;
   using fa::lds_addr;
@@ -91,7 +98,7 @@ __global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave >> 1, wn = wave & 1;  // WGM x 2 waves
   const int g = lane >> 4, l15 = lane & 15;
   const int tiles_n = p.N / BN;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -185,18 +192,25 @@ __global__ __launch_bounds__(256, 2) void gemm_proj_kernel(ProjArgs p) {
     const char* st = smem + (kt % NS) * CF::STAGE;
     const char* ai = st;
     const char* bi = st + CF::A_BYTES;
+    // GP_PRE: both k-steps' fragments are read up front (the second k-step's reads fly under the
+    // first k-step's MFMAs); else each k-step reads, then multiplies
+    u32x4 fa_[2][MT], fb_[2][NT];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      u32x4 fa_[MT], fb_[NT];
+      if (ks == 0 || !GP_PRE) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) fa_[mt] = kfrag(ai, CF::WM * wm + 16 * mt, ks);
+        for (int kk = ks; kk < (GP_PRE ? 2 : ks + 1); ++kk) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) fb_[nt] = bfrag(bi, nt, ks);
+          for (int mt = 0; mt < MT; ++mt) fa_[kk][mt] = kfrag(ai, CF::WM * wm + 16 * mt, kk);
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) fb_[kk][nt] = bfrag(bi, nt, kk);
+        }
+      }
       if constexpr (GP_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16<DT>(fb_[nt], fa_[mt], acc[mt][nt]);
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16<DT>(fb_[ks][nt], fa_[ks][mt], acc[mt][nt]);
       if constexpr (GP_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -243,22 +257,24 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hi
   if (nn && a->N % 128) return -3;
   auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
   int bm = 64, bn = 64;
-  if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
+  if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) { bm = 256; bn = 128; }
+  else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
   else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) bn = 128;
   const int64_t grid = tiles(bm, bn);
   if (grid > 0x7FFFFFFF) return -3;
   const bool bias = a->bias != nullptr;
 #define GPL(DTV, BMV, BNV, NNV, BV)                                                                          \
-  hipLaunchKernelGGL((gemm_proj_kernel<DTV, BMV, BNV, NNV, BV>), dim3((unsigned)grid), dim3(gp::NTH),       \
+  hipLaunchKernelGGL((gemm_proj_kernel<DTV, BMV, BNV, NNV, BV>), dim3((unsigned)grid), dim3(gp::Cfg<BMV, BNV, NNV>::NTH),       \
                      (gp::Cfg<BMV, BNV, NNV>::LDS), st, *a)
 #define GPB(DTV, BMV, BNV, NNV) \
   if (bias) GPL(DTV, BMV, BNV, NNV, true); else GPL(DTV, BMV, BNV, NNV, false)
 #define GPD(BMV, BNV, NNV) \
   if (dt == DT_BF16) { GPB(DT_BF16, BMV, BNV, NNV); } else { GPB(DT_F16, BMV, BNV, NNV); }
   if (nn) {
-    if (bm == 128) { GPD(128, 128, true); } else { GPD(64, 128, true); }
+    if (bm == 256) { GPD(256, 128, true); } else if (bm == 128) { GPD(128, 128, true); } else { GPD(64, 128, true); }
   } else {
-    if (bm == 128) { GPD(128, 128, false); }
+    if (bm == 256) { GPD(256, 128, false); }
+    else if (bm == 128) { GPD(128, 128, false); }
     else if (bn == 128) { GPD(64, 128, false); }
     else { GPD(64, 64, false); }
   }

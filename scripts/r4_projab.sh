@@ -20,4 +20,7 @@ timeout -k 10 200 python bench.py --seq-len 5000 --steps 50 --warmup 10 --fp32-s
 timeout -k 10 200 python benchmarks/bench_rank.py --world 8 --steps 30 --warmup 5 --fp32-steps 0 > $O/r8.log 2>&1 || exit $?
 timeout -k 10 200 python benchmarks/bench_rank.py --world 8 --rank 3 --steps 30 --warmup 5 --fp32-steps 0 > $O/r8_rank3.log 2>&1 || exit $?
 timeout -k 10 300 python benchmarks/host_step_profile.py --world 8 --steps 40 --inline-backward > $O/host8.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_module_gpu.py tests/test_ring_ops.py -x -q --timeout 300 --timeout-method thread -k "ring" > $O/pytest_ring.log 2>&1 || exit $?
+timeout -k 10 300 python benchmarks/bench_rank.py --world 8 --steps 10 --warmup 3 --impl ring --link-gbps 300 --p2p-gbps 64 --fp32-steps 0 > $O/ring8.log 2>&1 || exit $?
+XDOT_RING_BIDIR=0 timeout -k 10 300 python benchmarks/bench_rank.py --world 8 --steps 10 --warmup 3 --impl ring --link-gbps 300 --p2p-gbps 64 --fp32-steps 0 > $O/ring8_uni.log 2>&1 || exit $?
 echo projab-ok

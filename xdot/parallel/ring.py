@@ -112,7 +112,12 @@ class _Rings:
     With ``N >= 3`` ranks the block is split by rows: rows ``[0, R/2)`` travel one way round the
     ring and rows ``[R/2, R)`` the other, so every hop drives TWO xGMI links (to rank+1 and to
     rank-1) with half the bytes each: the hop takes half the time of a one-way ring.  Lane i is
-    ``(d, a, b)``: direction and the block rows it carries."""
+    ``(d, a, b)``: direction and the block rows it carries.
+
+    ``merged`` (B = 1): the two lanes' halves live in ONE (1, R, 2C) buffer per ring slot
+    (``full_cur`` / ``full_nxt``), so each step's kernels run once over the whole block (columns
+    [0, R/2) from one source rank, [R/2, R) from the other) -- as many launches per hop as the
+    one-way ring, at full width."""
 
     def __init__(self, comm, blk: Tensor, bidir: bool):
         R = blk.shape[1]
@@ -123,9 +128,20 @@ class _Rings:
             self.lanes = [(1, 0, h), (-1, h, R)]
         else:
             self.lanes = [(1, 0, R)]
-        self.rings = [_Ring(comm, blk[:, a:b].contiguous() if len(self.lanes) > 1 else blk, d)
-                      for (d, a, b) in self.lanes]
+        self.merged = len(self.lanes) > 1 and blk.shape[0] == 1 and blk.is_contiguous()
+        if self.merged:
+            self.full_first = self.full_cur = blk
+            self.full_nxt = torch.empty_like(blk)
+            self.rings = [_Ring(comm, blk[:, a:b], d) for (d, a, b) in self.lanes]
+            self._views()
+        else:
+            self.rings = [_Ring(comm, blk[:, a:b].contiguous() if len(self.lanes) > 1 else blk, d)
+                          for (d, a, b) in self.lanes]
         self.h = None
+
+    def _views(self):
+        for r, (_d, a, b) in zip(self.rings, self.lanes):
+            r.cur, r.nxt = self.full_cur[:, a:b], self.full_nxt[:, a:b]
 
     def start(self, s: int):
         if s < self.comm.world_size - 1:
@@ -135,8 +151,29 @@ class _Rings:
         if self.h is not None:
             self.h.wait()
             self.h = None
-            for r in self.rings:
-                r.rotate()
+            if self.merged:
+                old, self.full_cur = self.full_cur, self.full_nxt
+                self.full_nxt = torch.empty_like(old) if old is self.full_first else old
+                self._views()
+            else:
+                for r in self.rings:
+                    r.rotate()
+
+    def units(self, s: int, mask: Optional[Tensor], R: int):
+        """The kernel launches of step s: ``[(block, mask view fn or None, tag, lanes)]`` -- one
+        per lane, or one over the merged block (``lanes`` = the lane indices it covers)."""
+        if self.merged:
+            (_d0, _a0, h), _ = self.lanes
+            s0, s1 = self.rings[0].src(s), self.rings[1].src(s)
+            view = (lambda m, s0=s0, s1=s1: torch.cat([_block_mask(m, s0, R, 0, h), _block_mask(m, s1, R, h, R)], -1)) \
+                if mask is not None else None
+            return [(self.full_cur, view, ("ringm", s0, s1, h, R), (0, 1))]
+        out = []
+        for li, ((_d, a, b), ring) in enumerate(zip(self.lanes, self.rings)):
+            src = ring.src(s)
+            view = (lambda m, src=src, a=a, b=b: _block_mask(m, src, R, a, b)) if mask is not None else None
+            out.append((ring.cur, view, ("ring", src, a, b, R), (li,)))
+        return out
 
 
 def _block_mask(mask: Optional[Tensor], src: int, R: int, a: int = 0, b: Optional[int] = None) -> Optional[Tensor]:
@@ -174,26 +211,24 @@ class RingAttention(torch.autograd.Function):
             fm = flash.fp32_code(k.dtype)
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
             kk = flash.prescale(k, scale) if prescaled else k.contiguous()
-            ns = int(ops.flash_splits(B, R, max(b - a for _, a, b in rings.lanes), H, False))
-            # slot 0: the running (O, LSE) of the blocks seen so far (fp32), then ns slots per lane
+            U = 1 if rings.merged else L  # kernel launches per step
+            ns = int(ops.flash_splits(B, R, R if rings.merged else max(b - a for _, a, b in rings.lanes), H, False))
+            # slot 0: the running (O, LSE) of the blocks seen so far (fp32), then ns slots per launch
             # for the arriving pieces' split partials, merged into slot 0 after each step -- resident
-            # partials stay (1 + L ns) slots whatever the ring length
-            opart = torch.empty(1 + L * ns, B, R, C, dtype=torch.float32, device=k.device)
-            lpart = torch.empty(1 + L * ns, B, H, R, dtype=torch.float32, device=k.device)
+            # partials stay (1 + U ns) slots whatever the ring length
+            opart = torch.empty(1 + U * ns, B, R, C, dtype=torch.float32, device=k.device)
+            lpart = torch.empty(1 + U * ns, B, H, R, dtype=torch.float32, device=k.device)
             lpart[0].fill_(-float("inf"))
             lrun = torch.empty(B, H, R, dtype=torch.float32, device=k.device)
             for s in range(n):
                 rings.start(s)
                 step = []
-                for li, ((_d, a, b), ring) in enumerate(zip(rings.lanes, rings.rings)):
-                    src = ring.src(s)
-                    mk = flash.prepare_mask_cached(mask, B, R, b - a, tag=("ring", src, a, b, R),
-                                                   view=lambda m, src=src, a=a, b=b: _block_mask(m, src, R, a, b))
+                for ui, (g, view, tag, _lanes) in enumerate(rings.units(s, mask, R)):
+                    mk = flash.prepare_mask_cached(mask, B, R, g.shape[1], tag=tag, view=view)
                     step.append(mk)
                     bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
-                    g = ring.cur
                     ops.flash_fwd_partial(kk, flash._kv(g[..., :C]), flash._kv(g[..., C:]), bits, flags, int(H),
-                                          float(scale), opart, lpart, 1 + li * ns, ns, prescaled, fm)
+                                          float(scale), opart, lpart, 1 + ui * ns, ns, prescaled, fm)
                 mks.append(step)
                 if s < n - 1:
                     ops.flash_fwd_merge(opart, lpart, lrun, int(H))
@@ -258,10 +293,10 @@ class RingAttention(torch.autograd.Function):
             two = ov not in ("0", "false", "off", "no") and (ov != "auto" or -(-R // 128) * B * H >= 1024)
             hi = _side_stream(do.device) if two else cur  # XDOT_RING_OVERLAP (utils/env.py)
             delta = flash.bwd_delta(do, o, H)
-            nsr = int(ops.flash_splits(B, R, max(b - a for _, a, b in lanes), H, True))
-            L = len(lanes)
-            # slot 0: running fp32 dk, then nsr column-split partial slots per lane
-            dpart = torch.empty(1 + L * nsr, B, R, C, dtype=torch.float32, device=k.device)
+            U = 1 if rings.merged else len(lanes)  # kernel launches per step
+            nsr = int(ops.flash_splits(B, R, R if rings.merged else max(b - a for _, a, b in lanes), H, True))
+            # slot 0: running fp32 dk, then nsr column-split partial slots per launch
+            dpart = torch.empty(1 + U * nsr, B, R, C, dtype=torch.float32, device=k.device)
             dpart[0].zero_()
         else:
             cdt = lse.dtype
@@ -274,24 +309,26 @@ class RingAttention(torch.autograd.Function):
                 # the gathered-side kernels run on the high-priority side stream, concurrently with
                 # the row-side partials here, when a block is big enough for that to pay
                 # (``hi is cur`` otherwise)
+                units = rings.units(s, None, R)
+                full = []
                 hi.wait_stream(cur)
                 with torch.cuda.stream(hi):
-                    for li, ring in enumerate(rings.rings):
-                        g = ring.cur
-                        c_, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[s][li], H, scale, delta,
+                    for ui, (g, _v, _t, ls) in enumerate(units):
+                        c_, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, ctx.mks[s][ui], H, scale, delta,
                                                fp32_out=True, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
-                        contribs.append(c_)
-                for li, ring in enumerate(rings.rings):
-                    g = ring.cur
-                    mk = ctx.mks[s][li]
+                        full.append(c_)
+                        # a merged launch covers both lanes: lane li's contribution is its row range
+                        contribs.extend(c_ if len(ls) == 1 else c_[:, lanes[li][1]:lanes[li][2]] for li in ls)
+                for ui, (g, _v, _t, _ls) in enumerate(units):
+                    mk = ctx.mks[s][ui]
                     bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
                     ops.flash_bwd_rows_partial(do, k, flash._kv(g[..., :C]), flash._kv(g[..., C:]), lse, delta, bits,
-                                               flags, int(H), float(scale), dpart, 1 + li * nsr, nsr, ctx.prescaled,
+                                               flags, int(H), float(scale), dpart, 1 + ui * nsr, nsr, ctx.prescaled,
                                                ctx.fp32_mode)
                 if s < n - 1:
                     ops.sum_partials_into(dpart, dpart[0])
                 cur.wait_stream(hi)
-                for c_ in contribs:
+                for c_ in full:
                     c_.record_stream(cur)
             else:
                 for li, ring in enumerate(rings.rings):
