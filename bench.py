@@ -139,7 +139,7 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
     ``warmup`` untimed ones.  Returns (ms_per_step max over ranks, host enqueue ms, loss, impl)."""
     import xdot
     from xdot.parallel import GradSync
-    from xdot.ops.loss import unit_grad
+    from xdot.ops.loss import backward, unit_grad
 
     n, rank = comm.world_size, comm.rank
     T = a.seq_len
@@ -175,7 +175,8 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
         opt.zero_grad(set_to_none=True)
         out = model(x, x, x, mask)
         loss = crit(out, y)
-        loss.backward(unit_grad(loss))  # == loss.backward(), minus the seed fill / scaling pass
+        # == loss.backward(), minus the seed fill / scaling pass, on this thread (XDOT_INLINE_BACKWARD)
+        backward(loss, unit_grad(loss))
         # with several ranks the update of the buckets already reduced runs under the last
         # gradient all-reduce (GradSync.wait(optimizer=...)); otherwise one step after the wait
         stepped = sync.wait(optimizer=None if a.no_optim or not a.split_step else opt)

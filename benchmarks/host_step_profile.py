@@ -19,25 +19,25 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--inline-backward", action="store_true",
-                    help="run backward on the calling thread (torch.autograd.set_multithreading_enabled(False)) "
-                         "so cProfile sees the Python backward functions too")
+                    help="(default now: XDOT_INLINE_BACKWARD=1) kept for old scripts")
     a = ap.parse_args()
     import torch
 
     import bench
     from xdot.utils.comm import EmulatedComm
+    from xdot.utils.env import FLAGS
 
     args = bench.parse(["--gpus", str(a.world), "--fp32-steps", "0", "--no-check"])
     comm = EmulatedComm(a.world)
     dev = torch.device("cuda", 0)
+    inline = FLAGS.inline_backward
     bench.time_step(args, comm, dev, torch.bfloat16, 5, 5)  # warm everything (kernels, caches, allocator)
-    ms0, host0, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)
-    print(f"world {a.world}: {ms0:.3f} ms/step, host enqueue {host0:.3f} ms/step (unprofiled, engine thread)")
-    if a.inline_backward:
-        torch.autograd.set_multithreading_enabled(False)
-        bench.time_step(args, comm, dev, torch.bfloat16, 5, 5)
+    for mode in (False, True):  # autograd's device worker thread, then the calling thread
+        FLAGS.inline_backward = mode
         ms0, host0, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)
-        print(f"world {a.world}: {ms0:.3f} ms/step, host enqueue {host0:.3f} ms/step (unprofiled, inline backward)")
+        print(f"world {a.world}: {ms0:.3f} ms/step, host enqueue {host0:.3f} ms/step "
+              f"(unprofiled, {'inline backward' if mode else 'engine thread'})")
+    FLAGS.inline_backward = inline
     pr = cProfile.Profile()
     pr.enable()
     ms, host_ms, _, _ = bench.time_step(args, comm, dev, torch.bfloat16, a.steps, 2)

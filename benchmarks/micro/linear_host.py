@@ -6,7 +6,8 @@ For each shape (T/N = 3125 rows, D = 768; [q|v] = 1536 outputs) and route, print
   host_us   wall time to ENQUEUE one call (GPU kept busy first, so the host never waits),
   gpu_us    GPU time per call (events around `calls` calls queued behind busy work).
 Routes: torch F.linear / matmul on hipBLASLt (the default) and rocBLAS ("hipblas"), the projection
-kernel (`torch.ops.xdot.proj`, csrc/gemm_proj.hip: forward NT and input-gradient NN), and
+kernel (`torch.ops.xdot.proj`, csrc/gemm_proj.hip: forward NT and input-gradient NN; forced, and
+"auto" = the op's own kernel-or-library choice), and
 `xdot.gemm.strided_gemm` (path 1 = 128x128, 3 = gemm3).
 """
 from __future__ import annotations
@@ -81,15 +82,17 @@ def main():
                 res[f"torch_{lib}"] = measure(lambda: F.linear(x, w, b), args.calls)
                 res[f"torch_{lib}_nobias"] = measure(lambda: F.linear(x, w), args.calls)
             torch.backends.cuda.preferred_blas_library("hipblaslt")
-            res["xdot_proj"] = measure(lambda: ops.proj(x, w, b, False, None), args.calls)
-            res["xdot_proj_nobias"] = measure(lambda: ops.proj(x, w, None, False, None), args.calls)
+            res["xdot_proj"] = measure(lambda: ops.proj(x, w, b, False, None, 1), args.calls)
+            res["xdot_proj_nobias"] = measure(lambda: ops.proj(x, w, None, False, None, 1), args.calls)
+            res["xdot_proj_auto"] = measure(lambda: ops.proj(x, w, b, False, None, 0), args.calls)
             for path in (1, 3) if not args.quick else ():
                 res[f"xdot_path{path}"] = measure(
                     lambda: strided_gemm(x, w, out, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, path=path), args.calls)
         else:
             w = torch.randn(k, n, device="cuda", dtype=dt) * 0.03  # Linear(n -> k) weight: dx = dy W
             res["torch_hipblaslt"] = measure(lambda: x @ w, args.calls)
-            res["xdot_proj"] = measure(lambda: ops.proj(x, w, None, True, None), args.calls)
+            res["xdot_proj"] = measure(lambda: ops.proj(x, w, None, True, None, 1), args.calls)
+            res["xdot_proj_auto"] = measure(lambda: ops.proj(x, w, None, True, None, 0), args.calls)
         for r, (h, g) in res.items():
             print(json.dumps({"case": name, "M": m, "N": n, "K": k, "route": r, "host_us": round(h, 2),
                               "gpu_us": round(g, 2)}), flush=True)

@@ -685,9 +685,10 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
 // Projection GEMM (csrc/gemm_proj.hip): nn = false: y = x Wᵀ (+ bias), W (N, K); nn = true:
 // dx = dy W, W (K, N) (the input gradient of the same Linear).  x: (..., K) with unit last
 // stride; out (optional): an (M, N) row-major view to write (e.g. this rank's block of the
-// all-gather buffer).  Shapes / layouts the kernel does not take run on the library GEMM.
+// all-gather buffer).  Shapes / layouts the kernel does not take, and (force = 0) products
+// large enough for the library to be faster, run on the library GEMM.
 at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool nn,
-                const c10::optional<at::Tensor>& out) {
+                const c10::optional<at::Tensor>& out, int64_t force) {
   Range rr_("xdot.proj");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && w.dim() == 2 && x.dim() >= 1 && x.scalar_type() == w.scalar_type(),
               "xdot.proj: device tensors of one dtype, 2-D weight");
@@ -730,7 +731,7 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
                     (M - 1) * p.ldc + N <= avail_elems(c),
                 "xdot.proj: operand extents exceed their storage");
     c10::DeviceGuard guard(x.device());
-    rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, cur_stream(x));
+    rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, force ? 1 : 0, cur_stream(x));
     if (rc != -3) check_launch((hipError_t)rc, "gemm_proj");
   }
   if (rc == -3) {  // library GEMM
@@ -1218,7 +1219,7 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
-  m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None) -> Tensor");
+  m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0) -> Tensor");
   m.def("ipc_info() -> int[]");
   m.def("ipc_alloc(int nbytes, bool uncached) -> int");
   m.def("ipc_free(int ptr) -> ()");

@@ -246,9 +246,9 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
 }  // namespace xdot
 
 // Tile choice: the largest tile that still puts >= 2 workgroups on every CU of the 256
-// (NN needs BN = 128).  Returns -3 when the shape / layout is not eligible (the caller falls
-// back to the library GEMM).
-extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hipStream_t st) {
+// (NN needs BN = 128).  Returns -3 when the shape / layout is not eligible, or (force = 0) when
+// the product is large enough for the library GEMM to be faster; the caller then runs that.
+extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, int force, hipStream_t st) {
   using namespace xdot;
   if (dt != DT_BF16 && dt != DT_F16) return -3;
   if (a->M < 1 || a->K < gp::BK || a->K % gp::BK || a->N % 64 || a->lda % 8 || a->ldb % 8 || a->ldc % 4) return -3;
@@ -256,6 +256,9 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hi
   if (reinterpret_cast<uintptr_t>(a->C) & 7) return -3;
   if (nn && a->N % 128) return -3;
   auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
+  // >= 1024 tiles of 128x128 (the N=1 / N=2 products, M >= ~11000 rows): hipBLASLt is 1.05-1.3x
+  // faster there (profiles/r4_s2.md §5): decline unless forced
+  if (!force && a->N % 128 == 0 && tiles(128, 128) >= 1024) return -3;
   int bm = 64, bn = 64;
   if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) { bm = 256; bn = 128; }
   else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;

@@ -156,8 +156,9 @@ int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws, int splits
 int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);
 // projection GEMM; -3 = not eligible (16-bit, K % 64 == 0, N % 64 == 0 (NN: % 128), 16-byte
-// aligned A / B with lda, ldb % 8 == 0, 8-byte aligned C with ldc % 4 == 0)
-int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, hipStream_t st);
+// aligned A / B with lda, ldb % 8 == 0, 8-byte aligned C with ldc % 4 == 0) or, unless force,
+// large enough for the library to be faster
+int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, int force, hipStream_t st);
 // fp32 operand -> compact bf16 parts [z1][z2][3][seg][R][C] (hi, or lo where lo_mask bit p is set)
 int xdot_split3_launch(const float* src, void* dst, int64_t s1, int64_t s2, int64_t sseg, int64_t ld,
                        int nb1, int nb2, int nseg, int R, int C, int lo_mask, hipStream_t st);

@@ -36,7 +36,7 @@ def test_proj_nt(dt, M, N, K, bias):
     x = torch.randn(M, K, device=dev, dtype=dt)
     w = torch.randn(N, K, device=dev, dtype=dt) / K ** 0.5
     b = torch.randn(N, device=dev, dtype=dt) if bias else None
-    y = _ops().proj(x, w, b, False, None)
+    y = _ops().proj(x, w, b, False, None, 1)  # force: the kernel at every size
     ref = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     assert y.shape == (M, N) and y.dtype == dt
     _check(y, ref, dt)
@@ -49,7 +49,7 @@ def test_proj_nn(dt, M, Nout, Nin):
     torch.manual_seed(M + Nout)
     dy = torch.randn(M, Nout, device=dev, dtype=dt)
     w = torch.randn(Nout, Nin, device=dev, dtype=dt) / Nout ** 0.5
-    dx = _ops().proj(dy, w, None, True, None)
+    dx = _ops().proj(dy, w, None, True, None, 1)
     assert dx.shape == (M, Nin)
     _check(dx, dy.float() @ w.float(), dt)
 
@@ -63,22 +63,24 @@ def test_proj_batched_strided_and_out_view():
     packed = torch.randn(2 * 768, 768, device=dev, dtype=dt) / 28.0
     w = packed[768:]  # the values half of a [q|v] weight
     b = torch.randn(1536, device=dev, dtype=dt)[768:]
-    y = _ops().proj(x, w, b, False, None)
+    y = _ops().proj(x, w, b, False, None, 1)
     assert y.shape == (1, 3125, 768)
     ref = x.float() @ w.float().t() + b.float()
     _check(y, ref, dt)
     gbuf = torch.full((4, 1, 3125, 768), 7.0, device=dev, dtype=dt)
-    _ops().proj(x, w, b, False, gbuf[2].view(-1, 768))
+    _ops().proj(x, w, b, False, gbuf[2].view(-1, 768), 1)
     _check(gbuf[2], ref, dt)
     for r in (0, 1, 3):
         assert torch.all(gbuf[r] == 7.0)
 
 
 def test_proj_fallback_shapes_match_library():
-    """Shapes outside the kernel's envelope (K % 64, N % 64, fp32) take the library route in the
-    same op and still match the reference."""
+    """Shapes outside the kernel's envelope (K % 64, N % 64, fp32) and, unforced, the products
+    large enough for hipBLASLt to be faster take the library route in the same op and still
+    match the reference."""
     torch.manual_seed(1)
-    for dt, M, N, K in [(torch.bfloat16, 50, 96, 100), (torch.bfloat16, 50, 100, 64), (torch.float32, 64, 128, 64)]:
+    for dt, M, N, K in [(torch.bfloat16, 50, 96, 100), (torch.bfloat16, 50, 100, 64), (torch.float32, 64, 128, 64),
+                        (torch.bfloat16, 25000, 1536, 768)]:
         x = torch.randn(M, K, device=dev, dtype=dt)
         w = torch.randn(N, K, device=dev, dtype=dt) / K ** 0.5
         _check(_ops().proj(x, w, None, False, None), x.float() @ w.float().t(), dt if dt != torch.float32 else torch.float16)

@@ -49,8 +49,14 @@ def _splits(M: int, N: int, K: int) -> int:
 def _proj_ok(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> bool:
     from ..utils.env import FLAGS
 
-    return (FLAGS.proj_kernel and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype
+    return (FLAGS.proj_kernel > 0 and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype
             and (bias is None or bias.dtype == x.dtype) and _ext.use_hip(x, weight))
+
+
+def _force() -> int:
+    from ..utils.env import FLAGS
+
+    return 1 if FLAGS.proj_kernel >= 2 else 0
 
 
 def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -59,7 +65,7 @@ def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = N
     not take run on the library inside the op).  ``out``: an (M, N) row-major view to write,
     e.g. this rank's block of an all-gather buffer."""
     if _proj_ok(x, weight, bias):
-        return _ext.ops().proj(x, weight, bias, False, out)
+        return _ext.ops().proj(x, weight, bias, False, out, _force())
     if out is None:
         return F.linear(x, weight, bias)
     x2 = x.reshape(-1, x.shape[-1])
@@ -71,7 +77,7 @@ def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = N
 def proj_dx(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Input gradient ``dy · weight`` of ``F.linear`` for 2-D ``dy`` (M, N_out) -> (M, N_in)."""
     if _proj_ok(dy, weight):
-        return _ext.ops().proj(dy, weight, None, True, None)
+        return _ext.ops().proj(dy, weight, None, True, None, _force())
     return dy @ weight
 
 

@@ -11,6 +11,8 @@ over prediction and target in the backward, fills); at the N=8 rank shape it cos
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.nn.functional as F
 
@@ -60,6 +62,25 @@ def unit_grad(loss: torch.Tensor) -> torch.Tensor:
         t = _UNIT[key] = torch.ones(loss.shape, dtype=loss.dtype, device=loss.device)
         t._xdot_unit = True
     return t
+
+
+def backward(loss: torch.Tensor, grad: Optional[torch.Tensor] = None, inline: Optional[bool] = None) -> None:
+    """``loss.backward(grad)``, by default on the calling thread (``XDOT_INLINE_BACKWARD=1``).
+
+    For GPU tensors PyTorch's autograd engine runs the backward on a per-device worker thread
+    while the caller waits; the hand-off (and the GIL ping-pong for every Python backward
+    function) costs ~0.2 ms of host time per step at the N=8 rank shape, where the GPU step is
+    ~1.35 ms (profiles/r4_s2.md).  ``torch.autograd.set_multithreading_enabled(False)`` runs the
+    same graph, in the same order and on the same streams, on this thread."""
+    from ..utils.env import FLAGS
+
+    if inline is None:
+        inline = FLAGS.inline_backward
+    if not inline:
+        loss.backward(grad)
+        return
+    with torch.autograd.set_multithreading_enabled(False):
+        loss.backward(grad)
 
 
 def mse_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:

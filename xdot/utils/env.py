@@ -49,6 +49,11 @@ variable                    default   effect
 ``XDOT_WGRAD_SIDE``         0         weight gradients on side streams beside the attention
                                       backward (same GPU time, +0.1-0.4 ms host per step: off;
                                       profiles/r4_s2.md)
+``XDOT_INLINE_BACKWARD``    1         xdot.ops.loss.backward runs the backward on the calling thread
+                                      (no autograd worker-thread hand-off: -0.2 ms host per step)
+``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
+                                      (1: where it beats the library, i.e. below ~11000 rows;
+                                      2: every eligible shape; 0: library)
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
 ``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
@@ -114,7 +119,8 @@ class _Flags:
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
-        self.proj_kernel = _flag("XDOT_PROJ", default="1")
+        self.proj_kernel = _num("XDOT_PROJ", 1, int)
+        self.inline_backward = _flag("XDOT_INLINE_BACKWARD", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
         self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
