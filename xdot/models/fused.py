@@ -117,10 +117,11 @@ class AttnBlockFn(torch.autograd.Function):
         _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=side is None)
         wk_, bk_, wq_, bq_, wv_, bv_, wc_, bc_ = ctx.params
         sync = ctx.sync
-        cur = torch.cuda.current_stream(dout.device) if dout.is_cuda else None
+        # the current stream is only looked up when a side stream is in play (host cost per call)
+        cur = torch.cuda.current_stream(dout.device) if side is not None else None
         if sync is not None:  # hand the output projection's gradients to GradSync now: their
-            # all-reduce runs under the attention backward
-            sync.deliver([(wc_, dwc), (bc_, dbc)], stream=side or cur)
+            # all-reduce runs under the attention backward (stream None: the current one)
+            sync.deliver([(wc_, dwc), (bc_, dbc)], stream=side)
             dwc = dbc = None
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
         ctx.actx = None
@@ -131,7 +132,7 @@ class AttnBlockFn(torch.autograd.Function):
         _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=side is None)
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
-        qv_on = getattr(dqv, "_xdot_ready_on", None) or cur
+        qv_on = getattr(dqv, "_xdot_ready_on", None) if native_wgrad(dqv, xqv) else None  # (as linear_backward)
         dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], ng[5] or ng[7], hq and (ng[6] or ng[8]))
         n = ctx.nq
         dwq = dwv = dbq = dbv = None
@@ -141,7 +142,7 @@ class AttnBlockFn(torch.autograd.Function):
             dbq, dbv = dbqv[:n], dbqv[n:]
         if sync is not None:
             sync.deliver([(wq_, dwq), (bq_, dbq), (wv_, dwv), (bv_, dbv)], stream=qv_on)
-            sync.deliver([(wk_, dwk), (bk_, dbk)], stream=side or cur)
+            sync.deliver([(wk_, dwk), (bk_, dbk)], stream=side)
             dwq = dbq = dwv = dbv = dwk = dbk = None
         if side is not None:  # the gradients handed on are complete on this stream
             cur.wait_stream(side)
