@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--seq-len", type=int, default=25000)
+    ap.add_argument("--one-stream", action="store_true",
+                    help="(A/B) one-stream attention backward (xdot.parallel.attention.ONE_STREAM_BACKWARD)")
     ap.add_argument("--inline-backward", action="store_true",
                     help="(default now: XDOT_INLINE_BACKWARD=1) kept for old scripts")
     a = ap.parse_args()
@@ -27,8 +30,16 @@ def main():
     from xdot.utils.comm import EmulatedComm
     from xdot.utils.env import FLAGS
 
-    args = bench.parse(["--gpus", str(a.world), "--fp32-steps", "0", "--no-check"])
-    comm = EmulatedComm(a.world)
+    args = bench.parse(["--gpus", str(a.world), "--seq-len", str(a.seq_len), "--fp32-steps", "0", "--no-check"])
+    comm = EmulatedComm(a.world) if a.world > 1 else None
+    if comm is None:
+        from xdot.utils.comm import LocalComm
+
+        comm = LocalComm()
+    if a.one_stream:
+        import xdot.parallel.attention as pa
+
+        pa.ONE_STREAM_BACKWARD = True
     dev = torch.device("cuda", 0)
     inline = FLAGS.inline_backward
     bench.time_step(args, comm, dev, torch.bfloat16, 5, 5)  # warm everything (kernels, caches, allocator)

@@ -55,6 +55,9 @@ def test_thread_comm_collectives(ws):
         t = torch.tensor([float(r)])
         c.all_reduce(t, "max")
         assert t.item() == ws - 1
+        a = torch.tensor([float(r)])
+        c.all_reduce(a, "avg")
+        assert a.item() == sum(range(ws)) / ws
         b = torch.tensor([float(r + 10)])
         c.broadcast(b, src=1)
         assert b.item() == 11.0

@@ -196,3 +196,32 @@ def _fused_delivery_one_step(rank, ws):
 def test_fused_module_grad_delivery_gloo():
     run_gloo(_fused_delivery_one_step, 2)
     run_gloo(_fused_delivery_body, 2)
+
+
+def test_gradsync_native_avg_matches_sum_then_divide(monkeypatch):
+    """A communicator with a native average (RCCL ncclAvg: ``native_avg``) gets ONE avg collective
+    per bucket and no division pass; the gradients equal the sum-then-divide route (thread ranks)."""
+    from xdot.parallel import GradSync
+    from xdot.utils import comm as C
+
+    def run(native):
+        monkeypatch.setattr(C.ThreadComm, "native_avg", native, raising=False)
+
+        def body(r):
+            g = torch.Generator().manual_seed(0)  # per-thread generator (threads share the global one)
+            m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3))
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.copy_(torch.randn(p.shape, generator=g))
+            sync = GradSync(m, comm=C.get_comm(), bucket_mb=1e-5, op="avg")
+            x = torch.randn(4, 6, generator=g) * (r + 1)
+            m(x).square().sum().backward()
+            sync.wait()
+            return [p.grad.clone() for p in m.parameters()]
+
+        return C.ThreadGroup(3).run(body)
+
+    a, b = run(False), run(True)
+    for ra, rb in zip(a, b):
+        for ga, gb in zip(ra, rb):
+            torch.testing.assert_close(ga, gb, rtol=1e-6, atol=1e-7)

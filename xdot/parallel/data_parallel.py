@@ -206,12 +206,20 @@ class GradSync:
                 p.grad = torch.zeros_like(p)
         g0 = b[0].grad
         rdt = self.reduce_dtype or g0.dtype
-        if len(b) == 1 and g0.is_contiguous() and g0.dtype == rdt:
-            flat = g0  # one-tensor bucket: reduce the gradient in place (no flatten / copy back)
-        else:
-            flat = torch.cat([p.grad.reshape(-1).to(rdt) for p in b])
-        h = self.comm.all_reduce(flat, op="sum", async_op=True)
-        self._handles.append((i, flat, h))
+        # "avg" in the collective itself where the backend has it (RCCL): no division pass
+        nat = self.op == "avg" and self.comm.native_avg
+        op = "avg" if nat else "sum"
+        if all(p.grad.is_contiguous() and p.grad.dtype == rdt for p in b):
+            # the gradients reduced in place (one grouped launch for a several-tensor bucket): no
+            # flatten / copy-back passes
+            grads = [p.grad for p in b]
+            h = self.comm.all_reduce(g0, op=op, async_op=True) if len(b) == 1 else \
+                self.comm.all_reduce_multi(grads, op=op, async_op=True)
+            self._handles.append((i, grads, h, nat))
+            return
+        flat = torch.cat([p.grad.reshape(-1).to(rdt) for p in b])
+        h = self.comm.all_reduce(flat, op=op, async_op=True)
+        self._handles.append((i, flat, h, nat))
 
     @torch.no_grad()
     def wait(self, optimizer=None) -> bool:
@@ -235,15 +243,17 @@ class GradSync:
             for i in missing:  # bucket index order: the same on every rank
                 self._launch(i)
         last = len(self._handles) - 1
-        for k, (i, flat, h) in enumerate(self._handles):
+        for k, (i, flat, h, nat) in enumerate(self._handles):
             if split and k == last:  # everything reduced so far steps under the last all-reduce
-                optimizer.step(params=[p for j, _, _ in self._handles[:last] for p in self.buckets[j]])
+                optimizer.step(params=[p for j, _, _, _ in self._handles[:last] for p in self.buckets[j]])
             h.wait()
-            if self.op == "avg":
+            if isinstance(flat, list):  # reduced in place
+                if self.op == "avg" and not nat:
+                    torch._foreach_div_(flat, ws)
+                continue
+            if self.op == "avg" and not nat:
                 flat.div_(ws)
             b = self.buckets[i]
-            if len(b) == 1 and flat is b[0].grad:
-                continue
             off = 0
             for p in b:
                 n = p.numel()

@@ -72,6 +72,8 @@ class Communicator:
     # all_gather_into(out, out[rank]) (the input already in place in the output) is supported
     # without a staging copy of the own block
     inplace_gather: bool = False
+    # all_reduce(op="avg") is one native collective (RCCL ncclAvg): the caller skips its division
+    native_avg: bool = False
 
     # -- collectives ------------------------------------------------------------------
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -97,6 +99,16 @@ class Communicator:
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):
         raise NotImplementedError
+
+    def all_reduce_multi(self, ts, op: str = "sum", async_op: bool = False):
+        """``all_reduce`` of every tensor of ``ts`` in place, issued together (RCCL: one grouped
+        launch), so a bucket of several gradients needs no flatten / copy-back passes."""
+        hs = [self.all_reduce(t, op, async_op=True) for t in ts]
+        h = Handle(out=ts, post=lambda: [x.wait() for x in hs if x is not None])
+        if async_op:
+            return h
+        h.wait()
+        return None
 
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
         raise NotImplementedError
@@ -273,6 +285,7 @@ class EmulatedComm(LocalComm):
         return None
 
     inplace_gather = True
+    native_avg = True  # (the modelled all-reduce moves the same bytes for sum and avg)
 
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
@@ -364,6 +377,10 @@ class TorchDistComm(Communicator):
     def inplace_gather(self) -> bool:
         return self._backend == "nccl"  # RCCL all-gather in place: sendbuff = recvbuff + rank block
 
+    @property
+    def native_avg(self) -> bool:
+        return self._backend == "nccl" and _OPS["avg"] is not None  # gloo has no AVG
+
     def all_gather_into(self, out, inp, async_op=False):
         _check_gather(out, inp, self.world_size)
         if self._backend != "nccl" and inp.data_ptr() == out.view(self.world_size, -1)[self.rank].data_ptr():
@@ -376,6 +393,20 @@ class TorchDistComm(Communicator):
         inp = inp.contiguous()
         w = dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group, async_op=async_op)
         return Handle(w, out) if async_op else None
+
+    def all_reduce_multi(self, ts, op="sum", async_op=False):
+        if self._backend != "nccl" or len(ts) < 2 or not hasattr(dist, "_coalescing_manager") or \
+                any(self._staged(t) for t in ts):
+            return super().all_reduce_multi(ts, op, async_op)
+        # one grouped RCCL launch, every tensor reduced in place
+        with dist._coalescing_manager(group=self.group, device=ts[0].device, async_ops=True) as cm:
+            for t in ts:
+                dist.all_reduce(t, op=_OPS[op], group=self.group)
+        h = Handle(cm, ts)
+        if async_op:
+            return h
+        h.wait()
+        return None
 
     def all_gather_chunks(self, raw, inp, sizes, async_op=False):
         views = _chunk_views(raw, inp, sizes, self.world_size)
@@ -601,8 +632,12 @@ class ThreadComm(Communicator):
                 res = torch.maximum(res, p)
             elif op == "min":
                 res = torch.minimum(res, p)
+            elif op == "avg":
+                res += p
             else:
                 raise ValueError(op)
+        if op == "avg":
+            res /= len(parts)
         t.copy_(res)
         self._done(t)
         return Handle(out=t) if async_op else None

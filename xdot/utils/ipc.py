@@ -129,6 +129,10 @@ class IpcComm(Communicator):
     inplace_gather = True  # the pull kernel skips the own-block copy when inp is out[rank]
 
     @property
+    def native_avg(self) -> bool:  # all-reduce is the base communicator's
+        return self.base.native_avg
+
+    @property
     def backend(self) -> str:
         return f"ipc+{self.base.backend}"
 
@@ -219,6 +223,9 @@ class IpcComm(Communicator):
     # -- delegated ----------------------------------------------------------------------
     def all_reduce(self, t, op="sum", async_op=False):
         return self.base.all_reduce(t, op, async_op)
+
+    def all_reduce_multi(self, ts, op="sum", async_op=False):
+        return self.base.all_reduce_multi(ts, op, async_op)
 
     def broadcast(self, t, src=0, async_op=False):
         return self.base.broadcast(t, src, async_op)
