@@ -110,11 +110,13 @@ class AttnBlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         # output projection: d(o) for the attention on this stream; its weight / bias gradients
         # (only needed by the optimizer) on a second stream, under the attention backward
-        do, _, _ = linear_backward(dout, o, wc, True, False, False)
         side = _wgrad_stream(dout)
-        if side is not None:
+        if side is None:
+            do, dwc, dbc = linear_backward(dout, o, wc, True, ng[9], hc and ng[10])
+        else:
+            do, _, _ = linear_backward(dout, o, wc, True, False, False)
             dout._xdot_ready_on = _ready_on(dout, side)
-        _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=side is None)
+            _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=False)
         wk_, bk_, wq_, bq_, wv_, bv_, wc_, bc_ = ctx.params
         sync = ctx.sync
         # the current stream is only looked up when a side stream is in play (host cost per call)
@@ -126,10 +128,12 @@ class AttnBlockFn(torch.autograd.Function):
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
         ctx.actx = None
         # the row-side weight gradient also runs beside the input-gradient GEMMs that follow
-        if side is not None:
+        if side is None:
+            dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], ng[3], hk and ng[4])
+        else:
             dk._xdot_ready_on = _ready_on(dk, side)
-        dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
-        _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=side is None)
+            dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
+            _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=False)
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
         qv_on = getattr(dqv, "_xdot_ready_on", None) if native_wgrad(dqv, xqv) else None  # (as linear_backward)

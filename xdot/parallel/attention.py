@@ -525,7 +525,7 @@ class SeqParallelAttention(torch.autograd.Function):
             if one:
                 g = bufs[0]
                 dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
-                                    prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
+                                    nsplit=FLAGS.rows_split, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
             else:
                 ops = _ext.ops()
                 ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))

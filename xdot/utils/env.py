@@ -51,6 +51,8 @@ variable                    default   effect
                                       profiles/r4_s2.md)
 ``XDOT_INLINE_BACKWARD``    1         xdot.ops.loss.backward runs the backward on the calling thread
                                       (no autograd worker-thread hand-off: -0.2 ms host per step)
+``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
+                                      launcher's occupancy model; A/B knob)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
                                       (1: where it beats the library, i.e. below ~11000 rows;
                                       2: every eligible shape; 0: library)
@@ -121,6 +123,7 @@ class _Flags:
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _num("XDOT_PROJ", 1, int)
         self.inline_backward = _flag("XDOT_INLINE_BACKWARD", default="1")
+        self.rows_split = _num("XDOT_ROWS_SPLIT", 0, int)
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
         self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
