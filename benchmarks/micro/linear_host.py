@@ -96,6 +96,26 @@ def main():
         for r, (h, g) in res.items():
             print(json.dumps({"case": name, "M": m, "N": n, "K": k, "route": r, "host_us": round(h, 2),
                               "gpu_us": round(g, 2)}), flush=True)
+    wgrad_cases(args, dt, ops)
+
+
+def wgrad_cases(args, dt, ops):
+    """Weight gradients dyᵀ·x (K = rows): hipBLASLt vs the gemm3 split-K route vs
+    csrc/gemm_wgrad.hip (each including its partial reduction)."""
+    from xdot.ops.gemm import strided_gemm
+
+    for name, (K, M, N) in {"wk_rank8": (3125, 768, 768), "wqv_rank8": (3125, 1536, 768),
+                            "wk_n1": (25000, 768, 768), "wqv_n1": (25000, 1536, 768)}.items():
+        dy = torch.randn(K, M, device="cuda", dtype=dt)
+        x = torch.randn(K, N, device="cuda", dtype=dt)
+        out = torch.empty(M, N, device="cuda", dtype=dt)
+        res = {"torch_hipblaslt": measure(lambda: (dy.t() @ x), args.calls),
+               "xdot_gemm3_splitk": measure(lambda: strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N,
+                                                                 a_mc=True, b_mc=True, path=5), args.calls),
+               "xdot_wgrad": measure(lambda: ops.wgrad(dy, x, dt, 0), args.calls)}
+        for r, (h, g) in res.items():
+            print(json.dumps({"case": name, "M": M, "N": N, "K": K, "route": r, "host_us": round(h, 2),
+                              "gpu_us": round(g, 2)}), flush=True)
 
 
 def xdot_ops():

@@ -742,6 +742,37 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
   return out.has_value() ? c : c.view(oshape);
 }
 
+// Weight gradient of a Linear: dy (K, M), x (K, N) row-major 16-bit -> dyᵀ x (M, N) in out_dtype,
+// fp32 accumulation (csrc/gemm_wgrad.hip: S slabs of K -> fp32 partials -> one ordered sum).
+// splits 0: enough slabs for ~2 workgroups per CU, each >= 2 k-tiles of 64 rows.  Returns an
+// undefined tensor when the shape is not eligible (the caller takes another route).
+at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_dtype, int64_t splits) {
+  Range rr_("xdot.wgrad");
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) &&
+                  dy.scalar_type() == x.scalar_type() && dy.stride(1) == 1 && x.stride(1) == 1,
+              "xdot.wgrad: (K, M) and (K, N) row-major device tensors of one dtype");
+  const int64_t K = dy.size(0), M = dy.size(1), N = x.size(1);
+  if (K < 1 || M % 128 || N % 128 || (dy.scalar_type() != at::kBFloat16 && dy.scalar_type() != at::kHalf) ||
+      M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return at::Tensor();
+  const int64_t KT = (K + 63) / 64, tiles = (M / 128) * (N / 128);
+  int64_t S = splits > 0 ? splits : std::max<int64_t>(1, std::min<int64_t>((512 + tiles / 2) / tiles, KT / 2));
+  S = std::min<int64_t>(S, KT);
+  TORCH_CHECK((K - 1) * dy.stride(0) + M <= avail_elems(dy) && (K - 1) * x.stride(0) + N <= avail_elems(x),
+              "xdot.wgrad: operand extents exceed their storage");
+  auto part = at::empty({S, M, N}, dy.options().dtype(at::kFloat));
+  c10::DeviceGuard guard(dy.device());
+  const int rc = xdot_gemm_wgrad_launch(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)M, (int)N, (int)K,
+                                        (int)S, dy.stride(0), x.stride(0), dt_code(dy.scalar_type()), cur_stream(dy));
+  if (rc == -3) return at::Tensor();
+  check_launch((hipError_t)rc, "gemm_wgrad");
+  auto out = at::empty({M, N}, dy.options().dtype(out_dtype));
+  TORCH_CHECK(xdot_sum_partials_launch(part.data_ptr<float>(), out.data_ptr(), (int)S, M * N, dt_code(out_dtype),
+                                       cur_stream(dy)) == 0, "xdot.wgrad: out dtype");
+  check_launch(hipGetLastError(), "wgrad sum");
+  return out;
+}
+
 // fused MSE loss forward: (mean (y - t)^2 in y's dtype, dy = 2 (y - t) / n)
 std::tuple<at::Tensor, at::Tensor> mse_fwd(const at::Tensor& y, const at::Tensor& t) {
   Range rr_("xdot.mse_fwd");
@@ -1220,6 +1251,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
   m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x, ScalarType out_dtype, int splits=0) -> Tensor");
   m.def("ipc_info() -> int[]");
   m.def("ipc_alloc(int nbytes, bool uncached) -> int");
   m.def("ipc_free(int ptr) -> ()");
@@ -1266,6 +1298,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_prescale", &flash_prescale);
   m.impl("mse_fwd", &mse_fwd);
   m.impl("proj", &proj);
+  m.impl("wgrad", &wgrad);
   m.impl("flash_fwd_partial", &flash_fwd_partial);
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);

@@ -105,3 +105,35 @@ def test_linear_fn_routes_through_proj():
     _check(x.grad, xr.grad, dt)
     _check(w.grad, wr.grad, dt)
     _check(b.grad, br.grad, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K,M,N,S", [(3125, 768, 768, 0), (3125, 1536, 768, 0), (25000, 768, 768, 0), (100, 128, 256, 0),
+                                     (64, 128, 128, 0), (1, 128, 128, 0), (129, 256, 128, 3), (3125, 768, 768, 49)])
+def test_wgrad(dt, K, M, N, S):
+    """Weight-gradient kernel (csrc/gemm_wgrad.hip) dyᵀ·x vs fp32 torch: K slabs with a partial last
+    k-tile (zeros past K through the buffer descriptor), one slab per k-tile, fp32 and 16-bit
+    outputs."""
+    torch.manual_seed(K + M + N)
+    dy = torch.randn(K, M, device=dev, dtype=dt)
+    x = torch.randn(K, N, device=dev, dtype=dt)
+    ref = dy.float().t() @ x.float()
+    for odt in (dt, torch.float32):
+        got = _ops().wgrad(dy, x, odt, S)
+        assert got is not None and got.shape == (M, N) and got.dtype == odt
+        _check(got, ref, dt)
+
+
+def test_wgrad_declines_and_weight_grad_routes():
+    """Shapes the kernel does not take come back undefined; xdot.ops.linear.weight_grad then runs
+    the gemm3 / slab routes with the same result."""
+    from xdot.ops.linear import weight_grad
+
+    dt = torch.bfloat16
+    dy = torch.randn(500, 96, device=dev, dtype=dt)
+    x = torch.randn(500, 128, device=dev, dtype=dt)
+    assert _ops().wgrad(dy, x, dt, 0) is None
+    _check(weight_grad(dy, x), dy.float().t() @ x.float(), dt)
+    dy = torch.randn(3125, 768, device=dev, dtype=dt)
+    x = torch.randn(3125, 768, device=dev, dtype=dt)
+    _check(weight_grad(dy, x), dy.float().t() @ x.float(), dt)

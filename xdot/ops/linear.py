@@ -26,6 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
+from ..utils.env import FLAGS
 from .gemm import strided_gemm
 
 __all__ = ["linear", "linear_backward", "weight_grad", "LinearFn", "proj", "proj_dx"]
@@ -103,6 +104,12 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
         return (dy.to(ct).t() @ x.to(ct)).to(out_dtype)
     dy = dy.contiguous()
     x = x.contiguous()
+    if M % 128 == 0 and N % 128 == 0 and FLAGS.wgrad_kernel:
+        # csrc/gemm_wgrad.hip: 128x128 tiles x K slabs (~2 workgroups per CU), fp32 partials, one
+        # ordered sum (profiles/r4_s2.md)
+        out = _ext.ops().wgrad(dy, x, out_dtype, 0)
+        if out is not None:
+            return out
     # 256x256 kernel.  K slabs of the 128x128 kernel are faster in isolation at short K (K = 3125:
     # 36 vs 44 µs at 768²) but not inside the step (emulated N=8 rank 1.350 vs 1.343 ms):
     # profiles/r2_wgrad_route.md; the slab path serves the shapes the 256x256 kernel does not take.
