@@ -39,6 +39,16 @@ class FusedAdamW(torch.optim.Optimizer):
         self.capturable = capturable
         self._lr_dev = {}  # (group index, device) -> one-element fp32 device tensor (capturable)
 
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """``set_to_none`` (the default): drop every gradient with a plain loop (the base class
+        wraps the same work in a profiler range and per-device grouping: ~15 µs of host per
+        step at the module's 8 parameters)."""
+        if not set_to_none:
+            return super().zero_grad(set_to_none=False)
+        for group in self.param_groups:
+            for p in group["params"]:
+                p.grad = None
+
     @torch.no_grad()
     def step(self, closure=None, params=None):
         """``params``: update only these parameters (each must then be updated once per step —
