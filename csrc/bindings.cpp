@@ -744,7 +744,7 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
 
 // Weight gradient of a Linear: dy (K, M), x (K, N) row-major 16-bit -> dyᵀ x (M, N) in out_dtype,
 // fp32 accumulation (csrc/gemm_wgrad.hip: S slabs of K -> fp32 partials -> one ordered sum).
-// splits 0: enough slabs for ~2 workgroups per CU, each >= 2 k-tiles of 64 rows.  Returns an
+// splits 0: the slab count from a round / partial-traffic cost model.  Returns an
 // undefined tensor when the shape is not eligible (the caller takes another route).
 at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_dtype, int64_t splits) {
   Range rr_("xdot.wgrad");
@@ -756,8 +756,18 @@ at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_d
       M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return at::Tensor();
   const int64_t KT = (K + 63) / 64, tiles = (M / 128) * (N / 128);
-  int64_t S = splits > 0 ? splits : std::max<int64_t>(1, std::min<int64_t>((512 + tiles / 2) / tiles, KT / 2));
-  S = std::min<int64_t>(S, KT);
+  // slab count: rounds of 512 workgroup slots x (k-tiles per slab + a per-workgroup overhead of
+  // ~4 k-tiles) + the fp32 partials' write and ordered-sum read (~0.07 k-tile per tile and slab);
+  // fitted to the S sweep of benchmarks/micro/wgrad_splits.py (profiles/r4_s2.md §12)
+  int64_t S = splits;
+  if (S <= 0) {
+    double best = 1e300;
+    for (int64_t s = 1; s <= std::min<int64_t>(KT, 64); ++s) {
+      const double cost = (double)((tiles * s + 511) / 512) * ((double)KT / s + 4.0) + 0.07 * (double)(tiles * s);
+      if (cost < best) { best = cost; S = s; }
+    }
+  }
+  S = std::max<int64_t>(1, std::min<int64_t>(S, KT));
   TORCH_CHECK((K - 1) * dy.stride(0) + M <= avail_elems(dy) && (K - 1) * x.stride(0) + N <= avail_elems(x),
               "xdot.wgrad: operand extents exceed their storage");
   auto part = at::empty({S, M, N}, dy.options().dtype(at::kFloat));
