@@ -387,6 +387,18 @@ def _side_stream(dev: torch.device, priority: int = -1) -> "torch.cuda.Stream":
     return _SIDE[(i, priority)]
 
 
+_EV = {}
+
+
+def _prep_event(dev) -> "torch.cuda.Event":
+    """One reusable event per device for "δ is ready" (a stream wait captures the event's state at
+    the call, so re-recording it next step is safe): no event creation per backward."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _EV:
+        _EV[i] = torch.cuda.Event()
+    return _EV[i]
+
+
 # ----------------------------------------------------------------------------------------
 class SeqParallelAttention(torch.autograd.Function):
     """Fused seq-parallel attention on a PACKED gathered-side operand ``qv`` = [q | v]
@@ -488,7 +500,7 @@ class SeqParallelAttention(torch.autograd.Function):
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
             with torch.cuda.stream(hi):
                 delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
-                ev = torch.cuda.Event()
+                ev = _prep_event(hi.device)
                 ev.record(hi)
                 dqv = None
                 if n > 1 and len(chunks) > 1 and B == 1:
