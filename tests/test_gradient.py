@@ -16,7 +16,7 @@ DIM = 64
 
 
 def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, tol=1e-9, call="kqk", bias=False,
-                   length=LENGTH):
+                   length=LENGTH, batch=1):
     import xdot
     from xdot import DistributedDotProductAttn
     from xdot.parallel import broadcast_parameters, allreduce_gradients, gather_sequence
@@ -31,13 +31,13 @@ def _module_parity(rank, ws, heads, impl, offset, masked, dtype=torch.float64, t
 
     g = torch.Generator().manual_seed(7)
     T = length * ws
-    k_full = torch.rand(1, T, DIM, generator=g, dtype=dtype)
-    q_full = torch.rand(1, T, DIM, generator=g, dtype=dtype)
+    k_full = torch.rand(batch, T, DIM, generator=g, dtype=dtype)
+    q_full = torch.rand(batch, T, DIM, generator=g, dtype=dtype)
     if masked:
-        mask_full = torch.rand(1, T, T, generator=g) < 0.35
+        mask_full = torch.rand(batch, T, T, generator=g) < 0.35
         mask_full[..., torch.arange(T), torch.arange(T)] = False  # no fully-masked row
     else:
-        mask_full = torch.zeros(1, T, T, dtype=torch.bool)
+        mask_full = torch.zeros(batch, T, T, dtype=torch.bool)
 
     sl = slice(rank * length, (rank + 1) * length)
     k = k_full[:, sl].clone().requires_grad_(True)
@@ -114,6 +114,15 @@ def test_ring_bidirectional_odd_rows_threads(ws):
     from xdot.utils.comm import ThreadGroup
 
     ThreadGroup(ws).run(lambda r: _module_parity(r, ws, 4, "ring", None, True, length=7))
+
+
+@pytest.mark.parametrize("impl", ["ring", "flash"])
+def test_batch_two_threads(impl):
+    """B = 2: the bidirectional ring's per-lane buffers (its merged one-buffer launches are B = 1
+    only) and the flash path, masked, against the dense module."""
+    from xdot.utils.comm import ThreadGroup
+
+    ThreadGroup(3).run(lambda r: _module_parity(r, 3, 4, impl, None, True, batch=2))
 
 
 @pytest.mark.parametrize("ws", [3, 4])
