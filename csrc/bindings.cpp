@@ -688,7 +688,7 @@ at::Tensor sum_partials(const at::Tensor& part, at::ScalarType out_dtype) {
 // all-gather buffer).  Shapes / layouts the kernel does not take, and (force = 0) products
 // large enough for the library to be faster, run on the library GEMM.
 at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool nn,
-                const c10::optional<at::Tensor>& out, int64_t force) {
+                const c10::optional<at::Tensor>& out, int64_t force, double alpha) {
   Range rr_("xdot.proj");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && w.dim() == 2 && x.dim() >= 1 && x.scalar_type() == w.scalar_type(),
               "xdot.proj: device tensors of one dtype, 2-D weight");
@@ -726,6 +726,7 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
     p.lda = a.stride(0);
     p.ldb = w.stride(0);
     p.ldc = c.stride(0);
+    p.alpha = (float)alpha;
     // every address the kernel can touch lies inside the operands' storage
     TORCH_CHECK((M - 1) * p.lda + K <= avail_elems(a) && (nn ? (K - 1) * p.ldb + N : (N - 1) * p.ldb + K) <= avail_elems(w) &&
                     (M - 1) * p.ldc + N <= avail_elems(c),
@@ -734,10 +735,11 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
     rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, force ? 1 : 0, cur_stream(x));
     if (rc != -3) check_launch((hipError_t)rc, "gemm_proj");
   }
-  if (rc == -3) {  // library GEMM
+  if (rc == -3) {  // library GEMM (alpha scales the bias too: C = alpha (A op(B) + bias), one rounding)
     const at::Tensor wt = nn ? w : w.t();
-    if (has_b) at::addmm_out(c, *bias, a, wt);
-    else at::mm_out(c, a, wt);
+    if (has_b) at::addmm_out(c, *bias, a, wt, alpha, alpha);
+    else if (alpha == 1.0) at::mm_out(c, a, wt);
+    else at::addmm_out(c, c, a, wt, 0.0, alpha);
   }
   return out.has_value() ? c : c.view(oshape);
 }
@@ -1260,7 +1262,7 @@ TORCH_LIBRARY(xdot, m) {
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
-  m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0) -> Tensor");
+  m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0, float alpha=1.0) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, ScalarType out_dtype, int splits=0) -> Tensor");
   m.def("ipc_info() -> int[]");
   m.def("ipc_alloc(int nbytes, bool uncached) -> int");

@@ -2,7 +2,8 @@
 // distributed_dot_product/module.py:43-45 keys / queries / values, :75 composition), forward and
 // input gradient.
 //
-//   NT:  C[M, N] = A[M, K] · B[N, K]ᵀ (+ bias[N])   forward   y  = x · Wᵀ + b
+//   NT:  C[M, N] = α (A[M, K] · B[N, K]ᵀ (+ bias[N]))   forward   y  = x · Wᵀ + b (α: the
+//        attention's row-side pre-scale folded into the k projection, one rounding)
 //   NN:  C[M, N] = A[M, K] · B[K, N]                 backward  dx = dy · W
 //
 // A is k-contiguous (activations / output gradients, row stride lda), C row-major (ldc).  The
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
     if (m < p.M) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const f32x4 v = acc[mt][nt] + bv[nt];
+        const f32x4 v = (acc[mt][nt] + bv[nt]) * p.alpha;
         u32x2 w;
         w[0] = fa::pack2<DT>(v[0], v[1]);
         w[1] = fa::pack2<DT>(v[2], v[3]);

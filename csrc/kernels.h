@@ -123,6 +123,7 @@ struct ProjArgs {
   void* C;
   int M, N, K;
   int64_t lda, ldb, ldc;
+  float alpha;       // C = alpha * (A . op(B) + bias)
 };
 namespace ipc {
 constexpr int MAXR = 8;     // ranks of one node

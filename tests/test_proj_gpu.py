@@ -137,3 +137,19 @@ def test_wgrad_declines_and_weight_grad_routes():
     dy = torch.randn(3125, 768, device=dev, dtype=dt)
     x = torch.randn(3125, 768, device=dev, dtype=dt)
     _check(weight_grad(dy, x), dy.float().t() @ x.float(), dt)
+
+
+@pytest.mark.parametrize("M,force", [(3125, 1), (25000, 0), (100, 1)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_proj_alpha(M, force, bias):
+    """C = alpha (x Wᵀ + b) rounded once, on the kernel (force) and on the library route (the
+    fused module folds the attention's row pre-scale into the k projection this way)."""
+    dt = torch.bfloat16
+    torch.manual_seed(M)
+    x = torch.randn(M, 768, device=dev, dtype=dt)
+    w = torch.randn(768, 768, device=dev, dtype=dt) / 28.0
+    b = torch.randn(768, device=dev, dtype=dt) if bias else None
+    alpha = 0.036084391824351615 * 1.4426950408889634  # 1/sqrt(768) * log2 e
+    y = _ops().proj(x, w, b, False, None, force, alpha)
+    ref = alpha * (x.float() @ w.float().t() + (b.float() if bias else 0.0))
+    _check(y, ref, dt)

@@ -26,7 +26,9 @@ import torch
 from .. import _ext
 from ..ops.linear import linear_backward, native_wgrad, proj
 from ..utils.env import FLAGS
-from ..parallel.attention import SeqParallelAttention, gather_plan, start_gather
+from ..parallel.attention import SeqParallelAttention, gather_plan, prescale_wanted, start_gather
+
+_LOG2E = 1.4426950408889634  # as the kernels' scale * log2 e (csrc/flash_common.h, csrc/reduce.hip)
 
 __all__ = ["AttnBlockFn"]
 
@@ -89,9 +91,12 @@ class AttnBlockFn(torch.autograd.Function):
         else:
             qv = proj(xqv, wqv, bqv)
         pending = start_gather(qv, comm, chunks=chunk_plan, out=gbuf)  # in flight under the row-side GEMM
-        k = proj(xk, wk, bk)
+        # the row side's pre-scale (scale * log2 e) folded into the k projection: one rounding, no
+        # separate pass (the attention backward's dk is w.r.t. the unscaled k either way)
+        pre = xk.shape[-1] == wk.shape[1] and prescale_wanted(qv[..., :wk.shape[0]], qv, H)
+        k = proj(xk, wk, bk, alpha=scale * _LOG2E if pre else 1.0)
         actx = _Ctx()
-        o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending)
+        o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending, pre)  # k_prescaled
         out = proj(o, wc, bc)
         ctx.actx = actx
         ctx.sync = sync

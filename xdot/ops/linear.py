@@ -61,24 +61,26 @@ def _force() -> int:
 
 
 def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
-         out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear(x, weight, bias)`` on the projection GEMM (16-bit GPU tensors; shapes it does
-    not take run on the library inside the op).  ``out``: an (M, N) row-major view to write,
-    e.g. this rank's block of an all-gather buffer."""
+         out: Optional[torch.Tensor] = None, alpha: float = 1.0) -> torch.Tensor:
+    """``alpha * F.linear(x, weight, bias)`` on the projection GEMM (16-bit GPU tensors; shapes it
+    does not take run on the library inside the op), rounded once.  ``out``: an (M, N) row-major
+    view to write, e.g. this rank's block of an all-gather buffer."""
     if _proj_ok(x, weight, bias):
-        return _ext.ops().proj(x, weight, bias, False, out, _force())
+        return _ext.ops().proj(x, weight, bias, False, out, _force(), float(alpha))
     if out is None:
-        return F.linear(x, weight, bias)
+        y = F.linear(x, weight, bias)
+        return y if alpha == 1.0 else y.mul_(alpha)
     x2 = x.reshape(-1, x.shape[-1])
     if bias is None:
-        return torch.mm(x2, weight.t(), out=out)
-    return torch.addmm(bias, x2, weight.t(), out=out)
+        torch.mm(x2, weight.t(), out=out)
+        return out if alpha == 1.0 else out.mul_(alpha)
+    return torch.addmm(bias, x2, weight.t(), beta=alpha, alpha=alpha, out=out)
 
 
 def proj_dx(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Input gradient ``dy · weight`` of ``F.linear`` for 2-D ``dy`` (M, N_out) -> (M, N_in)."""
     if _proj_ok(dy, weight):
-        return _ext.ops().proj(dy, weight, None, True, None, _force())
+        return _ext.ops().proj(dy, weight, None, True, None, _force(), 1.0)
     return dy @ weight
 
 

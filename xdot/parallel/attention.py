@@ -399,6 +399,13 @@ def _prep_event(dev) -> "torch.cuda.Event":
     return _EV[i]
 
 
+def prescale_wanted(k_like: Tensor, qv_like: Tensor, H: int) -> bool:
+    """The HIP path will run on pre-scaled rows for a row side shaped / typed like ``k_like``
+    (the condition :meth:`SeqParallelAttention.forward` applies)."""
+    return (_hip_ok(k_like, qv_like, H) and FLAGS.prescale and k_like.numel() % 8 == 0
+            and k_like.dtype != torch.float32)
+
+
 # ----------------------------------------------------------------------------------------
 class SeqParallelAttention(torch.autograd.Function):
     """Fused seq-parallel attention on a PACKED gathered-side operand ``qv`` = [q | v]
@@ -408,7 +415,9 @@ class SeqParallelAttention(torch.autograd.Function):
 
     @staticmethod
     @_ext.pinned
-    def forward(ctx, k, qv, mask, H, scale, comm, pending=None):
+    def forward(ctx, k, qv, mask, H, scale, comm, pending=None, k_prescaled=False):
+        """``k_prescaled``: ``k`` already holds ``rows * scale * log2 e`` (:func:`prescale_wanted`;
+        the fused module folds it into the k projection's epilogue)."""
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
         B, R = k.shape[0], k.shape[1]
@@ -428,7 +437,7 @@ class SeqParallelAttention(torch.autograd.Function):
             # forward and both backward kernels read this same buffer and seed their score
             # accumulators instead of scaling every score (saved in place of k for backward)
             prescaled = FLAGS.prescale and (k.numel() % 8 == 0) and k.dtype != torch.float32
-            if prescaled:
+            if prescaled and not k_prescaled:
                 k = flash.prescale(k, scale)
             if isinstance(mask, flash.PendingMask):
                 if len(chunks) == 1:
