@@ -67,6 +67,9 @@ def main():
         "k_fwd": ("nt", R, D, D),
         "qv_dgrad": ("nn", R, 2 * D, D),
         "k_dgrad": ("nn", R, D, D),
+        "qv_fwd_n4": ("nt", 2 * R, D, 2 * D),
+        "qv_dgrad_n4": ("nn", 2 * R, 2 * D, D),
+        "qv_fwd_n2": ("nt", 4 * R, D, 2 * D),
         "qv_fwd_n1": ("nt", 8 * R, D, 2 * D),
         "qv_dgrad_n1": ("nn", 8 * R, 2 * D, D),
     }
