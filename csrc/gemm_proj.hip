@@ -257,9 +257,10 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, in
   if (reinterpret_cast<uintptr_t>(a->C) & 7) return -3;
   if (nn && a->N % 128) return -3;
   auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
-  // >= 1024 tiles of 128x128 (the N=1 / N=2 products, M >= ~11000 rows): hipBLASLt is 1.05-1.3x
-  // faster there (profiles/r4_s2.md §5): decline unless forced
-  if (!force && a->N % 128 == 0 && tiles(128, 128) >= 1024) return -3;
+  // >= 16384 rows (the N=1 products, 25000 rows): hipBLASLt is 1.1-1.3x faster there; at the
+  // 12500 / 6250 / 3125 rows of N = 2 / 4 / 8 this kernel is 0.84-1.0x its time (profiles/r4_s2.md
+  // §5): decline unless forced
+  if (!force && a->M >= 16384) return -3;
   int bm = 64, bn = 64;
   if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) { bm = 256; bn = 128; }
   else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;

@@ -55,7 +55,7 @@ variable                    default   effect
 ``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
                                       launcher's occupancy model; A/B knob)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
-                                      (1: where it beats the library, i.e. below ~11000 rows;
+                                      (1: where it beats the library, i.e. below 16384 rows;
                                       2: every eligible shape; 0: library)
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
