@@ -746,17 +746,21 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
 
 // Weight gradient of a Linear: dy (K, M), x (K, N) row-major 16-bit -> dyᵀ x (M, N) in out_dtype,
 // fp32 accumulation (csrc/gemm_wgrad.hip: S slabs of K -> fp32 partials -> one ordered sum).
-// splits 0: the slab count from a round / partial-traffic cost model.  Returns an
-// undefined tensor when the shape is not eligible (the caller takes another route).
-at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_dtype, int64_t splits) {
-  Range rr_("xdot.wgrad");
+// splits 0: the slab count from a round / partial-traffic cost model.  Returns an undefined tensor
+// when the shape is not eligible (the caller takes another route).
+struct WgradProb {
+  at::Tensor dy, x, part;
+  int64_t K, M, N, S;
+};
+
+bool wgrad_prob(const at::Tensor& dy, const at::Tensor& x, int64_t splits, WgradProb& q) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) &&
                   dy.scalar_type() == x.scalar_type() && dy.stride(1) == 1 && x.stride(1) == 1,
               "xdot.wgrad: (K, M) and (K, N) row-major device tensors of one dtype");
   const int64_t K = dy.size(0), M = dy.size(1), N = x.size(1);
   if (K < 1 || M % 128 || N % 128 || (dy.scalar_type() != at::kBFloat16 && dy.scalar_type() != at::kHalf) ||
       M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
-    return at::Tensor();
+    return false;
   const int64_t KT = (K + 63) / 64, tiles = (M / 128) * (N / 128);
   // slab count: rounds of 512 workgroup slots x (k-tiles per slab + a per-workgroup overhead of
   // ~4 k-tiles) + the fp32 partials' write and ordered-sum read (~0.07 k-tile per tile and slab);
@@ -772,17 +776,56 @@ at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_d
   S = std::max<int64_t>(1, std::min<int64_t>(S, KT));
   TORCH_CHECK((K - 1) * dy.stride(0) + M <= avail_elems(dy) && (K - 1) * x.stride(0) + N <= avail_elems(x),
               "xdot.wgrad: operand extents exceed their storage");
-  auto part = at::empty({S, M, N}, dy.options().dtype(at::kFloat));
-  c10::DeviceGuard guard(dy.device());
-  const int rc = xdot_gemm_wgrad_launch(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)M, (int)N, (int)K,
-                                        (int)S, dy.stride(0), x.stride(0), dt_code(dy.scalar_type()), cur_stream(dy));
-  if (rc == -3) return at::Tensor();
+  q = WgradProb{dy, x, at::empty({S, M, N}, dy.options().dtype(at::kFloat)), K, M, N, S};
+  return true;
+}
+
+// launch 1 or 2 products in one kernel, then one ordered sum per product; empty when not eligible
+std::vector<at::Tensor> wgrad_run(std::vector<WgradProb>& qs, at::ScalarType out_dtype) {
+  const int np = (int)qs.size();
+  const void* A[2];
+  const void* B[2];
+  float* part[2];
+  int M[2], N[2], K[2], S[2];
+  int64_t lda[2], ldb[2];
+  for (int i = 0; i < np; ++i) {
+    A[i] = qs[i].dy.data_ptr(); B[i] = qs[i].x.data_ptr(); part[i] = qs[i].part.data_ptr<float>();
+    M[i] = (int)qs[i].M; N[i] = (int)qs[i].N; K[i] = (int)qs[i].K; S[i] = (int)qs[i].S;
+    lda[i] = qs[i].dy.stride(0); ldb[i] = qs[i].x.stride(0);
+  }
+  const at::Tensor& d0 = qs[0].dy;
+  c10::DeviceGuard guard(d0.device());
+  const int rc = xdot_gemm_wgrad_launch(np, A, B, part, M, N, K, S, lda, ldb, dt_code(d0.scalar_type()), cur_stream(d0));
+  if (rc == -3) return {};
   check_launch((hipError_t)rc, "gemm_wgrad");
-  auto out = at::empty({M, N}, dy.options().dtype(out_dtype));
-  TORCH_CHECK(xdot_sum_partials_launch(part.data_ptr<float>(), out.data_ptr(), (int)S, M * N, dt_code(out_dtype),
-                                       cur_stream(dy)) == 0, "xdot.wgrad: out dtype");
-  check_launch(hipGetLastError(), "wgrad sum");
-  return out;
+  std::vector<at::Tensor> outs;
+  for (int i = 0; i < np; ++i) {
+    auto out = at::empty({qs[i].M, qs[i].N}, d0.options().dtype(out_dtype));
+    TORCH_CHECK(xdot_sum_partials_launch(part[i], out.data_ptr(), S[i], qs[i].M * qs[i].N, dt_code(out_dtype),
+                                         cur_stream(d0)) == 0, "xdot.wgrad: out dtype");
+    check_launch(hipGetLastError(), "wgrad sum");
+    outs.push_back(out);
+  }
+  return outs;
+}
+
+at::Tensor wgrad(const at::Tensor& dy, const at::Tensor& x, at::ScalarType out_dtype, int64_t splits) {
+  Range rr_("xdot.wgrad");
+  std::vector<WgradProb> qs(1);
+  if (!wgrad_prob(dy, x, splits, qs[0])) return at::Tensor();
+  auto outs = wgrad_run(qs, out_dtype);
+  return outs.empty() ? at::Tensor() : outs[0];
+}
+
+// two weight gradients in ONE launch (the fused backward's dWk and dW[q|v]); [] when either
+// shape is not eligible
+std::vector<at::Tensor> wgrad2(const at::Tensor& dy0, const at::Tensor& x0, const at::Tensor& dy1,
+                               const at::Tensor& x1, at::ScalarType out_dtype) {
+  Range rr_("xdot.wgrad2");
+  TORCH_CHECK(dy0.scalar_type() == dy1.scalar_type() && dy0.device() == dy1.device(), "xdot.wgrad2: dtype / device");
+  std::vector<WgradProb> qs(2);
+  if (!wgrad_prob(dy0, x0, 0, qs[0]) || !wgrad_prob(dy1, x1, 0, qs[1])) return {};
+  return wgrad_run(qs, out_dtype);
 }
 
 // fused MSE loss forward: (mean (y - t)^2 in y's dtype, dy = 2 (y - t) / n)
@@ -1264,6 +1307,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
   m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0, float alpha=1.0) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, ScalarType out_dtype, int splits=0) -> Tensor");
+  m.def("wgrad2(Tensor dy0, Tensor x0, Tensor dy1, Tensor x1, ScalarType out_dtype) -> Tensor[]");
   m.def("ipc_info() -> int[]");
   m.def("ipc_alloc(int nbytes, bool uncached) -> int");
   m.def("ipc_free(int ptr) -> ()");
@@ -1311,6 +1355,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("mse_fwd", &mse_fwd);
   m.impl("proj", &proj);
   m.impl("wgrad", &wgrad);
+  m.impl("wgrad2", &wgrad2);
   m.impl("flash_fwd_partial", &flash_fwd_partial);
   m.impl("flash_fwd_combine", &flash_fwd_combine);
   m.impl("flash_bwd_rows_partial", &flash_bwd_rows_partial);

@@ -16,6 +16,8 @@
 //   * v_mfma_f32_16x16x32 on the Cᵀ tile (each lane ends with 4 consecutive output columns):
 //     16-byte fp32 stores of the partial.
 // Eligibility: 16-bit, M % 128 == 0, N % 128 == 0, lda / ldb % 8 == 0, 16-byte aligned bases.
+// One launch may carry two independent products (dWk and dW[q|v], both due at the end of the
+// fused backward): their blocks share the GPU instead of running one after the other.
 #include "flash_common.h"
 
 namespace xdot {
@@ -54,27 +56,49 @@ __device__ __forceinline__ void bdma4(i32x4 rs, const uint32_t* o, uint32_t lds)
                : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(lds), "s"(rs) : "memory", "scc");
 }
 
-struct Args {
+struct Prob {
   const void* A;  // (K, M) row-major, row stride lda
   const void* B;  // (K, N) row-major, row stride ldb
   float* part;    // (S, M, N) fp32
   int M, N, K, S;
   int64_t lda, ldb;
 };
+// one or two independent products in one launch (the module's dWk and dW[q|v] at the end of the
+// backward: each alone fills only part of the GPU); problem 1's blocks start at wg1 (a multiple of
+// 8, so the XCD remap of either problem sees its own blocks in dispatch order)
+struct Args {
+  Prob q0, q1;
+  int np, wg1;
+};
 
 }  // namespace gw
 
 template <int DT>
-__global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(gw::Args p) {
+__global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(gw::Args pa) {
   using namespace gw;
   using fa::smem;
   using fa::lds_addr;
+  // this block's problem (wave-uniform selects: no dynamic indexing of the kernel arguments)
+  const int bx = blockIdx.x;
+  const bool q1 = pa.np > 1 && bx >= pa.wg1;
+  Prob p;
+  p.A = q1 ? pa.q1.A : pa.q0.A;
+  p.B = q1 ? pa.q1.B : pa.q0.B;
+  p.part = q1 ? pa.q1.part : pa.q0.part;
+  p.M = q1 ? pa.q1.M : pa.q0.M;
+  p.N = q1 ? pa.q1.N : pa.q0.N;
+  p.K = q1 ? pa.q1.K : pa.q0.K;
+  p.S = q1 ? pa.q1.S : pa.q0.S;
+  p.lda = q1 ? pa.q1.lda : pa.q0.lda;
+  p.ldb = q1 ? pa.q1.ldb : pa.q0.ldb;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4;
   const int tiles_n = p.N / BN, tiles = (p.M / BM) * tiles_n;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // slab-major: one slab's tiles share an XCD
+  const int span = q1 ? (int)gridDim.x - pa.wg1 : (pa.np > 1 ? pa.wg1 : (int)gridDim.x);
+  const int lin = xcd_remap(q1 ? bx - pa.wg1 : bx, span);  // slab-major: one slab's tiles share an XCD
+  if (lin >= tiles * p.S) return;  // problem 0's padding to a multiple of 8 blocks (before any barrier)
   const int s = lin / tiles, t = lin % tiles;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int KT = (p.K + BK - 1) / BK;
@@ -170,20 +194,43 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(gw::Args p) {
 
 }  // namespace xdot
 
-// part must hold S * M * N fp32; returns -3 when the shape / layout is not eligible
-extern "C" int xdot_gemm_wgrad_launch(const void* A, const void* B, float* part, int M, int N, int K, int S,
-                                      int64_t lda, int64_t ldb, int dt, hipStream_t st) {
+namespace {
+bool wgrad_ok(const xdot::gw::Prob& q) {
+  using namespace xdot;
+  if (q.M % gw::BM || q.N % gw::BN || q.K < 1 || q.S < 1 || q.lda % 8 || q.ldb % 8) return false;
+  if ((reinterpret_cast<uintptr_t>(q.A) | reinterpret_cast<uintptr_t>(q.B)) & 15) return false;
+  const int KT = (q.K + gw::BK - 1) / gw::BK;
+  if (q.S > KT) return false;
+  // every slab's descriptor spans at most 2^32 - 1 bytes
+  const int64_t ld = q.lda > q.ldb ? q.lda : q.ldb;
+  return (int64_t)((KT + q.S - 1) / q.S) * gw::BK * 2 * ld < (int64_t)0xFFFFFFFF;
+}
+}  // namespace
+
+// np (1 or 2) products {A, B, part, M, N, K, S, lda, ldb} in one launch; each part must hold
+// S * M * N fp32; returns -3 when a shape / layout is not eligible
+extern "C" int xdot_gemm_wgrad_launch(int np, const void* const* A, const void* const* B, float* const* part,
+                                      const int* M, const int* N, const int* K, const int* S, const int64_t* lda,
+                                      const int64_t* ldb, int dt, hipStream_t st) {
   using namespace xdot;
   if (dt != DT_BF16 && dt != DT_F16) return -3;
-  if (M % gw::BM || N % gw::BN || K < 1 || S < 1 || lda % 8 || ldb % 8) return -3;
-  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -3;
-  const int KT = (K + gw::BK - 1) / gw::BK;
-  if (S > KT) return -3;
-  // every slab's descriptor spans at most 2^32 - 1 bytes
-  const int64_t ld = lda > ldb ? lda : ldb;
-  if ((int64_t)((KT + S - 1) / S) * gw::BK * 2 * ld >= (int64_t)0xFFFFFFFF) return -3;
-  gw::Args a{A, B, part, M, N, K, S, lda, ldb};
-  const int64_t grid = (int64_t)(M / gw::BM) * (N / gw::BN) * S;
+  if (np < 1 || np > 2) return -3;
+  gw::Args a{};
+  gw::Prob* qs[2] = {&a.q0, &a.q1};
+  int64_t grid = 0;
+  for (int i = 0; i < np; ++i) {
+    *qs[i] = gw::Prob{A[i], B[i], part[i], M[i], N[i], K[i], S[i], lda[i], ldb[i]};
+    if (!wgrad_ok(*qs[i])) return -3;
+    const int64_t blocks = (int64_t)(M[i] / gw::BM) * (N[i] / gw::BN) * S[i];
+    if (i == 0 && np > 1) {
+      a.wg1 = (int)((blocks + 7) / 8 * 8);
+      grid = a.wg1;
+    } else {
+      grid += blocks;
+    }
+  }
+  a.np = np;
+  if (grid > 0x7FFFFFFF) return -3;
   if (dt == DT_BF16) hipLaunchKernelGGL(gemm_wgrad_kernel<DT_BF16>, dim3((unsigned)grid), dim3(gw::NTH), gw::LDS, st, a);
   else hipLaunchKernelGGL(gemm_wgrad_kernel<DT_F16>, dim3((unsigned)grid), dim3(gw::NTH), gw::LDS, st, a);
   return (int)hipGetLastError();

@@ -160,10 +160,12 @@ int xdot_gemm3_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_ou
 // aligned A / B with lda, ldb % 8 == 0, 8-byte aligned C with ldc % 4 == 0) or, unless force,
 // large enough for the library to be faster
 int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, int force, hipStream_t st);
-// weight gradient dW = Aᵀ B (csrc/gemm_wgrad.hip): A (K, M), B (K, N) row-major 16-bit, S slabs of K
-// -> fp32 partials part (S, M, N); -3 = not eligible (M, N % 128, lda / ldb % 8, 16-byte bases)
-int xdot_gemm_wgrad_launch(const void* A, const void* B, float* part, int M, int N, int K, int S, int64_t lda,
-                           int64_t ldb, int dt, hipStream_t st);
+// weight gradients dW_i = A_iᵀ B_i (csrc/gemm_wgrad.hip), np = 1 or 2 products in one launch: A (K, M),
+// B (K, N) row-major 16-bit, S slabs of K -> fp32 partials part (S, M, N); -3 = not eligible
+// (M, N % 128, lda / ldb % 8, 16-byte bases)
+int xdot_gemm_wgrad_launch(int np, const void* const* A, const void* const* B, float* const* part, const int* M,
+                           const int* N, const int* K, const int* S, const int64_t* lda, const int64_t* ldb, int dt,
+                           hipStream_t st);
 // fp32 operand -> compact bf16 parts [z1][z2][3][seg][R][C] (hi, or lo where lo_mask bit p is set)
 int xdot_split3_launch(const float* src, void* dst, int64_t s1, int64_t s2, int64_t sseg, int64_t ld,
                        int nb1, int nb2, int nseg, int R, int C, int lo_mask, hipStream_t st);

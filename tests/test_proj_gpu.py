@@ -153,3 +153,23 @@ def test_proj_alpha(M, force, bias):
     y = _ops().proj(x, w, b, False, None, force, alpha)
     ref = alpha * (x.float() @ w.float().t() + (b.float() if bias else 0.0))
     _check(y, ref, dt)
+
+
+@pytest.mark.parametrize("K", [3125, 25000, 100])
+def test_wgrad_pair_one_launch(K):
+    """Two weight gradients in one launch (the fused backward's dWk and dW[q|v]) equal the
+    separate products (bitwise: same slabs, same ordered sums)."""
+    from xdot.ops.linear import weight_grad_pair
+
+    dt = torch.bfloat16
+    torch.manual_seed(K)
+    x = torch.randn(K, 768, device=dev, dtype=dt)
+    dk = torch.randn(K, 768, device=dev, dtype=dt)
+    dqv = torch.randn(K, 1536, device=dev, dtype=dt)
+    outs = _ops().wgrad2(dk, x, dqv, x, dt)
+    assert len(outs) == 2
+    assert torch.equal(outs[0], _ops().wgrad(dk, x, dt, 0)) and torch.equal(outs[1], _ops().wgrad(dqv, x, dt, 0))
+    _check(outs[1], dqv.float().t() @ x.float(), dt)
+    a, b = weight_grad_pair(dk.view(1, K, 768), x.view(1, K, 768), dqv.view(1, K, 1536), x.view(1, K, 768))
+    assert torch.equal(a, outs[0]) and torch.equal(b, outs[1])
+    assert _ops().wgrad2(dk[:, :96], x, dqv, x, dt) == []  # not eligible: the caller falls back

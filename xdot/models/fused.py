@@ -24,7 +24,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from ..ops.linear import linear_backward, native_wgrad, proj
+from ..ops.linear import linear_backward, native_wgrad, proj, weight_grad_pair
 from ..utils.env import FLAGS
 from ..parallel.attention import SeqParallelAttention, gather_plan, prescale_wanted, start_gather
 
@@ -133,16 +133,23 @@ class AttnBlockFn(torch.autograd.Function):
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
         ctx.actx = None
         # the row-side weight gradient also runs beside the input-gradient GEMMs that follow
-        if side is None:
-            dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], ng[3], hk and ng[4])
-        else:
-            dk._xdot_ready_on = _ready_on(dk, side)
-            dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
-            _, dwk, dbk = linear_backward(dk, xk, wk, False, ng[3], hk and ng[4], join=False)
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
         qv_on = getattr(dqv, "_xdot_ready_on", None) if native_wgrad(dqv, xqv) else None  # (as linear_backward)
-        dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], ng[5] or ng[7], hq and (ng[6] or ng[8]))
+        need_wk, need_wqv = ng[3], ng[5] or ng[7]
+        if side is None and qv_on is None and need_wk and need_wqv:
+            # one stream: dWk and dW[q|v] in ONE launch (weight_grad_pair)
+            dxk, _, dbk = linear_backward(dk, xk, wk, ng[0], False, hk and ng[4])
+            dxqv, _, dbqv = linear_backward(dqv, xqv, wqv, ng[1], False, hq and (ng[6] or ng[8]))
+            dwk, dwqv = weight_grad_pair(dk, xk, dqv, xqv, wk.dtype)
+        else:
+            if side is None:
+                dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], need_wk, hk and ng[4])
+            else:
+                dk._xdot_ready_on = _ready_on(dk, side)
+                dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
+                _, dwk, dbk = linear_backward(dk, xk, wk, False, need_wk, hk and ng[4], join=False)
+            dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], need_wqv, hq and (ng[6] or ng[8]))
         n = ctx.nq
         dwq = dwv = dbq = dbv = None
         if dwqv is not None:

@@ -29,7 +29,7 @@ from .. import _ext
 from ..utils.env import FLAGS
 from .gemm import strided_gemm
 
-__all__ = ["linear", "linear_backward", "weight_grad", "LinearFn", "proj", "proj_dx"]
+__all__ = ["linear", "linear_backward", "weight_grad", "weight_grad_pair", "LinearFn", "proj", "proj_dx"]
 
 _SLOTS = 512       # 2 workgroups per CU x 256 CUs
 _MIN_SLAB = 256    # rows of K per split
@@ -134,6 +134,22 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
     if (M * N) % 4 == 0:
         return _ext.ops().sum_partials(part, out_dtype)
     return part.sum(0).to(out_dtype)
+
+
+def weight_grad_pair(dy0: torch.Tensor, x0: torch.Tensor, dy1: torch.Tensor, x1: torch.Tensor,
+                     out_dtype: Optional[torch.dtype] = None):
+    """``(dy0ᵀ·x0, dy1ᵀ·x1)``: both products in ONE launch of csrc/gemm_wgrad.hip where it takes
+    them (their workgroups share the GPU instead of two under-filled launches back to back), else
+    two :func:`weight_grad` calls."""
+    dy0, x0 = dy0.reshape(-1, dy0.shape[-1]), x0.reshape(-1, x0.shape[-1])
+    dy1, x1 = dy1.reshape(-1, dy1.shape[-1]), x1.reshape(-1, x1.shape[-1])
+    out_dtype = out_dtype or dy0.dtype
+    if (FLAGS.wgrad_kernel and native_wgrad(dy0, x0) and native_wgrad(dy1, x1) and dy0.dtype == dy1.dtype
+            and all(t.shape[1] % 128 == 0 for t in (dy0, x0, dy1, x1))):
+        outs = _ext.ops().wgrad2(dy0.contiguous(), x0.contiguous(), dy1.contiguous(), x1.contiguous(), out_dtype)
+        if len(outs) == 2:
+            return outs[0], outs[1]
+    return weight_grad(dy0, x0, out_dtype), weight_grad(dy1, x1, out_dtype)
 
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, need_dx: bool, need_dw: bool,
