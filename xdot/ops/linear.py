@@ -144,7 +144,8 @@ def weight_grad_pair(dy0: torch.Tensor, x0: torch.Tensor, dy1: torch.Tensor, x1:
     dy0, x0 = dy0.reshape(-1, dy0.shape[-1]), x0.reshape(-1, x0.shape[-1])
     dy1, x1 = dy1.reshape(-1, dy1.shape[-1]), x1.reshape(-1, x1.shape[-1])
     out_dtype = out_dtype or dy0.dtype
-    if (FLAGS.wgrad_kernel and native_wgrad(dy0, x0) and native_wgrad(dy1, x1) and dy0.dtype == dy1.dtype
+    if (FLAGS.wgrad_kernel and FLAGS.wgrad_pair and native_wgrad(dy0, x0) and native_wgrad(dy1, x1)
+            and dy0.dtype == dy1.dtype
             and all(t.shape[1] % 128 == 0 for t in (dy0, x0, dy1, x1))):
         outs = _ext.ops().wgrad2(dy0.contiguous(), x0.contiguous(), dy1.contiguous(), x1.contiguous(), out_dtype)
         if len(outs) == 2:

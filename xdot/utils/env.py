@@ -52,6 +52,7 @@ variable                    default   effect
 ``XDOT_INLINE_BACKWARD``    1         xdot.ops.loss.backward runs the backward on the calling thread
                                       (no autograd worker-thread hand-off: -0.2 ms host per step)
 ``XDOT_WGRAD``              1         Linear weight gradients on csrc/gemm_wgrad.hip (0: gemm3 split-K)
+``XDOT_WGRAD_PAIR``         1         the fused backward's dWk and dW[q|v] in one launch (A/B knob)
 ``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
                                       launcher's occupancy model; A/B knob)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
@@ -126,6 +127,7 @@ class _Flags:
         self.inline_backward = _flag("XDOT_INLINE_BACKWARD", default="1")
         self.rows_split = _num("XDOT_ROWS_SPLIT", 0, int)
         self.wgrad_kernel = _flag("XDOT_WGRAD", default="1")
+        self.wgrad_pair = _flag("XDOT_WGRAD_PAIR", default="1")
         self.ring_overlap = _str("XDOT_RING_OVERLAP", "auto")
         self.ring_bidir = _flag("XDOT_RING_BIDIR", default="1")
         self.hipcc_flags = os.environ.get("XDOT_HIPCC_FLAGS")
