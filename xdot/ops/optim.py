@@ -27,6 +27,8 @@ import torch
 
 from .. import _ext
 
+from torch.optim import optimizer as _optim_mod
+
 __all__ = ["FusedAdamW"]
 
 
@@ -49,11 +51,29 @@ class FusedAdamW(torch.optim.Optimizer):
             for p in group["params"]:
                 p.grad = None
 
-    @torch.no_grad()
     def step(self, closure=None, params=None):
         """``params``: update only these parameters (each must then be updated once per step —
         :meth:`xdot.parallel.GradSync.wait` with ``optimizer=`` splits a step this way so the
-        early buckets' update overlaps the last gradient all-reduce).  Not with ``capturable``."""
+        early buckets' update overlaps the last gradient all-reduce).  Not with ``capturable``.
+
+        torch wraps every optimizer's ``step`` in a profiler range plus the step-hook loops
+        (``Optimizer.profile_hook_step``): ~35 µs of host per call, twice per training step when
+        the step is split around the last all-reduce.  This class opts out of that wrapper
+        (``step.hooked`` below) and takes torch's wrapped path only when something would observe
+        it: a registered step hook (per optimizer or global) or an active autograd profiler."""
+        if (self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks or _optim_mod._global_optimizer_pre_hooks
+                or _optim_mod._global_optimizer_post_hooks or torch.autograd._profiler_enabled()):
+            return _hooked_step(self, closure, params)
+        prev = torch.is_grad_enabled()
+        torch._C._set_grad_enabled(False)
+        try:
+            return self._step_impl(closure, params)
+        finally:
+            torch._C._set_grad_enabled(prev)
+
+    step.hooked = True  # torch.optim.Optimizer._patch_step_function: leave this step unwrapped
+
+    def _step_impl(self, closure=None, params=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -145,3 +165,14 @@ class FusedAdamW(torch.optim.Optimizer):
         pf = p.float().mul_(1 - group["lr"] * group["weight_decay"])
         pf.addcdiv_(m, (v.sqrt() / bc2 ** 0.5).add_(group["eps"]), value=-group["lr"] / bc1)
         p.copy_(pf)
+
+
+@torch.no_grad()
+def _unwrapped_step(self, closure=None, params=None):
+    return self._step_impl(closure, params)
+
+
+# torch's own wrapper (profiler range + pre/post step hooks) around the same update, for the
+# calls that something observes
+_hooked_step = torch.optim.Optimizer.profile_hook_step(_unwrapped_step)
+
