@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC counters of the flash kernels at HEAD (T = R = 25000, H = 8, D = 96, bf16): one rocprofv3
 # pass per counter group (block limits respected: <= 8 SQ, <= 4 TCC, <= 2 GRBM per pass), no
-# tracing domains besides --kernel-trace; a failing pass ends the script.
+# tracing domains besides --kernel-trace; a failing pass ends the script.  PMC_SCRIPT / PMC_ARGS
+# profile another benchmark (e.g. benchmarks/micro/linear_host.py for the projection kernels).
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-pmchead}
 mkdir -p $OUT
@@ -13,6 +14,6 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY 
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp -d $OUT/g$i -o pmc --output-format csv \
-    -- python3 $GRAFT_REPO_ROOT/benchmarks/bench_flash.py --iters 3 $FLASH_ARGS > $OUT/g$i.log 2>&1 || { echo "group $i failed rc=$?" >> $OUT/errors.log; exit 1; }
+    -- python3 $GRAFT_REPO_ROOT/${PMC_SCRIPT:-benchmarks/bench_flash.py} ${PMC_ARGS:---iters 3} $FLASH_ARGS > $OUT/g$i.log 2>&1 || { echo "group $i failed rc=$?" >> $OUT/errors.log; exit 1; }
 done
 echo pmc-ok

@@ -6,12 +6,17 @@ import glob
 import sys
 
 d = sys.argv[1]
+# optional second argument: comma-separated kernel-name substrings to keep (default: flash kernels)
+keep = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(d + "/g*/pmc_counter_collection.csv")):
     per = collections.defaultdict(float)  # (kernel, dispatch, counter) -> summed value
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if not any(x in k for x in ("flash_", "fa3::", "fa32::")) or (
+        if keep is not None:
+            if not any(x in k for x in keep):
+                continue
+        elif not any(x in k for x in ("flash_", "fa3::", "fa32::")) or (
                 "fwd_kernel" not in k and "cols" not in k and "rows_kernel" not in k):
             continue
         per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
