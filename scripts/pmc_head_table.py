@@ -29,6 +29,8 @@ for k, c in sorted(m.items()):
     g = lambda n: c.get(n, float("nan"))  # noqa: E731
     busy = g("SQ_VALU_MFMA_BUSY_CYCLES") / 1024 / (g("GRBM_GUI_ACTIVE") / 8)
     mf = g("SQ_INSTS_MFMA")
+    if not mf > 0:  # no matrix work (prep / combine / sum kernels a name filter let through)
+        continue
     print(f"| `{k.split('::')[-1]}` | {100 * busy:.0f} % | {g('SQ_INSTS_VALU') / mf:.2f} | {g('SQ_INSTS_LDS') / mf:.2f} | "
           f"{g('SQ_INSTS_SALU') / mf:.2f} | {g('SQ_INSTS_VMEM') / mf:.2f} | "
           f"{100 * g('SQ_WAIT_INST_ANY') / g('SQ_WAVE_CYCLES'):.0f} % | "
