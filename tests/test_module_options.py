@@ -127,3 +127,20 @@ def test_library_weight_gradient_stays_on_current_stream():
     torch.testing.assert_close(dx, dy @ w)
     torch.testing.assert_close(dw, dy.t() @ x)
     torch.testing.assert_close(db, dy.sum(0))
+
+
+def test_weight_grad_pair_and_prescale_gate_cpu():
+    """CPU tensors: weight_grad_pair falls back to two weight_grad products (dyᵀ·x, fp32
+    accumulation, cast to the requested dtype) and the row pre-scale is never wanted."""
+    from xdot.ops.linear import weight_grad_pair
+    from xdot.parallel.attention import prescale_wanted
+
+    g = torch.Generator().manual_seed(3)
+    dy0, x0 = torch.randn(2, 5, 128, generator=g), torch.randn(2, 5, 256, generator=g)
+    dy1, x1 = torch.randn(10, 256, generator=g), torch.randn(10, 128, generator=g)
+    a, b = weight_grad_pair(dy0, x0, dy1, x1, torch.float32)
+    torch.testing.assert_close(a, dy0.reshape(-1, 128).t() @ x0.reshape(-1, 256), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(b, dy1.t() @ x1, rtol=1e-5, atol=1e-5)
+    assert a.shape == (128, 256) and b.shape == (256, 128)
+    k = torch.randn(1, 16, 64, dtype=torch.bfloat16)
+    assert not prescale_wanted(k, torch.cat([k, k], -1), 4)
