@@ -799,12 +799,18 @@ std::vector<at::Tensor> wgrad_run(std::vector<WgradProb>& qs, at::ScalarType out
   if (rc == -3) return {};
   check_launch((hipError_t)rc, "gemm_wgrad");
   std::vector<at::Tensor> outs;
+  for (int i = 0; i < np; ++i) outs.push_back(at::empty({qs[i].M, qs[i].N}, d0.options().dtype(out_dtype)));
+  if (np == 2) {  // both ordered sums in one launch
+    TORCH_CHECK(xdot_sum_partials2_launch(part[0], outs[0].data_ptr(), S[0], qs[0].M * qs[0].N, part[1],
+                                          outs[1].data_ptr(), S[1], qs[1].M * qs[1].N, dt_code(out_dtype),
+                                          cur_stream(d0)) == 0, "xdot.wgrad2: out dtype");
+    check_launch(hipGetLastError(), "wgrad2 sum");
+    return outs;
+  }
   for (int i = 0; i < np; ++i) {
-    auto out = at::empty({qs[i].M, qs[i].N}, d0.options().dtype(out_dtype));
-    TORCH_CHECK(xdot_sum_partials_launch(part[i], out.data_ptr(), S[i], qs[i].M * qs[i].N, dt_code(out_dtype),
+    TORCH_CHECK(xdot_sum_partials_launch(part[i], outs[i].data_ptr(), S[i], qs[i].M * qs[i].N, dt_code(out_dtype),
                                          cur_stream(d0)) == 0, "xdot.wgrad: out dtype");
     check_launch(hipGetLastError(), "wgrad sum");
-    outs.push_back(out);
   }
   return outs;
 }

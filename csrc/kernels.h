@@ -185,6 +185,9 @@ int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStr
 int xdot_flash_bwd_cols2_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 // out (n elements, dtype dto) = Σ_s part[s] (fp32 partials, n % 4 == 0)
 int xdot_sum_partials_launch(const float* part, void* out, int S, int64_t n, int dto, hipStream_t st);
+// both products of a paired weight-gradient launch in one pass (a: n_a elements, b: n_b)
+int xdot_sum_partials2_launch(const float* pa, void* oa, int Sa, int64_t na, const float* pb, void* ob, int Sb,
+                              int64_t nb, int dto, hipStream_t st);
 // out = (16-bit) (x * (scale * log2 e)) elementwise, n % 8 == 0: the pre-scaled row side of the
 // flash kernels (the factor is formed in fp32 exactly as the kernels form it)
 int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, int dt, hipStream_t st);

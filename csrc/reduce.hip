@@ -21,6 +21,31 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
   }
 }
 
+// the two products of one paired weight-gradient launch (csrc/gemm_wgrad.hip) summed by ONE
+// launch: threads [0, n4a) sum problem a, the rest problem b (same per-element order as above)
+template <int DTO>
+__global__ __launch_bounds__(256) void sum_partials2_kernel(const float* __restrict__ pa, void* __restrict__ oa, int Sa,
+                                                             int64_t n4a, const float* __restrict__ pb,
+                                                             void* __restrict__ ob, int Sb, int64_t n4b) {
+  using TO = typename dt_traits<DTO>::T;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool first = i < n4a;
+  if (!first) i -= n4a;
+  const int64_t n4 = first ? n4a : n4b;
+  if (i >= n4) return;
+  const float* part = first ? pa : pb;
+  const int S = first ? Sa : Sb;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(part + 4 * i);
+  for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n4 * 4 + 4 * i);
+  if constexpr (DTO == DT_F32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(first ? oa : ob) + 4 * i) = acc;
+  } else {
+    TO* o = reinterpret_cast<TO*>(first ? oa : ob) + 4 * i;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (TO)acc[e];
+  }
+}
+
 template <int DT>
 __global__ __launch_bounds__(256) void prescale_rows_kernel(const u32x4* __restrict__ x, u32x4* __restrict__ out,
                                                              int64_t n8, float scale) {
@@ -116,6 +141,22 @@ extern "C" int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, fl
   if (dt == DT_BF16) hipLaunchKernelGGL(prescale_rows_kernel<DT_BF16>, grid, dim3(256), 0, st, xi, o, n8, scale);
   else if (dt == DT_F16) hipLaunchKernelGGL(prescale_rows_kernel<DT_F16>, grid, dim3(256), 0, st, xi, o, n8, scale);
   else return -1;
+  return 0;
+}
+
+extern "C" int xdot_sum_partials2_launch(const float* pa, void* oa, int Sa, int64_t na, const float* pb, void* ob,
+                                         int Sb, int64_t nb, int dto, hipStream_t st) {
+  using namespace xdot;
+  if ((na % 4) || (nb % 4)) return -1;
+  const int64_t n4a = na / 4, n4b = nb / 4;
+  if (n4a + n4b == 0) return 0;
+  const dim3 grid((unsigned)((n4a + n4b + 255) / 256));
+#define SP2(D) hipLaunchKernelGGL(sum_partials2_kernel<D>, grid, dim3(256), 0, st, pa, oa, Sa, n4a, pb, ob, Sb, n4b)
+  if (dto == DT_F32) SP2(DT_F32);
+  else if (dto == DT_BF16) SP2(DT_BF16);
+  else if (dto == DT_F16) SP2(DT_F16);
+  else return -1;
+#undef SP2
   return 0;
 }
 
