@@ -152,8 +152,9 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
         opt = xdot.FusedAdamW(model.parameters(), lr=1e-4, capturable=graph)
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=(dev.type == "cuda"))
-    sync = GradSync(model, comm=comm, bucket_mb=1.0)  # per-parameter buckets: the output
-    # projection's all-reduce overlaps the attention backward
+    # per-parameter buckets (the output projection's all-reduce overlaps the attention backward),
+    # reduced in fp32 (one rounding to the parameter dtype at the end instead of one per ring step)
+    sync = GradSync(model, comm=comm, bucket_mb=1.0, reduce_dtype=torch.float32)
     crit = xdot.MSELoss()  # fused loss + gradient pass (torch.nn.MSELoss semantics)
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)

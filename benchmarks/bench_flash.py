@@ -52,6 +52,9 @@ def main():
                     help="fp32 kernel family (default: XDOT_FP32_MODE)")
     ap.add_argument("--no-prescale", action="store_true",
                     help="kernels scale every score (default: pre-scaled rows + seeded accumulators, the module's path)")
+    ap.add_argument("--scores", action="store_true",
+                    help="exact fp32: score-buffer mode (forward stores S, bwd_cols reads S and writes dS, "
+                         "bwd_rows reads dS; products 2 / 3 / 1 instead of 2 / 4 / 3)")
     ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
     ap.add_argument("--concurrent", action="store_true",
                     help="also time bwd_cols and bwd_rows launched together on two streams (cols on a normal "
@@ -81,22 +84,34 @@ def main():
     scale = 1.0 / math.sqrt(D)
     ps = not a.no_prescale and dt != torch.float32
     rk = flash.prescale(rows, scale) if ps else rows
-    out, lse = flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps)
-    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps)
+    sb = None
+    if a.scores:
+        assert dt == torch.float32, "--scores is an exact-fp32 mode"
+        sb = flash.score_buffer(B, H, R, T, dev)
+        assert sb is not None, "score buffer does not fit"
+    # (timing only: after the first bwd_cols the buffer holds dS, which later calls read as S)
+    out, lse = flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps, sbuf=sb)
+    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb)
     gemm = 2.0 * B * R * T * H * D
+    np_cols, np_rows = (3, 1) if sb is not None else (4, 3)
     res = []
     if a.only in ("all", "mask") and mask is not None:
         ms, mn = timeit(lambda: flash.prepare_mask(mask, B, R, T), a.iters)
         res.append({"kernel": "mask_pack", "ms": ms, "min_ms": mn, "GB_s": B * R * T / ms / 1e6})
     if a.only in ("all", "fwd"):
-        ms, mn = timeit(lambda: flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps), a.iters)
-        res.append({"kernel": "flash_fwd", "ms": ms, "min_ms": mn, "TFLOPs": 2 * gemm / ms / 1e9})
+        ms, mn = timeit(lambda: flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps, sbuf=sb), a.iters)
+        res.append({"kernel": "flash_fwd" + ("+S" if sb is not None else ""), "ms": ms, "min_ms": mn,
+                    "TFLOPs": 2 * gemm / ms / 1e9})
     if a.only in ("all", "bwd_cols"):
-        ms, mn = timeit(lambda: flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps), a.iters)
-        res.append({"kernel": "flash_bwd_cols", "ms": ms, "min_ms": mn, "TFLOPs": 4 * gemm / ms / 1e9})
+        ms, mn = timeit(lambda: flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb),
+                        a.iters)
+        res.append({"kernel": "flash_bwd_cols" + ("(S->dS)" if sb is not None else ""), "ms": ms, "min_ms": mn,
+                    "TFLOPs": np_cols * gemm / ms / 1e9})
     if a.only in ("all", "bwd_rows"):
-        ms, mn = timeit(lambda: flash.bwd_rows(do, rk, kc, vc, lse, delta, mk, H, scale, a.nsplit, prescaled=ps), a.iters)
-        res.append({"kernel": "flash_bwd_rows", "ms": ms, "min_ms": mn, "TFLOPs": 3 * gemm / ms / 1e9})
+        ms, mn = timeit(lambda: flash.bwd_rows(do, rk, kc, vc, lse, delta, mk, H, scale, a.nsplit, prescaled=ps,
+                                               sbuf=sb), a.iters)
+        res.append({"kernel": "flash_bwd_rows" + ("(dS)" if sb is not None else ""), "ms": ms, "min_ms": mn,
+                    "TFLOPs": np_rows * gemm / ms / 1e9})
     if a.concurrent:
         for prio in (0, -1):
             side = torch.cuda.Stream(device=dev, priority=prio)

@@ -17,9 +17,15 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
+// sha256 of csrc/* + flags, compiled in by xdot/build.py (build/xdot/build_id.cpp)
+extern "C" const char xdot_build_id[];
+
 namespace {
+
+std::string build_id() { return std::string(xdot_build_id + 14); }  // after "XDOT_BUILD_ID="
 
 // roctx ranges around every op (visible in rocprofv3 --marker-trace timelines); enabled by
 // XDOT_ROCTX=1 so the default path pays one predictable branch.
@@ -550,11 +556,26 @@ bool head_heavy_plan(int64_t NB, int64_t T, int* whole, int* rem, int* split) {
   return true;
 }
 
+// exact-fp32 score buffer (flash_f32.hip): (B*H, ceil(R/32), ceil(T/32)) blocks of 1024 floats
+float* sbuf_ptr(const c10::optional<at::Tensor>& sbuf, const FlashGeom& g, int64_t H, const at::Tensor& rows,
+                int64_t fp32_mode, const char* what) {
+  if (!sbuf.has_value() || !sbuf->defined()) return nullptr;
+  const auto& t = *sbuf;
+  TORCH_CHECK(rows.scalar_type() == at::kFloat && fp32_mode == 0, what, ": the score buffer is an exact-fp32 feature");
+  const int64_t need = g.B * H * ((g.R + 31) / 32) * ((g.T + 31) / 32) * 1024;
+  TORCH_CHECK(t.is_cuda() && t.device() == rows.device() && t.scalar_type() == at::kFloat && t.is_contiguous() &&
+                  t.numel() == need && aligned16(t.data_ptr()),
+              what, ": score buffer must be a contiguous fp32 device tensor of ", need, " elements");
+  return t.data_ptr<float>();
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                                              const c10::optional<at::Tensor>& bits, const c10::optional<at::Tensor>& flags,
-                                             int64_t H, double scale, int64_t nsplit, bool prescaled, int64_t fp32_mode) {
+                                             int64_t H, double scale, int64_t nsplit, bool prescaled, int64_t fp32_mode,
+                                             const c10::optional<at::Tensor>& sbuf) {
   Range rr_("xdot.flash_fwd");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_fwd");
   auto out = at::empty_like(rows);
   auto lse = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   const int rpw = xdot_flash_fwd_rows_per_wg();
@@ -588,6 +609,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   a.lpart = ns > 1 ? lpart.data_ptr<float>() : nullptr;
   a.prescaled = prescaled ? 1 : 0;
   a.fp32_mode = (int)fp32_mode;
+  a.sbuf = sb;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_fwd_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0, "xdot.flash_fwd: config");
   check_launch(hipGetLastError(), "flash_fwd");
@@ -622,9 +644,11 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               double scale, const c10::optional<at::Tensor>& delta_in,
                                                               bool fp32_out, bool prescaled,
                                                               const c10::optional<at::Tensor>& lse2_in,
-                                                              int64_t fp32_mode) {
+                                                              int64_t fp32_mode,
+                                                              const c10::optional<at::Tensor>& sbuf) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
+  float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols");
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
@@ -654,6 +678,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
     lse2 = at::empty({g.B, H, g.R}, rows.options().dtype(at::kFloat));
   }
   a.lse2 = lse2.data_ptr<float>();
+  a.sbuf = sb;
   c10::DeviceGuard guard(rows.device());
   const int dt = dt_code(rows.scalar_type());
   // prep: lse2 (+ δ unless given)
@@ -976,9 +1001,10 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_prep(const at::Tensor& dout, const 
 at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                           const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                           const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit,
-                          bool prescaled, int64_t fp32_mode) {
+                          bool prescaled, int64_t fp32_mode, const c10::optional<at::Tensor>& sbuf) {
   Range rr_("xdot.flash_bwd_rows");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
+  float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_rows");
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
               "xdot.flash_bwd_rows: delta");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
@@ -990,6 +1016,7 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   a.nsplit = ns; a.dpart = ns > 1 ? dpart.data_ptr<float>() : nullptr;
   a.prescaled = prescaled ? 1 : 0;
   a.fp32_mode = (int)fp32_mode;
+  a.sbuf = sb;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows: config");
@@ -1289,10 +1316,10 @@ TORCH_LIBRARY(xdot, m) {
   m.def("softmax_fwd(Tensor x, Tensor? mask, float scale, int mdiv, int mmul, int mmod) -> Tensor");
   m.def("softmax_bwd(Tensor y, Tensor dy, float scale) -> Tensor");
   m.def("mask_pack(Tensor mask) -> (Tensor, Tensor, Tensor)");
-  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> (Tensor, Tensor)");
+  m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor(a!)? sbuf=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False, "
-        "Tensor? lse2=None, int fp32_mode=0) -> (Tensor, Tensor)");
+        "Tensor? lse2=None, int fp32_mode=0, Tensor(a!)? sbuf=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_prep(Tensor dout, Tensor out, Tensor lse, int H) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
@@ -1308,7 +1335,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0) -> Tensor");
+        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor? sbuf=None) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
   m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0, float alpha=1.0) -> Tensor");
@@ -1327,11 +1354,13 @@ TORCH_LIBRARY(xdot, m) {
         "int ticks, int nwg) -> ()");
   m.def("ipc_reduce_scatter(Tensor inp, Tensor(a!) out, int[] stage, int[] sig, int status, int rank, int epoch, "
         "int ticks, int nwg) -> ()");
+  m.def("build_id() -> str");
   m.def("graph_kernel_priorities(int graph) -> int[]");
   m.def("graph_set_kernel_priority(int graph, int index, int prio) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(xdot, CompositeExplicitAutograd, m) {
+  m.impl("build_id", &build_id);
   m.impl("graph_kernel_priorities", &graph_kernel_priorities);
   m.impl("graph_set_kernel_priority", &graph_set_kernel_priority);
   m.impl("flash_splits", &flash_splits);

@@ -24,6 +24,19 @@
 //   * 32-row tiles staged global -> VGPR -> LDS one tile ahead (double-buffered LDS, one
 //     barrier per tile): at 64+ MFMA cycles per 64-bit of operand this kernel family is MFMA
 //     bound, so the simple staging costs nothing measurable.
+//
+// Score-buffer mode (FwdArgs/BwdArgs::sbuf).  In fp32 a product costs 2*D FLOP per score at the
+// fp32 matrix rate (~131 TF/s): 1.47 ps per score at D = 96, while writing and re-reading the
+// score costs 8 bytes of HBM traffic (~1.6 ps at 5 TB/s) that the MFMA-bound kernels leave idle.
+// So the backward reads what the forward already computed instead of recomputing it:
+//   forward      stores the raw S of every computed 32x32 tile (1 extra store pass, 0 products)
+//   column side  loads S (no S product), computes dP, dV, dQ and overwrites the block with dS
+//   row side     loads dS: dK = dS · Q is its ONLY product (no S, no dP recompute)
+// 6 products per step instead of 9; the S / dS values are bit-identical to the recomputed ones
+// (same MFMA chains), so results do not change.  Blocks are (B*H, ceil(R/32), ceil(T/32)) x
+// 1024 floats; within a block a tile sits in the READER's accumulator order (16 floats per lane,
+// 4 x b128 loads), the writer scatters (blk_store).  Tiles the mask flags skip are neither
+// written nor read.
 #include "flash_common.h"
 
 namespace xdot {
@@ -113,6 +126,30 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
 // tile index of accumulator register r for lane half hf
 __device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
+// Score-buffer block I/O.  A 32x32 accumulator x holds element (a, b) with a = lane & 31 (lane
+// index) and b = tidx(r, lane >> 5) (register r).  blk_store writes it TRANSPOSED into the
+// reader's accumulator order: element (a, b) to [lane' = b + 32((a>>2)&1)][r' = (a&3) + 4(a>>3)],
+// i.e. the reader whose lane index is b finds it in its register r' -> blk_load(blk, lane)[r'].
+// (forward: a = row, b = column -> the column kernel's order; column kernel: a = column,
+// b = row -> the row kernel's order.)  Per lane 16 scattered dword stores / 4 b128 loads.
+__device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane) {
+  const int a = lane & 31, hf = lane >> 5;
+  float* p = blk + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
+}
+__device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
+  f32x16 x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 v = p[q];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) x[4 * q + t] = v[t];
+  }
+  return x;
+}
+
 // flag of (32-row block rb32, 64-col tile kt64): 0 none / 1 all / 2 some masked
 __device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
   return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
@@ -120,7 +157,8 @@ __device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, i
 
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
-template <int D>
+// SS: store the raw scores into a.sbuf (score-buffer mode)
+template <int D, bool SS>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
@@ -150,6 +188,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
   f32x16 o[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) o[i] = f32x16{};
+  // score buffer: this wave's row of 32x32 blocks (r0 < R: waves past R never store)
+  float* sbw = SS ? a.sbuf + ((int64_t)bh * NRB32 + (r0 >> 5)) * NKT32 * 1024 : nullptr;
 
   Stager<D> st;
   if (kt_beg < kt_end) {
@@ -166,6 +206,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
       f32x16 s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
+      if constexpr (SS) blk_store(sbw + (int64_t)kt * 1024, s, lane);  // raw S (rows past R: 0)
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
@@ -359,7 +400,9 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
 // ------------------------------------------------------------------------------------------
 // backward, gathered side: dQ_cols = scale · Σ_rows dSᵀ · K_rows, dV_cols = Σ_rows Pᵀ · dO.
 // 4 waves x 32 columns of one (b, h); sweeps 32-row tiles of K_rows / dO + their lse2 / δ.
-template <int D>
+// LS (score-buffer mode): S comes from a.sbuf (prefetched one tile ahead) instead of the
+// K·Qᵀ product, and each block is overwritten with dS / scale for the row kernel.
+template <int D, bool LS>
 __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
@@ -375,14 +418,20 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const bool col_ok = col < a.T;
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
-  const int NRT = (a.R + 31) / 32;
+  const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
 
-  float qf[D / 2], vf[D / 2];
+  float qf[LS ? 1 : D / 2], vf[D / 2];
   {
     const int64_t off = ((int64_t)b * a.T + (col_ok ? col : 0)) * a.ldkv + h * D + 4 * hf;
-    load_frag<D>(qf, reinterpret_cast<const float*>(a.kc) + off, col_ok);
+    if constexpr (!LS) load_frag<D>(qf, reinterpret_cast<const float*>(a.kc) + off, col_ok);
     load_frag<D>(vf, reinterpret_cast<const float*>(a.vc) + off, col_ok);
   }
+  // score buffer column of this wave: block (bh, rt, c0/32) at sbc + rt * NKT32 * 1024
+  const bool sown = LS && c0 < a.T;
+  float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
+  const int64_t sstep = (int64_t)NKT32 * 1024;
+  f32x16 snext{};
+  if (sown && NRT > 0) snext = blk_load(sbc, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
@@ -410,9 +459,13 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   }
   for (int rt = 0; rt < NRT; ++rt) {
     const bool more = rt + 1 < NRT;
+    f32x16 scur;
+    if constexpr (LS) scur = snext;
     if (more) {
       st.load(kb, db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
+      if constexpr (LS)
+        if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
     const float* ki = sm + (rt & 1) * CF::STAGE;
     const float* di = ki + CF::IMG;
@@ -420,7 +473,9 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
-      f32x16 s = rowprod<D>(ki, qf, f32x16{}, lane);   // S  (row x col)
+      f32x16 s;
+      if constexpr (LS) s = scur;                        // S  (row x col), stored by the forward
+      else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
       f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
       uint32_t w = 0;
       if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
@@ -433,6 +488,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
         s[r] = p;
         dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
       }
+      if constexpr (LS) blk_store(sbc + rt * sstep, dp, lane);  // dS in place of S (row-kernel order)
       trprod<D>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
     }
@@ -456,6 +512,96 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
       *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
           f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward, row side in score-buffer mode: dK = scale · Σ_cols dS · Q_cols with dS read from the
+// buffer the column kernel wrote (one product per tile: no S, no dP, no V / dO traffic).  Same
+// grid, column split and partial protocol as bwd_rows_kernel; the only LDS image is Q.
+template <int D> struct Stager1 {  // one 32-row image (Q) global -> registers -> LDS
+  using CF = Cfg<D>;
+  f32x4 r[CF::NC];  // 32 rows x D floats = 256 threads x NC f32x4
+  __device__ __forceinline__ void load(const float* b0, int64_t ld, int64_t row0, int rmax, int tid) {
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      r[i] = *reinterpret_cast<const f32x4*>(b0 + (row0 + min(row, rmax)) * ld + 4 * c);
+    }
+  }
+  __device__ __forceinline__ void store(float* img, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CF::NC; ++i) {
+      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
+      *reinterpret_cast<f32x4*>(img + row * CF::P + 4 * c) = r[i];
+    }
+  }
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  constexpr int DB = CF::DB;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R, wave_ok = r0 < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* sbr = a.sbuf + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
+  f32x16 dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+
+  Stager1<D> st;
+  f32x16 dnext{};
+  if (kt_beg < kt_end) {
+    st.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    if (wave_ok) dnext = blk_load(sbr + (int64_t)kt_beg * 1024, lane);
+    st.store(sm, tid);
+    __syncthreads();
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    const bool more = kt + 1 < kt_end;
+    f32x16 ds = dnext;
+    if (more) {
+      st.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+      if (wave_ok) dnext = blk_load(sbr + (int64_t)(kt + 1) * 1024, lane);
+    }
+    const float* qi = sm + ((kt - kt_beg) & 1) * CF::IMG;
+    int flag = !wave_ok ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      const int valid = a.T - kt * 32;
+      if (valid < 32) {  // columns past T: the column kernel's values there are not gradients
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (tidx(r, hf) >= valid) ds[r] = 0.f;
+      }
+      trprod<D>(qi, ds, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+    }
+    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::IMG, tid);
+    __syncthreads();
+  }
+  if (!row_ok) return;
+  float* op = (a.nsplit > 1 || a.force_partial) ? a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D
+                                                : reinterpret_cast<float*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dk[db][4 * g] * sc, dk[db][4 * g + 1] * sc, dk[db][4 * g + 2] * sc, dk[db][4 * g + 3] * sc};
 }
 
 // sum a.nsplit slots of a.dpart into the fp32 row-side grad
@@ -487,7 +633,12 @@ extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipS
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
   const int nrb = (a->R + 127) / 128;
   const dim3 grid(nrb * a->B * a->H * a->nsplit);
-#define L(DV) hipLaunchKernelGGL(fwd_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
+  if (a->sbuf) {
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+    XF32_DISPATCH(L)
+#undef L
+  }
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, false>), grid, dim3(256), lds_bytes<DV>(), st, *a)
   XF32_DISPATCH(L)
 #undef L
 }
@@ -514,6 +665,11 @@ extern "C" int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->prescaled) return -1;
   const int nrb = (a->R + 127) / 128;
   const dim3 grid(nrb * a->B * a->H * a->nsplit);
+  if (a->sbuf) {  // score-buffer mode: dS from the column kernel, Q image only
+#define L(DV) hipLaunchKernelGGL(bwd_rows_ds_kernel<DV>, grid, dim3(256), 2 * Cfg<DV>::IMG * 4, st, *a)
+    XF32_DISPATCH(L)
+#undef L
+  }
 #define L(DV) hipLaunchKernelGGL(bwd_rows_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
   XF32_DISPATCH(L)
 #undef L
@@ -524,7 +680,12 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
-#define L(DV) hipLaunchKernelGGL(bwd_cols_kernel<DV>, grid, dim3(256), lds_bytes<DV>(), st, *a)
+  if (a->sbuf) {
+#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+    XF32_DISPATCH(L)
+#undef L
+  }
+#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), lds_bytes<DV>(), st, *a)
   XF32_DISPATCH(L)
 #undef L
 }

@@ -61,6 +61,9 @@ struct FwdArgs {
   // are split into nsplit column pieces whose partials go to a compact buffer
   // opart/lpart[(piece * 8*xrem + tail) * 128 + row-in-block] (* D for opart)
   int xrbs, xwhole, xrem;
+  // exact fp32 only: non-null -> the raw scores S of every computed 32x32 tile are stored here
+  // ((B*H, ceil(R/32), ceil(T/32)) blocks of 1024 floats, flash_f32.hip "score buffer")
+  float* sbuf;
 };
 
 struct BwdArgs {
@@ -87,6 +90,9 @@ struct BwdArgs {
   int force_partial;       // 1: write partials even with nsplit == 1 (summed separately)
   int prescaled;           // 1: rows hold K * scale * log2(e) (same buffer as the forward's)
   int fp32_mode;           // fp32 inputs: 0 exact (flash_f32.hip), 1 split-bf16 (flash_x3.hip)
+  // exact fp32 only: the forward's score buffer (FwdArgs::sbuf).  The column kernel reads S from it
+  // instead of recomputing it and overwrites each block with dS; the row kernel then reads dS
+  float* sbuf;
 };
 
 }  // namespace fa

@@ -143,7 +143,9 @@ def test_gradsync_contract_gloo():
 def _fused_delivery_body(rank, ws):
     """The fused module node hands its parameter gradients to an attached GradSync as it computes
     them (GradSync.deliver): same Sum-reduced gradients as autograd accumulation followed by
-    allreduce_gradients, for two steps in a row (accumulation into existing .grad included)."""
+    allreduce_gradients, step by step, for two steps in a row (the second accumulates into the
+    reduced .grad of the first and the bucket is reduced again: in both models the result is
+    ws * G1 + sum of the step-2 local gradients)."""
     import xdot
     from xdot.parallel import GradSync, allreduce_gradients, broadcast_parameters
 
@@ -158,18 +160,92 @@ def _fused_delivery_body(rank, ws):
     for step in range(2):
         x = torch.rand(1, 6, 32, generator=g, dtype=torch.float64)
         m1(x, x, x, None).square().sum().backward()
+        allreduce_gradients(m1)
         m2(x, x, x, None).square().sum().backward()
-        if step == 0:
-            sync.wait()  # first step: reduced now; the second backward accumulates on top
-    allreduce_gradients(m1)
-    # m1 accumulated two steps then reduced the sum; m2 reduced step 1, then step 2's delivered
-    # local grads were added to the reduced step-1 grads and the bucket reduced again: compare
-    # the same quantity by reducing m1's step-1 part twice -> use per-step comparison instead
-    sync.wait()
-    for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert p2.grad is not None, n2
+        sync.wait()
+        for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            assert p2.grad is not None, n2
+            torch.testing.assert_close(p2.grad, p1.grad, rtol=1e-10, atol=1e-12, msg=f"step {step} {n2}")
     sync.remove()
     assert m2._xdot_grad_sync is None
+
+
+def _fused_twice_body(rank, ws):
+    """One module called twice in one forward under an attached GradSync: the node must not
+    deliver (the two uses are summed by AccumulateGrad first), so the reduced gradients equal the
+    plain autograd + allreduce_gradients result (fused.py delivery)."""
+    import xdot
+    from xdot.parallel import GradSync, allreduce_gradients, broadcast_parameters
+
+    torch.manual_seed(rank)
+    m1 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    broadcast_parameters(m1)
+    m2 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    m2.load_state_dict(m1.state_dict())
+    sync = GradSync(m2, bucket_mb=0.0001)
+    g = torch.Generator().manual_seed(7 + rank)
+    x = torch.rand(1, 6, 32, generator=g, dtype=torch.float64)
+    y = torch.rand(1, 6, 32, generator=g, dtype=torch.float64)
+    for _ in range(2):  # the use count resets at wait()
+        for p in list(m1.parameters()) + list(m2.parameters()):
+            p.grad = None
+        (m1(x, x, x, None).square().sum() + m1(y, y, y, None).pow(3).sum()).backward()
+        allreduce_gradients(m1)
+        (m2(x, x, x, None).square().sum() + m2(y, y, y, None).pow(3).sum()).backward()
+        sync.wait()
+        for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            torch.testing.assert_close(p2.grad, p1.grad, rtol=1e-10, atol=1e-12, msg=n2)
+
+
+def _fused_frozen_body(rank, ws):
+    """A frozen queries weight beside a trained values weight: the fused node hands back (and
+    delivers) no gradient for the frozen one (needs_input_grad)."""
+    import xdot
+    from xdot.parallel import GradSync, allreduce_gradients, broadcast_parameters
+
+    torch.manual_seed(rank)
+    m1 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    broadcast_parameters(m1)
+    m2 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    m2.load_state_dict(m1.state_dict())
+    for m in (m1, m2):
+        m.queries.weight.requires_grad_(False)
+        m.values.bias.requires_grad_(False)
+    sync = GradSync(m2, bucket_mb=0.0001)
+    x = torch.rand(1, 6, 32, generator=torch.Generator().manual_seed(11 + rank), dtype=torch.float64)
+    m1(x, x, x, None).square().sum().backward()
+    allreduce_gradients(m1)
+    m2(x, x, x, None).square().sum().backward()
+    sync.wait()
+    assert m2.queries.weight.grad is None and m2.values.bias.grad is None
+    for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        if p1.requires_grad:
+            torch.testing.assert_close(p2.grad, p1.grad, rtol=1e-10, atol=1e-12, msg=n2)
+
+
+def test_gradsync_fused_module_called_twice():
+    run_gloo(_fused_twice_body, 2)
+
+
+def test_gradsync_fused_frozen_half_of_packed_weight():
+    run_gloo(_fused_frozen_body, 2)
+
+
+def test_fused_module_retain_graph_twice():
+    """backward twice through a retained graph of the fused module node: the second pass gives
+    the same gradients again (they accumulate to twice the first), no error."""
+    import xdot
+
+    torch.manual_seed(0)
+    m = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash", distributed=False).double()
+    x = torch.rand(1, 6, 32, dtype=torch.float64, requires_grad=True)
+    loss = m(x, x, x, None).square().sum()
+    loss.backward(retain_graph=True)
+    g1 = [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
+    loss.backward()
+    g2 = [p.grad for p in m.parameters()] + [x.grad]
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(b, 2 * a, rtol=1e-12, atol=1e-14)
 
 
 def _fused_delivery_one_step(rank, ws):

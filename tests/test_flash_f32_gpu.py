@@ -99,6 +99,86 @@ def test_flash_f32_column_split(gpu, nsplit):
     assert _rel(d2, d1) <= 1e-6
 
 
+# ---- exact fp32, score-buffer mode (XDOT_FP32_SCORES: S stored by the forward, dS by the column
+# kernel; csrc/flash_f32.hip) -------------------------------------------------------------------
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
+@pytest.mark.parametrize("nsplit", [0, 3])
+def test_flash_f32_score_buffer_bitwise(gpu, case, mask_kind, nsplit):
+    """Reading S / dS from the score buffer instead of recomputing them changes nothing: the
+    forward, both backward kernels and the column-split partials are BITWISE equal to the
+    recompute path (same MFMA chains), which the fp64 test above bounds."""
+    from xdot.ops import flash
+
+    B, R, N, Rc, H, D = case
+    T = N * Rc
+    rows, kc, vc, do, mask = _inputs(case, mask_kind, gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    o1, l1 = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=nsplit, fp32_mode=0)
+    dkv1, dl1 = flash.bwd_cols(do, rows, kb, vb, o1, l1, mk, H, scale, fp32_mode=0)
+    dr1 = flash.bwd_rows(do, rows, kb, vb, l1, dl1, mk, H, scale, nsplit=nsplit, fp32_mode=0)
+    sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)  # no stale zeros
+    o2, l2 = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=nsplit, fp32_mode=0, sbuf=sb)
+    dkv2, dl2 = flash.bwd_cols(do, rows, kb, vb, o2, l2, mk, H, scale, fp32_mode=0, sbuf=sb)
+    dr2 = flash.bwd_rows(do, rows, kb, vb, l2, dl2, mk, H, scale, nsplit=nsplit, fp32_mode=0, sbuf=sb)
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    assert torch.equal(dkv1, dkv2), f"d cols {_rel(dkv2, dkv1):.2e}"
+    assert torch.equal(dr1, dr2), f"d rows {_rel(dr2, dr1):.2e}"
+
+
+def test_flash_f32_score_buffer_checks(gpu):
+    """Wrong-sized buffers and non-exact modes are refused on the host."""
+    from xdot.ops import flash
+
+    rows = torch.randn(1, 64, 128, device=gpu)
+    kc = torch.randn(1, 96, 128, device=gpu)
+    n = flash.score_buffer_numel(1, 2, 64, 96)
+    assert n == 2 * 2 * 3 * 1024
+    with pytest.raises(RuntimeError, match="score buffer"):
+        flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=0, sbuf=torch.empty(n - 1, device=gpu))
+    with pytest.raises(RuntimeError, match="exact-fp32"):
+        flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=1, sbuf=torch.empty(n, device=gpu))
+
+
+def test_module_fp32_score_buffer_matches_recompute(gpu):
+    """The fp32 module with the score buffer (default) and without (XDOT_FP32_SCORES=0) gives
+    bitwise equal outputs and gradients, twice in a row (determinism), and a retained graph's
+    second backward (the buffer then holds dS: the recompute path runs) gives the same again."""
+    import xdot
+    from xdot.utils.comm import LocalComm, use_comm
+    from xdot.utils.env import FLAGS
+
+    def run(scores):
+        old = FLAGS.fp32_scores
+        FLAGS.fp32_scores = scores
+        try:
+            torch.manual_seed(0)
+            with use_comm(LocalComm()):
+                m = xdot.DistributedDotProductAttn(256, num_heads=4, add_bias=True).to(gpu)
+                x = torch.randn(1, 700, 256, device=gpu, requires_grad=True)
+                mask = torch.rand(1, 700, 700, device=gpu) < 0.2
+                mask[..., 0] = False
+                loss = m(x, x, x, mask).square().sum()
+                loss.backward(retain_graph=True)
+                g1 = [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
+                loss.backward()
+                g2 = [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
+            return loss.detach(), g1, g2
+        finally:
+            FLAGS.fp32_scores = old
+
+    la, a1, a2 = run(True)
+    lb, b1, b2 = run(False)
+    lc, c1, c2 = run(True)
+    assert torch.equal(la, lb) and torch.equal(la, lc)
+    for x, y, z in zip(a1, b1, c1):
+        assert torch.equal(x, y) and torch.equal(x, z)
+    for x, y in zip(a2, b2):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("fm", [0, 1])
 def test_flash_f32_fully_masked_row_nan(gpu, fm):
     from xdot.ops import flash

@@ -240,3 +240,34 @@ def test_fp32_mode_codes():
             flash.fp32_code(torch.float32)
     finally:
         FLAGS.fp32_mode = old
+
+
+def test_build_id_detects_edited_sources(tmp_path):
+    """The extension carries the content hash of csrc/ (xdot/build.py); editing any source makes
+    the loader refuse the old binary (a stale _C.so once crashed a GPU run with a
+    changed op schema)."""
+    import shutil
+
+    import pytest
+
+    from xdot import _ext
+    from xdot import build as b
+
+    src = tmp_path / "csrc"
+    shutil.copytree(b.CSRC, src)
+    h0 = b.tree_hash(str(src))
+    assert h0 == b.tree_hash(b.CSRC)
+    lib = tmp_path / "_C.so"
+    lib.write_bytes(b"\x7fELF..." + b.ID_TAG + h0.encode() + b"\0rest")
+    assert b.embedded_id(str(lib)) == h0
+    _ext._check_provenance(str(lib), str(src), rebuild=False)  # matching: no error
+    f = src / "flash_f32.hip"
+    f.write_text(f.read_text() + "\n// edited\n")
+    assert b.tree_hash(str(src)) != h0
+    with pytest.raises(RuntimeError, match="stale"):
+        _ext._check_provenance(str(lib), str(src), rebuild=False)
+    # flags are part of the id too
+    assert b.tree_hash(b.CSRC, extra=["-O2"]) != b.tree_hash(b.CSRC)
+    # the in-tree binary, when built, matches the in-tree sources
+    if os.path.exists(b.OUT):
+        assert b.embedded_id(b.OUT) == b.tree_hash(b.CSRC)

@@ -23,8 +23,41 @@ def lib_path() -> str:
     return _LIB
 
 
+def provenance(lib: str = None, csrc: str = None):
+    """(build id embedded in ``lib``, hash of the ``csrc`` tree): equal when the binary was built
+    from exactly these sources and flags (:func:`xdot.build.tree_hash`)."""
+    from . import build as _b
+
+    return _b.embedded_id(lib or _LIB), _b.tree_hash(csrc or _b.CSRC)
+
+
+def _check_provenance(lib: str = None, csrc: str = None, rebuild: bool = None) -> None:
+    """Refuse (or rebuild) an in-tree ``_C.so`` that was not built from the sources next to it:
+    a stale binary either crashes on a changed op schema or silently runs old kernels.  Skipped
+    for ``XDOT_EXT_PATH`` builds (A/B experiments) and when the sources are not present."""
+    from . import build as _b
+
+    csrc = csrc or _b.CSRC
+    if (FLAGS.ext_path and lib is None) or not os.path.isdir(csrc):
+        return
+    have, want = provenance(lib, csrc)
+    if have == want:
+        return
+    rebuild = FLAGS.auto_rebuild if rebuild is None else rebuild
+    if rebuild and lib is None and os.path.exists(_b.HIPCC):
+        import sys
+
+        print(f"xdot: {_LIB} build id {have} != sources {want}: rebuilding", file=sys.stderr, flush=True)
+        _b.build()
+        have = _b.embedded_id(_LIB)
+        if have == want:
+            return
+    raise RuntimeError(f"xdot: {lib or _LIB} is stale (build id {have}, csrc/ tree {want}); rebuild it with "
+                       "`python -m xdot.build` (or set XDOT_EXT_PATH to load a specific build)")
+
+
 def load(build_if_missing: bool = False) -> bool:
-    """Load ``_C.so`` once.  Returns True on success."""
+    """Load ``_C.so`` once (after :func:`_check_provenance`).  Returns True on success."""
     if _state["loaded"]:
         return True
     with _lock:
@@ -37,6 +70,7 @@ def load(build_if_missing: bool = False) -> bool:
         if not os.path.exists(_LIB):
             _state["error"] = f"{_LIB} not built (run `python -m xdot.build`)"
             return False
+        _check_provenance()
         try:
             torch.ops.load_library(_LIB)
             _state["loaded"] = True

@@ -86,7 +86,10 @@ def _stacked_rows(a: Tensor, b: Tensor) -> Tensor:
     view of it."""
     if not _adjacent(a, b):
         if not (isinstance(a, nn.Parameter) and isinstance(b, nn.Parameter) and a.dtype == b.dtype
-                and a.device == b.device and tuple(a.shape[1:]) == tuple(b.shape[1:])):
+                and a.device == b.device and tuple(a.shape[1:]) == tuple(b.shape[1:])) \
+                or torch.is_inference_mode_enabled():
+            # (under inference mode the packed buffer would be an inference tensor that later
+            # in-place optimizer updates could not touch: no repack there)
             return torch.cat([a, b], 0)
         with torch.no_grad():
             packed = torch.empty((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
@@ -193,7 +196,11 @@ class DistributedDotProductAttn(nn.Module):
                     _stacked_rows(wq, wv)  # (re)pack the two parameters into one storage once
                     if bq is not None:
                         _stacked_rows(bq, bv)
-                sync = self._xdot_grad_sync() if self._xdot_grad_sync is not None else None
+                gs = self._xdot_grad_sync() if self._xdot_grad_sync is not None else None
+                sync = None
+                if gs is not None and torch.is_grad_enabled():
+                    gs.note_use(id(self))
+                    sync = (gs, id(self))
                 return AttnBlockFn.apply(keys, queries, attn_mask, self.keys.weight, self.keys.bias, wq, bq, wv, bv,
                                          self.composition.weight, self.composition.bias, self.num_heads, scale, comm,
                                          self.chunk_plan, sync)

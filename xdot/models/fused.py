@@ -99,17 +99,21 @@ class AttnBlockFn(torch.autograd.Function):
         o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending, pre)  # k_prescaled
         out = proj(o, wc, bc)
         ctx.actx = actx
-        ctx.sync = sync
+        ctx.sync = sync  # (GradSync, module key) or None
         ctx.params = (wk, bk, wq, bq, wv, bv, wc, bc)
         ctx.nq = wq.shape[0]
         ctx.has_b = (bk is not None, bq is not None, bc is not None)
-        ctx.save_for_backward(xk, xqv, wk, wqv, wc, o)
+        # the attention's tensors go through save_for_backward too (version checks, and a graph
+        # retained for a second backward keeps them)
+        asaved, actx._saved = actx._saved, None
+        ctx.save_for_backward(xk, xqv, wk, wqv, wc, o, *asaved)
         return out
 
     @staticmethod
     @_ext.pinned
     def backward(ctx, dout):
-        xk, xqv, wk, wqv, wc, o = ctx.saved_tensors
+        xk, xqv, wk, wqv, wc, o, *asaved = ctx.saved_tensors
+        ctx.actx._saved = tuple(asaved)
         ng = ctx.needs_input_grad
         hk, hq, hc = ctx.has_b
         dout = dout.contiguous()
@@ -123,7 +127,12 @@ class AttnBlockFn(torch.autograd.Function):
             dout._xdot_ready_on = _ready_on(dout, side)
             _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=False)
         wk_, bk_, wq_, bq_, wv_, bv_, wc_, bc_ = ctx.params
-        sync = ctx.sync
+        sync = None
+        if ctx.sync is not None:
+            gs, key = ctx.sync
+            # deliver only when this forward was the parameters' ONLY use since the last wait():
+            # a module called twice has its gradients summed by autograd (AccumulateGrad) first
+            sync = gs if gs.sole_use(key) else None
         # the current stream is only looked up when a side stream is in play (host cost per call)
         cur = torch.cuda.current_stream(dout.device) if side is not None else None
         if sync is not None:  # hand the output projection's gradients to GradSync now: their
@@ -131,7 +140,6 @@ class AttnBlockFn(torch.autograd.Function):
             sync.deliver([(wc_, dwc), (bc_, dbc)], stream=side)
             dwc = dbc = None
         dk, dqv = SeqParallelAttention.backward(ctx.actx, do)[:2]
-        ctx.actx = None
         # the row-side weight gradient also runs beside the input-gradient GEMMs that follow
         # d[q|v] may be ready on the backward's priority stream (``_xdot_ready_on``): its weight
         # gradient runs there, under the row-side kernel (linear_backward)
@@ -152,10 +160,12 @@ class AttnBlockFn(torch.autograd.Function):
             dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], need_wqv, hq and (ng[6] or ng[8]))
         n = ctx.nq
         dwq = dwv = dbq = dbv = None
+        # the packed products cover both halves; hand back only what is asked for (a frozen
+        # queries weight next to a trained values weight gets None, and is never delivered)
         if dwqv is not None:
-            dwq, dwv = dwqv[:n], dwqv[n:]
+            dwq, dwv = (dwqv[:n] if ng[5] else None), (dwqv[n:] if ng[7] else None)
         if dbqv is not None:
-            dbq, dbv = dbqv[:n], dbqv[n:]
+            dbq, dbv = (dbqv[:n] if ng[6] else None), (dbqv[n:] if ng[8] else None)
         if sync is not None:
             sync.deliver([(wq_, dwq), (bq_, dbq), (wv_, dwv), (bv_, dbv)], stream=qv_on)
             sync.deliver([(wk_, dwk), (bk_, dbk)], stream=side)
@@ -165,5 +175,4 @@ class AttnBlockFn(torch.autograd.Function):
             for t in (dwc, dbc, dwk, dbk) + tuple(p.grad for p in ctx.params if p is not None and sync is not None):
                 if t is not None:
                     t.record_stream(cur)
-        ctx.params = ctx.sync = None
         return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None, None)

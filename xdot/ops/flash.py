@@ -204,18 +204,44 @@ def fp32_code(dtype: torch.dtype, mode: Optional[str] = None) -> int:
     return FP32_MODES[mode]
 
 
+def score_buffer_numel(B: int, H: int, R: int, T: int) -> int:
+    """Floats of the exact-fp32 score buffer: (B*H, ceil(R/32), ceil(T/32)) blocks of 32x32."""
+    return B * H * ((R + 31) // 32) * ((T + 31) // 32) * 1024
+
+
+def score_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tensor]:
+    """The exact-fp32 score buffer (``csrc/flash_f32.hip``, score-buffer mode) or None.
+
+    The forward stores every computed score tile there; the backward's column kernel reads S
+    instead of recomputing it and overwrites it with dS, which the row kernel reads: 6 fp32
+    products per step instead of 9 for 8 bytes of otherwise idle HBM traffic per score.  It is
+    R x T x H floats (20 GB at T = R = 25000, H = 8), so it is only taken when it fits within
+    ``XDOT_FP32_SCORES_FRAC`` of the memory free on the device (free + cached by torch); else
+    None and the kernels recompute (``XDOT_FP32_SCORES=0`` forces that)."""
+    if not FLAGS.fp32_scores:
+        return None
+    n = score_buffer_numel(B, H, R, T)
+    dev = torch.device(device)
+    free, _ = torch.cuda.mem_get_info(dev)
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    if 4 * n > FLAGS.fp32_scores_frac * (free + cached):
+        return None
+    return torch.empty(n, dtype=torch.float32, device=dev)
+
+
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
         scale: float, nsplit: int = 0, prescaled: bool = False,
-        fp32_mode: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """-> (out (B, R, H*D) in rows.dtype, lse (B, H, R) fp32 natural log).
 
     ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU).
     ``prescaled``: ``rows`` is :func:`prescale` output.  ``fp32_mode``: :func:`fp32_code`
-    (None: from ``XDOT_FP32_MODE``)."""
+    (None: from ``XDOT_FP32_MODE``).  ``sbuf``: exact fp32 only, a :func:`score_buffer` the
+    raw scores are stored into for :func:`bwd_cols` / :func:`bwd_rows`."""
     bits, flags = _mask_args(mk)
     fm = fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode)
     return _ext.ops().flash_fwd(rows.contiguous(), _kv(kc), _kv(vc), bits, flags, int(H), float(scale), int(nsplit),
-                                bool(prescaled), fm)
+                                bool(prescaled), fm, sbuf)
 
 
 def bwd_delta(dout: torch.Tensor, out: torch.Tensor, H: int) -> torch.Tensor:
@@ -230,38 +256,44 @@ def bwd_prep(dout: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, H: int):
 
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
              delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False,
-             lse2: Optional[torch.Tensor] = None, fp32_mode: Optional[int] = None):
+             lse2: Optional[torch.Tensor] = None, fp32_mode: Optional[int] = None,
+             sbuf: Optional[torch.Tensor] = None):
     """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
     ``delta`` (from :func:`bwd_delta`) is computed here when not given; with ``lse2`` too (both
     from :func:`bwd_prep`) no prep pass is launched here.  The grads are fp32
-    (``fp32_out``) or rounded once to the input dtype in the kernel epilogue."""
+    (``fp32_out``) or rounded once to the input dtype in the kernel epilogue.  ``sbuf``: the
+    forward's :func:`score_buffer`; S is read from it and it is OVERWRITTEN with dS for
+    :func:`bwd_rows` (run once per forward)."""
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
                                      bool(fp32_out), bool(prescaled), lse2,
-                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode))
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf)
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0,
-             prescaled: bool = False, fp32_mode: Optional[int] = None):
+             prescaled: bool = False, fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None):
     """Row-side grad (B, R, H*D) in rows.dtype.  ``nsplit`` 0: the launcher's occupancy model
-    (column splits so the row kernel fills the GPU; 1 measured 7 % / 32 % slower at N = 1 / 8)."""
+    (column splits so the row kernel fills the GPU; 1 measured 7 % / 32 % slower at N = 1 / 8).
+    ``sbuf``: the score buffer after :func:`bwd_cols` wrote dS into it (dK is then its only product)."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
                                      int(nsplit), bool(prescaled),
-                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode))
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf)
 
 
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,
         lse: torch.Tensor, mk: Optional[PackedMask], H: int, scale: float, prescaled: bool = False,
-        fp32_mode: Optional[int] = None):
+        fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None):
     """-> (d_rows (B, R, H*D) rows.dtype, d_kc, d_vc (B, T, H*D) fp32 partial grads).
 
     ``prescaled``: ``rows`` is :func:`prescale` output (the buffer the forward read); d_rows is
-    still the gradient of the unscaled rows."""
-    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode)
-    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode)
+    still the gradient of the unscaled rows.  ``sbuf``: the forward's score buffer (consumed)."""
+    dkv, delta = bwd_cols(dout, rows, kc, vc, out, lse, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode,
+                          sbuf=sbuf)
+    drows = bwd_rows(dout, rows, kc, vc, lse, delta, mk, H, scale, prescaled=prescaled, fp32_mode=fp32_mode,
+                     sbuf=sbuf)
     C = rows.shape[-1]
     return drows, dkv[..., :C], dkv[..., C:]

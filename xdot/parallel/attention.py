@@ -466,11 +466,26 @@ class SeqParallelAttention(torch.autograd.Function):
                 mask = mask.raw
         mask = getattr(mask, "raw", mask)
         segmented = n > 1 and (FLAGS.local_first or len(chunks) > 1)
+        sbuf = None
+        if use_hip and k.dtype == torch.float32 and fm == 0 and (len(chunks) == 1 or B == 1):
+            # exact fp32: score buffer (flash.score_buffer) when it fits: the backward then reads
+            # S / dS instead of recomputing them.  One kernel over the whole gathered side (in fp32
+            # the own-block-first segmentation hides < 5 % of a rank's forward)
+            sbuf = flash.score_buffer(B, H, R, n * qv.shape[1], k.device)
+            if sbuf is not None:
+                segmented = False
         if not segmented:
             if use_hip:
-                mk = packed_full if packed_full is not None else flash.prepare_mask_cached(mask, B, R, n * R)
-                qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
-                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mk, H, scale, prescaled=prescaled, fp32_mode=fm)
+                if len(chunks) > 1:  # several gather chunks, one buffer in (chunk, rank, row) order
+                    pending.wait_all()
+                    qvg = pending.permuted()
+                    mk = flash.prepare_mask_cached(mask, B, R, n * R, tag=("perm", tuple(chunks), n),
+                                                   view=_perm_cols(B, R, n, chunks))
+                else:
+                    mk = packed_full if packed_full is not None else flash.prepare_mask_cached(mask, B, R, n * R)
+                    qvg = flash.gathered_to_btc(pending.wait(0))     # (B, T, 2C), a view for B = 1
+                o, lse = flash.fwd(k, qvg[..., :C], qvg[..., C:], mk, H, scale, prescaled=prescaled, fp32_mode=fm,
+                                   sbuf=sbuf)
                 bufs, mks = [qvg], [mk]
             else:
                 qvg = pending.wait(0)                            # (N, B, R, 2C)
@@ -482,6 +497,7 @@ class SeqParallelAttention(torch.autograd.Function):
         ctx.save_for_backward(k, o, lse, *bufs)
         ctx.mks, ctx.mask, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, mask, chunks, H, scale, comm, use_hip
         ctx.prescaled, ctx.fp32_mode = prescaled, fm
+        ctx.sbuf = sbuf  # consumed (overwritten with dS) by the first backward
         return o
 
     @staticmethod
@@ -528,6 +544,10 @@ class SeqParallelAttention(torch.autograd.Function):
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
+            # score buffer: S -> dS in the column kernel, then dK from dS; a second backward through
+            # a retained graph recomputes (the buffer no longer holds S)
+            sbuf, ctx.sbuf = getattr(ctx, "sbuf", None), None
+            ev_cols = None
             with _on_stream(hi, cur):
                 delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
                 ev = _prep_event(hi.device)
@@ -541,7 +561,10 @@ class SeqParallelAttention(torch.autograd.Function):
                     g = bufs[0]
                     dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
                                             fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
-                                            fp32_mode=ctx.fp32_mode)
+                                            fp32_mode=ctx.fp32_mode, sbuf=sbuf)
+                    if sbuf is not None:  # the row kernel reads the dS this kernel wrote
+                        ev_cols = torch.cuda.Event()
+                        ev_cols.record(hi)
                     off = 0
                     for r0, rc in chunks:  # (chunk, rank, row) order: chunk c's ranks are contiguous
                         part = dkv if len(chunks) == 1 else dkv[:, off:off + n * rc]
@@ -562,12 +585,15 @@ class SeqParallelAttention(torch.autograd.Function):
                         outs.append(oc)
             # the row-side kernel starts as soon as δ exists: back to back measured slower at
             # every rank shape (profiles/r2_bwd_overlap.md)
-            cur.wait_event(ev)
+            cur.wait_event(ev if ev_cols is None else ev_cols)
             delta.record_stream(cur)
             if one:
                 g = bufs[0]
                 dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
-                                    nsplit=FLAGS.rows_split, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode)
+                                    nsplit=FLAGS.rows_split, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode,
+                                    sbuf=sbuf)
+                if sbuf is not None:
+                    sbuf.record_stream(cur)
             else:
                 ops = _ext.ops()
                 ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))

@@ -140,6 +140,7 @@ class GradSync:
         self._rest: List[torch.Tensor] = []
         self._attached = []
         self._dlv = set()  # ids of parameters whose gradient was delivered this round
+        self._uses = {}    # fused-module forwards since the last wait() (note_use / sole_use)
         if self.comm.world_size > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -162,6 +163,16 @@ class GradSync:
         finally:
             self._muted = prev
 
+    def note_use(self, key) -> None:
+        """A fused node's forward (``key``: its module) ran with gradients enabled."""
+        self._uses[key] = self._uses.get(key, 0) + 1
+
+    def sole_use(self, key) -> bool:
+        """Did ``key``'s module run exactly one forward since the last :meth:`wait`?  Only then
+        may its node :meth:`deliver` gradients itself; a second use (the module called twice in
+        one step) must leave the summing to autograd's AccumulateGrad."""
+        return self._uses.get(key, 0) == 1
+
     @torch.no_grad()
     def deliver(self, pairs, stream=None) -> None:
         """Gradients computed early inside a multi-parameter backward node: accumulate each
@@ -178,8 +189,8 @@ class GradSync:
                 else:
                     p.grad.add_(g)
             for p, g in pairs:
-                if g is not None:
-                    self._dlv.add(id(p))
+                if g is not None and id(p) in self._index:  # (a parameter outside the buckets is
+                    self._dlv.add(id(p))                   # accumulated, never reduced here)
                     self._on_grad(p, delivered=True)
 
     def _on_grad(self, p, delivered: bool = False):
@@ -281,6 +292,7 @@ class GradSync:
     def _reset(self):
         self._handles.clear()
         self._dlv = set()
+        self._uses = {}
         self._seen = [set() for _ in self.buckets]
         self._launched = [False] * len(self.buckets)
 

@@ -16,6 +16,9 @@ variable                    default   effect
 ``XDOT_ALLOW_TORCH_FALLBACK`` 0       let GPU ops fall back to torch when ``_C.so`` is absent
                                       (default: fail loudly)
 ``XDOT_EXT_PATH``           (in-tree) load this build of the extension instead of ``xdot/_C.so``
+                                      (skips the build-id check)
+``XDOT_AUTO_REBUILD``       1         an in-tree ``_C.so`` whose embedded build id differs from the
+                                      ``csrc/`` tree is rebuilt on load (0: raise instead)
 ``XDOT_COMM_TIMEOUT_S``     600       bound of every collective (process group timeout; also the
                                       default bound of the IPC kernels' device-side waits)
 ``XDOT_CHUNK_BUDGET_MB``    0 (auto)  transient-buffer budget of the chunk planner and of the
@@ -41,6 +44,10 @@ variable                    default   effect
                                       relative vs fp64: the reference's precision) or ``split``
                                       (opt-in, like TF32: hi/lo bf16 halves, 3 bf16 products:
                                       <= 9e-6 flash, <= 2e-5 GEMM; profiles/r3_fp32_split.md)
+``XDOT_FP32_SCORES``        1         exact fp32 flash: the forward stores the raw scores and the
+                                      backward reads S / dS instead of recomputing them (6 fp32
+                                      products per step instead of 9; needs R*T*H*4 bytes)
+``XDOT_FP32_SCORES_FRAC``   0.5       ... only when that fits this fraction of the free device memory
 ``XDOT_FUSED_MODULE``       1         the module's flash path as ONE autograd node (projections +
                                       attention + output projection, xdot/models/fused.py; 0: one
                                       node per op)
@@ -63,8 +70,9 @@ variable                    default   effect
 ``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
                                       (two xGMI links per hop), 16-bit accumulators  [collective]
 ``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
-``XDOT_GEMM_LIB`` (C++)     0         1: plain large products on hipBLASLt instead of the hand-written
-                                      MFMA GEMMs (``csrc/bindings.cpp``)
+``XDOT_GEMM_LIB`` (C++)     fp32      which plain large products may run on the library GEMM
+                                      (hipBLASLt, ``csrc/bindings.cpp``): unset = exact-fp32 ones only,
+                                      0 = none (every product on the xdot kernels), 1 = 16-bit too
 ``XDOT_GEMM3`` (C++)        1         16-bit products with M, N >= 256 and beta = 0 run the 8-phase
                                       16x16x32 kernel (``csrc/gemm3.hip``; 0: the 256x256 v2 kernel)
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
@@ -108,6 +116,7 @@ class _Flags:
         self.backend = _str("XDOT_BACKEND", "auto")
         self.allow_torch_fallback = _flag("XDOT_ALLOW_TORCH_FALLBACK")
         self.ext_path = os.environ.get("XDOT_EXT_PATH") or None
+        self.auto_rebuild = _flag("XDOT_AUTO_REBUILD", default="1")
         self.comm_timeout_s = _num("XDOT_COMM_TIMEOUT_S", 600.0)
         self.chunk_budget_mb = _num("XDOT_CHUNK_BUDGET_MB", 0.0)
         self.ops_schedule = _str("XDOT_OPS_SCHEDULE", "gather")
@@ -121,6 +130,8 @@ class _Flags:
         self.prescale = _flag("XDOT_PRESCALE", default="1")
         self.fp32_mode = _str("XDOT_FP32_MODE", "exact")
         self.mask_async = _flag("XDOT_MASK_ASYNC")
+        self.fp32_scores = _flag("XDOT_FP32_SCORES", default="1")
+        self.fp32_scores_frac = _num("XDOT_FP32_SCORES_FRAC", 0.5)
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _num("XDOT_PROJ", 1, int)
