@@ -72,6 +72,8 @@ def parse(argv=None):
                     help="also time this many steps of the same step in fp32 (the reference's precision; "
                          "0 = skip); reported as fp32_ms_per_step")
     ap.add_argument("--fp32-warmup", type=int, default=2)
+    ap.add_argument("--no-diagnostics", dest="diagnostics", action="store_false",
+                    help="N > 1: skip the post-timing breakdown (collectives alone, compute-only step)")
     ap.add_argument("--trace", action="store_true",
                     help="print stage / step progress with timestamps to stderr (diagnostics)")
     ap.add_argument("--graph", action="store_true",
@@ -242,6 +244,95 @@ def time_step(a, comm, dev, dt, steps, warmup, graph=False, profile_dir=None):
     return ms, (th - t0) * 1e3 / max(1, steps), lossv, impl
 
 
+def _max_over_ranks(comm, dev, v: float) -> float:
+    t = torch.tensor([v], dtype=torch.float64, device=dev if "gloo" not in comm.backend else "cpu")
+    comm.all_reduce(t, op="max")
+    return float(t.item())
+
+
+def multirank_diagnostics(a, comm, dev, dt, step_ms: float, impl: str, iters: int = 10) -> dict:
+    """N > 1, after the headline timing: what the step's time is made of.
+
+    * the step's own collectives alone, at the step's sizes and chunking: the [q|v] all-gather,
+      the [dq|dv] reduce-scatter (gradient wire dtype) and the per-parameter fp32 gradient
+      all-reduces; ms per step and nccl-tests bus bandwidth (all-gather / reduce-scatter:
+      bytes x (N-1)/N, all-reduce: x 2(N-1)/N);
+    * ``compute_only_ms``: the same per-rank step with an :class:`EmulatedComm` inside each
+      rank (collectives replaced by device copies of the same shapes: no transport);
+    * ``exposed_comm_ms`` = step - compute-only.
+    Every measurement is max over ranks; a failure becomes an ``*_error`` string, never an exit."""
+    from xdot.parallel.attention import _row_chunks
+    from xdot.utils.comm import EmulatedComm
+    from xdot.utils.env import FLAGS
+
+    n, rank = comm.world_size, comm.rank
+    R, C, B = a.seq_len // n, a.dim, a.batch
+    cuda = dev.type == "cuda"
+    out = {}
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        sync()
+        return _max_over_ranks(comm, dev, (time.perf_counter() - t0) * 1e3 / iters)
+
+    def record(name, fn, nbytes, factor):
+        try:
+            ms = timed(fn)
+            out[f"{name}_ms"] = round(ms, 4)
+            out[f"{name}_busbw_gbps"] = round(nbytes * factor / (ms * 1e-3) / 1e9, 2)
+        except Exception as e:  # noqa: BLE001
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"[:300]
+
+    chunks = _row_chunks(n, R, impl == "flash")
+    gdt = torch.float32 if (FLAGS.grad_fp32 or dt == torch.float32) else dt
+    try:
+        xs = [torch.randn(B, rc, 2 * C, device=dev).to(dt) for _, rc in chunks]
+        gbufs = [torch.empty(n, B, rc, 2 * C, device=dev, dtype=dt) for _, rc in chunks]
+        parts = [torch.randn(n, B, rc, 2 * C, device=dev).to(gdt) for _, rc in chunks]
+        rbufs = [torch.empty(B, rc, 2 * C, device=dev, dtype=gdt) for _, rc in chunks]
+        grads = [torch.randn(C, C, device=dev) for _ in range(4)]  # the 4 weights, fp32 reduce dtype
+    except Exception as e:  # noqa: BLE001
+        return {"diagnostics_error": f"{type(e).__name__}: {e}"[:300]}
+
+    def gather():
+        for x, g in zip(xs, gbufs):
+            comm.all_gather_into(g, x)
+
+    def rscatter():
+        for p_, r_ in zip(parts, rbufs):
+            comm.reduce_scatter(r_, p_)
+
+    def allreduce():
+        hs = [comm.all_reduce(g, op="sum", async_op=True) for g in grads]
+        for h in hs:
+            if h is not None:
+                h.wait()
+
+    f = (n - 1) / n
+    record("allgather_qv", gather, sum(g.nbytes for g in gbufs), f)
+    record("reduce_scatter_dqv", rscatter, sum(p_.nbytes for p_ in parts), f)
+    record("allreduce_grads", allreduce, sum(g.nbytes for g in grads), 2 * f)
+    del xs, gbufs, parts, rbufs, grads
+    try:
+        cms = time_step(a, EmulatedComm(n, rank), dev, dt, a.steps, a.warmup)[0]
+        cms = _max_over_ranks(comm, dev, cms)
+        out["compute_only_ms"] = round(cms, 4)
+        out["exposed_comm_ms"] = round(step_ms - cms, 4)
+    except Exception as e:  # noqa: BLE001
+        out["compute_only_error"] = f"{type(e).__name__}: {e}"[:300]
+    return out
+
+
 def _free_port() -> int:
     import socket
 
@@ -364,6 +455,11 @@ def main(argv=None, comm=None):
     _trace(a, "numerics check done")
     ms, host_ms, lossv, impl = time_step(a, comm, dev, dt, a.steps, a.warmup, graph=a.graph,
                                          profile_dir=a.profile_dir)
+    diag = {}
+    if n > 1 and not emulated and a.diagnostics:
+        _trace(a, "multi-rank diagnostics start")
+        diag = multirank_diagnostics(a, comm, dev, dt, ms, impl)
+        _trace(a, "multi-rank diagnostics done")
     fp32 = {}
     if a.fp32_steps > 0 and dt != torch.float32 and dev.type == "cuda":
         # the reference computes in fp32 only (module.py:60-71): time the same step in fp32 too,
@@ -419,6 +515,7 @@ def main(argv=None, comm=None):
             "local_first": bool(FLAGS.local_first),
             "numerics_check_max_rel_err": None if check_err is None else round(check_err, 5),
         }
+        rec.update(diag)
         if fp32:
             first = next(iter(fp32))
             rec["fp32_ms_per_step"] = round(fp32[first][0], 4)

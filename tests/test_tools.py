@@ -106,6 +106,14 @@ def test_bench_two_ranks_gloo(impl):
     assert recs[0]["n_gpus"] == 2 and recs[0]["config"]["parallelism"] == "sp2"
     assert recs[0]["world_size"] == 2 and recs[0]["transport"] == "gloo"
     assert recs[0]["numerics_check_max_rel_err"] < 1e-3
+    # the N>1 breakdown: collectives alone + the compute-only step
+    r = recs[0]
+    errs = {k: v for k, v in r.items() if k.endswith("_error")}
+    assert not errs, errs
+    for k in ("allgather_qv", "reduce_scatter_dqv", "allreduce_grads"):
+        assert r[f"{k}_ms"] > 0 and r[f"{k}_busbw_gbps"] > 0, k
+    assert r["compute_only_ms"] > 0
+    assert abs(r["exposed_comm_ms"] - (r["ms_per_step"] - r["compute_only_ms"])) < 1e-3
 
 
 def test_bench_mismatched_collective_knobs_raise():
