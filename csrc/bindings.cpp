@@ -476,7 +476,9 @@ FlashGeom flash_check(const at::Tensor& rows, const at::Tensor& kc, const at::Te
   TORCH_CHECK(g.ld % 8 == 0 && g.ld >= g.C, "xdot.flash: row stride must be a multiple of 8 elements");
   TORCH_CHECK(H > 0 && g.C % H == 0, "xdot.flash: C not divisible by heads");
   g.D = g.C / H;
-  TORCH_CHECK(g.D == 32 || g.D == 64 || g.D == 96 || g.D == 128, "xdot.flash: head dim must be 32/64/96/128");
+  TORCH_CHECK(g.D == 32 || g.D == 64 || g.D == 96 || g.D == 128 || g.D == 160 || g.D == 192 || g.D == 256 ||
+                  g.D == 384,
+              "xdot.flash: head dim must be 32/64/96/128 or (flash_wide.hip) 160/192/256/384");
   TORCH_CHECK(g.T < (1LL << 31) && g.R < (1LL << 31) && g.B * H * ((g.R + 127) / 128) * 8 < (1LL << 31), "xdot.flash: too large");
   TORCH_CHECK(aligned16(rows.data_ptr()) && aligned16(kc.data_ptr()) && aligned16(vc.data_ptr()), "xdot.flash: 16-byte alignment");
   const bool hb = bits.has_value() && bits->defined(), hf = flags.has_value() && flags->defined();
@@ -581,7 +583,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   const int rpw = xdot_flash_fwd_rows_per_wg();
   const int64_t NB = ((g.R + rpw - 1) / rpw) * g.B * H;
   int hw = 0, hr = 0, hs = 0;
-  const bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
+  const bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && g.D <= 128 && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
   const int ns = heavy ? hs : pick_split(NB, g.T, 512, nsplit);
   at::Tensor opart, lpart;
   if (heavy) {  // compact partials of the split tail blocks only

@@ -603,6 +603,18 @@ static void launch_bwd_rows(const BwdArgs& a, hipStream_t st) {
   if (dt == DT_F16 && D == 128) { CALL(DT_F16, 128); return 0; }                                 \
   return -1;
 
+// the D-templated helpers (prep, row-partial sum) also for the wide heads of flash_wide.hip
+#define XB_DISPATCH_W(CALL)                                                                      \
+  if (dt == DT_BF16 && D == 160) { CALL(DT_BF16, 160); return 0; }                               \
+  if (dt == DT_BF16 && D == 192) { CALL(DT_BF16, 192); return 0; }                               \
+  if (dt == DT_BF16 && D == 256) { CALL(DT_BF16, 256); return 0; }                               \
+  if (dt == DT_BF16 && D == 384) { CALL(DT_BF16, 384); return 0; }                               \
+  if (dt == DT_F16 && D == 160) { CALL(DT_F16, 160); return 0; }                                 \
+  if (dt == DT_F16 && D == 192) { CALL(DT_F16, 192); return 0; }                                 \
+  if (dt == DT_F16 && D == 256) { CALL(DT_F16, 256); return 0; }                                 \
+  if (dt == DT_F16 && D == 384) { CALL(DT_F16, 384); return 0; }                                 \
+  XB_DISPATCH(CALL)
+
 extern "C" int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int dt, int D,
                                            hipStream_t st) {
   using namespace xdot;
@@ -610,7 +622,7 @@ extern "C" int xdot_flash_bwd_delta_launch(const xdot::fa::BwdArgs* a, const voi
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
   if (dt == DT_F32) return xdot_flash_bwd_prep_f32_launch(a, out, delta, D, st);
 #define XP(DTV, DV) launch_bwd_delta<DTV, DV>(*a, out, delta, st)
-  XB_DISPATCH(XP)
+  XB_DISPATCH_W(XP)
 #undef XP
 }
 
@@ -618,6 +630,7 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (D > 128) return xdot_flash_wide_cols_launch(a, dt, D, st);  // dV pass + dQ pass
   if (dt == DT_F32) return a->fp32_mode ? xdot_flash_bwd_cols_x3_launch(a, D, st) : xdot_flash_bwd_cols_f32_launch(a, D, st);
 #define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
@@ -631,7 +644,7 @@ extern "C" int xdot_flash_bwd_rows_sum_launch(const xdot::fa::BwdArgs* a, int dt
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
   if (dt == DT_F32) return xdot_flash_rows_sum_f32_launch(a, D, st);
 #define XS(DTV, DV) launch_rows_sum<DTV, DV>(*a, st)
-  XB_DISPATCH(XS)
+  XB_DISPATCH_W(XS)
 #undef XS
 }
 
@@ -639,6 +652,11 @@ extern "C" int xdot_flash_bwd_rows_launch(const xdot::fa::BwdArgs* a, int dt, in
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (D > 128) {
+    const int rc = xdot_flash_wide_rows_launch(a, dt, D, st);
+    if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_bwd_rows_sum_launch(a, dt, D, st);
+    return rc;
+  }
   if (dt == DT_F32) {
     const int rc = a->fp32_mode ? xdot_flash_bwd_rows_x3_launch(a, D, st) : xdot_flash_bwd_rows_f32_launch(a, D, st);
     if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_rows_sum_f32_launch(a, D, st);

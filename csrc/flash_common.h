@@ -67,9 +67,13 @@ __device__ __forceinline__ u32x4 acc_to_frag(const f32x16& x, int s) {
 // the gfx950 LDS bank model (ds_read_b128: four 16-lane groups, ds_read_b64_tr_b16: two
 // 32-lane halves, banks (addr/4) % 64): both the row-operand reads and the transposed reads
 // below are conflict-free.
+// Wide heads (flash_wide.hip, D > 128): 2D bytes, + 64 unless ROW/4 is already 16 or 48 mod 64
+// dwords (the residues the bank analysis above holds for).
+constexpr int wide_row(int D) { return ((D / 2) % 64 == 16 || (D / 2) % 64 == 48) ? 2 * D : 2 * D + 64; }
 template <int D> struct Img {
-  static constexpr int ROW = (D == 32) ? 64 : (D == 64 || D == 96) ? 192 : 320;
+  static constexpr int ROW = (D == 32) ? 64 : (D == 64 || D == 96) ? 192 : (D == 128) ? 320 : wide_row(D);
   static constexpr int BYTES = 64 * ROW;  // one 64-row tile
+  static_assert((ROW / 4) % 64 == 16 || (ROW / 4) % 64 == 48, "image row residue");
 };
 template <int D>
 __device__ __forceinline__ int img_off(int row, int chunk) {

@@ -545,6 +545,8 @@ extern "C" int xdot_flash_fwd_combine_launch(const xdot::fa::FwdArgs* a, int dt,
 #define XF(DTV, DV) if (dt == DTV && D == DV) { launch_combine<DTV, DV>(*a, st); return 0; }
   XF(DT_BF16, 32) XF(DT_BF16, 64) XF(DT_BF16, 96) XF(DT_BF16, 128)
   XF(DT_F16, 32) XF(DT_F16, 64) XF(DT_F16, 96) XF(DT_F16, 128)
+  XF(DT_BF16, 160) XF(DT_BF16, 192) XF(DT_BF16, 256) XF(DT_BF16, 384)  // wide heads (flash_wide.hip)
+  XF(DT_F16, 160) XF(DT_F16, 192) XF(DT_F16, 256) XF(DT_F16, 384)
 #undef XF
   return -1;
 }
@@ -553,6 +555,14 @@ extern "C" int xdot_flash_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, 
   using namespace xdot;
   using namespace xdot::fa;
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (D > 128) {  // wide heads: csrc/flash_wide.hip (fp32: always exact)
+    const int rc = xdot_flash_wide_fwd_launch(a, dt, D, st);
+    if (rc == 0 && a->nsplit > 1 && !a->force_partial) {
+      if (dt == DT_F32) return xdot_flash_combine_f32_launch(a, D, st);
+      return xdot_flash_fwd_combine_launch(a, dt, D, st);
+    }
+    return rc;
+  }
   if (dt == DT_F32) {
     const int rc = a->fp32_mode ? xdot_flash_fwd_x3_launch(a, D, st) : xdot_flash_fwd_f32_launch(a, D, st);
     if (rc == 0 && a->nsplit > 1 && !a->force_partial) return xdot_flash_combine_f32_launch(a, D, st);

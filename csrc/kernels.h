@@ -214,6 +214,11 @@ int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, 
 int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+// wide head dims (csrc/flash_wide.hip): D = 160 / 192 / 256 / 384, 16-bit and exact fp32 (a wide
+// fp32 launch always runs exact); -1 = not a wide (dtype, D), -2 = needs the score buffer (fp32 D > 256)
+int xdot_flash_wide_fwd_launch(const xdot::fa::FwdArgs* a, int dt, int D, hipStream_t st);
+int xdot_flash_wide_rows_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
+int xdot_flash_wide_cols_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st);
 // split-bf16 fp32 family (csrc/flash_x3.hip, fp32_mode = 1); prep / combine / sum are shared
 int xdot_flash_fwd_x3_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st);
 int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);

@@ -40,9 +40,13 @@ from ..utils.env import FLAGS
 __all__ = ["seq_parallel_attention", "seq_parallel_attention_packed", "start_gather", "flash_supported",
            "SeqParallelAttention"]
 
-FLASH_HEAD_DIMS = (32, 64, 96, 128)
-# bf16/fp16: 32x32x16 MFMA kernels (csrc/flash_fwd.hip, flash_bwd.hip); fp32: exact-f32 MFMA
-# kernels (csrc/flash_f32.hip) — the reference's own precision without materialised scores
+# D <= 128: the tuned families (csrc/flash_fwd.hip, flash_bwd.hip, flash_f32.hip); 160-384: the
+# wide-head family (csrc/flash_wide.hip: the reference's example.py 768 / 2 heads = 384 and its
+# num_heads = 1 gradient test at 256).  Exact fp32 heads past 256 need the score buffer.
+FLASH_HEAD_DIMS = (32, 64, 96, 128, 160, 192, 256, 384)
+WIDE_F32_NEEDS_SCORES = 256
+# bf16/fp16: 32x32x16 MFMA kernels; fp32: exact-f32 MFMA kernels — the reference's own precision
+# without materialised scores
 FLASH_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
 
@@ -450,10 +454,11 @@ class SeqParallelAttention(torch.autograd.Function):
         prescaled = False
         fm = 0  # fp32 kernel family (XDOT_FP32_MODE), fixed at forward for the backward too
         packed_full = None  # the whole-row packed mask, when the caller packed it ahead
+        D = C // H
         if use_hip:
             from ..ops import flash
 
-            fm = flash.fp32_code(k.dtype)
+            fm = flash.fp32_code(k.dtype) if D <= 128 else 0  # wide fp32 heads are exact only
             # the row side pre-multiplied by scale*log2 e once (XDOT_PRESCALE, default on): the
             # forward and both backward kernels read this same buffer and seed their score
             # accumulators instead of scaling every score (saved in place of k for backward)
@@ -474,6 +479,14 @@ class SeqParallelAttention(torch.autograd.Function):
             sbuf = flash.score_buffer(B, H, R, n * qv.shape[1], k.device)
             if sbuf is not None:
                 segmented = False
+        if use_hip and k.dtype == torch.float32 and D > WIDE_F32_NEEDS_SCORES and sbuf is None:
+            # no kernel recomputes an fp32 head this wide (three D-wide register sets): the torch path
+            import warnings
+
+            warnings.warn(f"xdot: exact fp32 head dim {D} needs the flash score buffer, which does not fit; "
+                          "running the torch attention path", RuntimeWarning)
+            use_hip = False
+            fm = 0
         if not segmented:
             if use_hip:
                 if len(chunks) > 1:  # several gather chunks, one buffer in (chunk, rank, row) order

@@ -194,10 +194,12 @@ class RingAttention(torch.autograd.Function):
         check_consistent(comm, "ring_attention", k, qv, H)
         B, R, C = k.shape
         n = comm.world_size
-        from .attention import FLASH_DTYPES, FLASH_HEAD_DIMS
+        from .attention import FLASH_DTYPES, FLASH_HEAD_DIMS, WIDE_F32_NEEDS_SCORES
 
+        # (the ring has no score buffer: exact fp32 heads past 256 run the torch path)
         use_hip = (_ext.use_hip(k) and k.dtype in FLASH_DTYPES and qv.shape[-1] == 2 * C
-                   and C // H in FLASH_HEAD_DIMS)
+                   and C // H in FLASH_HEAD_DIMS
+                   and not (k.dtype == torch.float32 and C // H > WIDE_F32_NEEDS_SCORES))
         qv = qv.contiguous()
         rings = _Rings(comm, qv, _bidir())
         L = len(rings.lanes)
