@@ -201,3 +201,39 @@ def test_flash_wide_long_context_h2(gpu):
         dsc = pc * ((dO @ V[cj].t()) - delta[0, h][:, None])
         assert _rel(dkv[0, cj, C + h * D:C + (h + 1) * D], pc.t() @ dO) <= 3e-2
         assert _rel(dkv[0, cj, sl], scale * (dsc.t() @ Q)) <= 3e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cfg", [dict(key_dim=320, num_heads=4), dict(key_dim=64, value_dim=128, num_heads=1),
+                                 dict(key_dim=384, value_dim=192, num_heads=1)])
+def test_module_padded_heads_flash(gpu, dtype, cfg):
+    """Head dims no kernel takes (80), or a value width different from the key width (num_heads =
+    1, the reference's only such case: module.py:28-38) run the flash path on zero-padded heads
+    (flash_head_dim) and match the fp64 dense module."""
+    import xdot
+    from xdot.parallel.attention import flash_head_dim
+    from xdot.utils.comm import LocalComm, use_comm
+
+    T = 400
+    torch.manual_seed(1)
+    with use_comm(LocalComm()):
+        m = xdot.DistributedDotProductAttn(**cfg).to(gpu, dtype)
+        dk, dv = m.dim, m.value_dim // m.num_heads
+        assert flash_head_dim(dk, dv) not in (None, dk) or dk != dv
+        xk = torch.randn(1, T, cfg["key_dim"], device=gpu).to(dtype).requires_grad_(True)
+        xv = torch.randn(1, T, cfg.get("value_dim", cfg["key_dim"]), device=gpu).to(dtype).requires_grad_(True)
+        assert m._pick_impl(xk) == "flash"
+        ref = xdot.DistributedDotProductAttn(**cfg, distributed=False, impl="materialized",
+                                             backend="torch").to(gpu, torch.float64)
+        ref.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+        out = m(xk, xk, xv, None)
+        out.float().square().sum().backward()
+        xkd = xk.detach().double().requires_grad_(True)
+        xvd = xv.detach().double().requires_grad_(True)
+        ro = ref(xkd, xkd, xvd, None)
+        ro.square().sum().backward()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ro) <= tol
+    assert _rel(xk.grad, xkd.grad) <= 10 * tol and _rel(xv.grad, xvd.grad) <= 10 * tol
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad) <= 10 * tol, n

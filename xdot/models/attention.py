@@ -175,9 +175,21 @@ class DistributedDotProductAttn(nn.Module):
     def _forward(self, keys: Tensor, queries: Tensor, values: Tensor, attn_mask: Optional[Tensor]) -> Tensor:
         scale = 1.0 / math.sqrt(self.dim)
         if self._pick_impl(keys) == "flash":
+            from ..parallel import attention as pa
             from ..parallel.attention import seq_parallel_attention_packed, start_gather
 
             comm = (self.comm or _comm.get_comm()) if self.distributed else _comm.LocalComm()
+            H, dk, dv = self.num_heads, self.dim, self.value_dim // self.num_heads
+            Dp = pa.flash_head_dim(dk, dv) if keys.is_cuda else dk
+            if keys.is_cuda and Dp is not None and (Dp != dk or Dp != dv):
+                # head dims the kernels do not take (or value width != key width): every head
+                # zero-padded to the next kernel dim, same scale 1/sqrt(dk)
+                qv = self._project_qv(queries, values)
+                qv = torch.cat([pa.pad_heads(qv[..., :H * dk], H, dk, Dp), pa.pad_heads(qv[..., H * dk:], H, dv, Dp)],
+                               dim=-1)
+                k = pa.pad_heads(self._proj(self.keys, keys), H, dk, Dp)
+                o = seq_parallel_attention_packed(k, qv, attn_mask, H, scale, comm=comm)
+                return self._proj(self.composition, pa.unpad_heads(o, H, dv, Dp))
             if attn_mask is not None and attn_mask.is_cuda and attn_mask.dim() == 3 and FLAGS.mask_async:
                 # pack the mask on a side stream while the projection GEMMs run
                 from ..ops import flash

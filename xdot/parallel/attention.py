@@ -50,10 +50,37 @@ WIDE_F32_NEEDS_SCORES = 256
 FLASH_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
 
+def flash_head_dim(head_dim: int, v_head_dim: int) -> Optional[int]:
+    """The kernel head dim a (key, value) head pair runs at: itself when both are equal and a
+    kernel dim, else the smallest kernel dim holding both (heads zero-padded: zero key / query
+    columns add nothing to a score, zero value columns give zero outputs that are dropped), or
+    None past 384."""
+    m = max(head_dim, v_head_dim)
+    return next((d for d in FLASH_HEAD_DIMS if d >= m), None)
+
+
+def pad_heads(x: Tensor, H: int, d: int, Dp: int) -> Tensor:
+    """(B, R, H*d) -> (B, R, H*Dp), every head zero-padded from d to Dp columns (differentiable)."""
+    if d == Dp:
+        return x
+    B, R = x.shape[0], x.shape[1]
+    return torch.nn.functional.pad(x.reshape(B, R, H, d), (0, Dp - d)).reshape(B, R, H * Dp)
+
+
+def unpad_heads(x: Tensor, H: int, d: int, Dp: int) -> Tensor:
+    """(B, R, H*Dp) -> (B, R, H*d): the first d columns of every head."""
+    if d == Dp:
+        return x
+    B, R = x.shape[0], x.shape[1]
+    return x.reshape(B, R, H, Dp)[..., :d].reshape(B, R, H * d)
+
+
 def flash_supported(x: Tensor, head_dim: int, v_head_dim: int) -> bool:
+    """The flash kernels take this (dtype, device, head dims), directly or zero-padded
+    (:func:`flash_head_dim`)."""
     if not x.is_cuda or x.dtype not in FLASH_DTYPES:
         return False
-    if head_dim not in FLASH_HEAD_DIMS or v_head_dim != head_dim:
+    if flash_head_dim(head_dim, v_head_dim) is None:
         return False
     return _ext.use_hip(x) and hasattr(_ext.ops(), "flash_fwd")
 
