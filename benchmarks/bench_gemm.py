@@ -78,6 +78,27 @@ def main():
                                         a_mc=True, b_mc=True, path=pc)
             ref = lambda: torch.matmul(A.view(R, n, R).permute(1, 2, 0), B, out=C)
             flops = 2 * n * R * R * D
+        elif case in ("proj", "proj_dx", "wgrad"):  # the module's projections at T = 25000, d = 768
+            M, D = 25000, 768
+            if case == "proj":  # y = x Wᵀ
+                A = torch.randn(M, D, device=dev, dtype=dt)
+                B = torch.randn(D, D, device=dev, dtype=dt)
+                C = torch.empty(M, D, device=dev, dtype=dt)
+                ours = lambda: strided_gemm(A, B, C, M=M, N=D, K=D, lda=D, ldb=D, ldc=D, path=pc)
+                ref = lambda: torch.matmul(A, B.t(), out=C)
+            elif case == "proj_dx":  # dx = dy W
+                A = torch.randn(M, D, device=dev, dtype=dt)
+                B = torch.randn(D, D, device=dev, dtype=dt)
+                C = torch.empty(M, D, device=dev, dtype=dt)
+                ours = lambda: strided_gemm(A, B, C, M=M, N=D, K=D, lda=D, ldb=D, ldc=D, b_mc=True, path=pc)
+                ref = lambda: torch.matmul(A, B, out=C)
+            else:  # dW = dyᵀ x (K = rows)
+                A = torch.randn(M, D, device=dev, dtype=dt)
+                B = torch.randn(M, D, device=dev, dtype=dt)
+                C = torch.empty(D, D, device=dev, dtype=dt)
+                ours = lambda: strided_gemm(A, B, C, M=D, N=D, K=M, lda=D, ldb=D, ldc=D, a_mc=True, b_mc=True, path=pc)
+                ref = lambda: torch.matmul(A.t(), B, out=C)
+            flops = 2 * M * D * D
         else:
             raise SystemExit(f"unknown case {case}")
         t_ours = timeit(ours, a.iters, a.warmup)

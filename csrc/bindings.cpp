@@ -71,19 +71,26 @@ int64_t avail_elems(const at::Tensor& t) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // XDOT_GEMM_LIB: which plain large products may take the library GEMM (at::baddbmm ->
-// hipBLASLt) on in-place strided views.  fp32 (default) = exact-fp32 products only: the
-// library's fp32 GEMM runs at ~140 TF/s on the big square products vs 115 TF/s for the 128x128
-// exact kernel (profiles/r3_gemm3.md), and plain GEMMs are what the library is for; every
-// 16-bit product stays on the xdot kernels (gemm3 matches or beats the library there).
-// 0 = never (every product on the xdot kernels); 1 = 16-bit products too (round-2 route).
+// hipBLASLt) on in-place strided views.  Default (unset / 0) = none: 16-bit products run gemm3
+// (matches or beats the library), exact-fp32 products the 128x128 f32-MFMA kernel of
+// csrc/gemm_f32.hip.  "fp32" = exact-fp32 plain products on the library (the round-4 default,
+// kept for A/B); 1 = 16-bit products too (round-2 route).
 int gemm_lib() {
   static const int v = [] {
     const char* e = std::getenv("XDOT_GEMM_LIB");
-    if (e && e[0] == '0') return 0;
     if (e && e[0] == '1') return 2;
-    return 1;  // fp32 only
+    if (e && (e[0] == 'f' || e[0] == 'F')) return 1;  // fp32 only
+    return 0;
   }();
   return v;
+}
+
+// exact-fp32 products: the f32-MFMA kernel of csrc/gemm_f32.hip (fp32 out); anything else (an
+// fp32 -> 16-bit output) the generic kernel
+int gemm_exact(const xdot::GemmArgs* g, int batches, int dt_in, int dt_out, bool a_mc, bool b_mc, bool vec,
+               hipStream_t st) {
+  if (dt_in == xdot::DT_F32 && dt_out == xdot::DT_F32) return xdot_gemm_f32_launch(g, batches, a_mc, b_mc, vec, st);
+  return xdot_gemm_launch(g, batches, dt_in, dt_out, a_mc, b_mc, vec, st);
 }
 
 // The library route of xdot.gemm: true when it ran.  opA / opB / C are expressed as strided
@@ -354,8 +361,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
         gs.K = (int)Ks;
         const int full = (int)(K / Ks) == S ? (int)S : (int)S - 1;
         const bool vs = vec && (Ks * (a_mc ? lda : 1)) % eps == 0 && (Ks * (b_mc ? ldb : 1)) % eps == 0;
-        int rc1 = xdot_gemm_launch(&gs, full * (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vs,
-                                   cur_stream(A));
+        int rc1 = gemm_exact(&gs, full * (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vs,
+                             cur_stream(A));
         if (rc1 == 0 && full < S) {  // the short last slab
           xdot::GemmArgs gl = gs;
           const int64_t k0 = (int64_t)full * Ks;
@@ -364,7 +371,7 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
           gl.C = ws.data_ptr<float>() + (int64_t)full * nb2 * M * N;
           gl.K = (int)(K - k0);
           const bool vl = vs && (a_mc ? k0 * lda : k0) % eps == 0 && (b_mc ? k0 * ldb : k0) % eps == 0;
-          rc1 = xdot_gemm_launch(&gl, (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vl, cur_stream(A));
+          rc1 = gemm_exact(&gl, (int)nb2, dt_code(A.scalar_type()), xdot::DT_F32, a_mc, b_mc, vl, cur_stream(A));
         }
         TORCH_CHECK(rc1 == 0, "xdot.gemm: unsupported dtype combination ", A.scalar_type(), " -> fp32 slabs");
         check_launch(hipGetLastError(), "gemm (K slabs)");
@@ -375,8 +382,8 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
       }
     }
   }
-  const int rc = xdot_gemm_launch(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()),
-                                  dt_code(C.scalar_type()), a_mc, b_mc, vec, cur_stream(A));
+  const int rc = gemm_exact(&g, (int)(nb1 * nb2), dt_code(A.scalar_type()), dt_code(C.scalar_type()), a_mc, b_mc,
+                            vec, cur_stream(A));
   TORCH_CHECK(rc == 0, "xdot.gemm: unsupported dtype combination ", A.scalar_type(), " -> ", C.scalar_type());
   check_launch(hipGetLastError(), "gemm");
 }

@@ -153,6 +153,8 @@ struct Args {
 extern "C" {
 int xdot_gemm_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc,
                      int b_mc, int vec, hipStream_t st);
+// exact-fp32 GEMM (csrc/gemm_f32.hip): fp32 in / out, same arguments as xdot_gemm_launch
+int xdot_gemm_f32_launch(const xdot::GemmArgs* a, int batches, int a_mc, int b_mc, int vec, hipStream_t st);
 // 256x256 LDS-DMA 16-bit GEMM (csrc/gemm2.hip); splits > 1 needs ws: splits*batches*M*N fp32
 int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);

@@ -54,6 +54,13 @@ def _proj_ok(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
             and (bias is None or bias.dtype == x.dtype) and _ext.use_hip(x, weight))
 
 
+def _f32_ok(*ts) -> bool:
+    """Exact-fp32 products of a projection on csrc/gemm_f32.hip (through xdot.gemm): fp32 GPU
+    tensors, ``XDOT_FP32_MODE=exact``, ``XDOT_F32_PROJ`` on (the library's fp32 GEMM otherwise)."""
+    return (FLAGS.f32_proj and all(t is None or (t.dtype == torch.float32 and t.is_cuda) for t in ts)
+            and FLAGS.fp32_mode == "exact" and _ext.use_hip(*[t for t in ts if t is not None]))
+
+
 def _force() -> int:
     from ..utils.env import FLAGS
 
@@ -67,6 +74,19 @@ def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = N
     view to write, e.g. this rank's block of an all-gather buffer."""
     if _proj_ok(x, weight, bias):
         return _ext.ops().proj(x, weight, bias, False, out, _force(), float(alpha))
+    if _f32_ok(x, weight, bias):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) != 1 or x2.stride(0) != K:
+            x2 = x2.contiguous()
+        w = weight.contiguous()
+        M, N = x2.shape[0], w.shape[0]
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
+        if bias is not None:
+            y.copy_(bias.expand(M, N))  # C = alpha * x Wᵀ + alpha * bias
+        strided_gemm(x2, w, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=y.stride(0), alpha=alpha,
+                     beta=alpha if bias is not None else 0.0)
+        return y if out is not None else y.view(*x.shape[:-1], N)
     if out is None:
         y = F.linear(x, weight, bias)
         return y if alpha == 1.0 else y.mul_(alpha)
@@ -81,6 +101,12 @@ def proj_dx(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Input gradient ``dy · weight`` of ``F.linear`` for 2-D ``dy`` (M, N_out) -> (M, N_in)."""
     if _proj_ok(dy, weight):
         return _ext.ops().proj(dy, weight, None, True, None, _force(), 1.0)
+    if _f32_ok(dy, weight):
+        dy, w = dy.contiguous(), weight.contiguous()
+        M, K, N = dy.shape[0], dy.shape[1], w.shape[1]
+        out = torch.empty(M, N, dtype=dy.dtype, device=dy.device)
+        strided_gemm(dy, w, out, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, b_mc=True)
+        return out
     return dy @ weight
 
 
@@ -101,6 +127,12 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
     K, M = dy.shape
     N = x.shape[1]
     out_dtype = out_dtype or dy.dtype
+    if _f32_ok(dy, x) and out_dtype == torch.float32:
+        # exact fp32 on csrc/gemm_f32.hip; the long K (= rows) runs as K slabs + one ordered sum
+        dy, x = dy.contiguous(), x.contiguous()
+        out = torch.empty(M, N, dtype=torch.float32, device=dy.device)
+        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True)
+        return out
     if not native_wgrad(dy, x):
         ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else torch.promote_types(dy.dtype, x.dtype)
         return (dy.to(ct).t() @ x.to(ct)).to(out_dtype)
@@ -206,7 +238,7 @@ class LinearFn(torch.autograd.Function):
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``F.linear`` on the projection GEMM with the split-K MFMA weight gradient for bf16/fp16 GPU
     tensors."""
-    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dtype == weight.dtype \
+    if x.is_cuda and x.dtype == weight.dtype and (x.dtype in (torch.bfloat16, torch.float16) or _f32_ok(x, weight)) \
             and _ext.use_hip(x):
         if torch.is_grad_enabled():
             return LinearFn.apply(x, weight, bias)

@@ -62,6 +62,8 @@ variable                    default   effect
 ``XDOT_WGRAD_PAIR``         1         the fused backward's dWk and dW[q|v] in one launch (A/B knob)
 ``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
                                       launcher's occupancy model; A/B knob)
+``XDOT_F32_PROJ``           1         exact-fp32 projections / weight gradients on csrc/gemm_f32.hip
+                                      (0: the library's fp32 GEMM)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
                                       (1: where it beats the library, i.e. below 16384 rows;
                                       2: every eligible shape; 0: library)
@@ -135,6 +137,7 @@ class _Flags:
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _num("XDOT_PROJ", 1, int)
+        self.f32_proj = _flag("XDOT_F32_PROJ", default="1")
         self.inline_backward = _flag("XDOT_INLINE_BACKWARD", default="1")
         self.rows_split = _num("XDOT_ROWS_SPLIT", 0, int)
         self.wgrad_kernel = _flag("XDOT_WGRAD", default="1")
