@@ -138,6 +138,25 @@ __device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane)
 #pragma unroll
   for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
 }
+// The same through a wave-private 4-KiB LDS tile: the scatter goes to LDS (16 ds_write_b32, the
+// 2-way bank conflicts of which cost nothing), then the block leaves as 4 coalesced 16-byte global
+// stores per lane (64 lanes x 64 B contiguous) instead of 16 dword stores in 64-byte pieces.
+// XDOT_SB_DIRECT: the direct scatter (A/B).
+__device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x16& x, int lane) {
+#ifdef XDOT_SB_DIRECT
+  blk_store(blk, x, lane);
+#else
+  const int a = lane & 31, hf = lane >> 5;
+  float* p = wl + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
+  const f32x4* q = reinterpret_cast<const f32x4*>(wl + 16 * lane);
+  f32x4* d = reinterpret_cast<f32x4*>(blk + 16 * lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = q[i];
+#endif
+}
 __device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
   const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
   f32x16 x;
@@ -206,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
       f32x16 s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
-      if constexpr (SS) blk_store(sbw + (int64_t)kt * 1024, s, lane);  // raw S (rows past R: 0)
+      if constexpr (SS) blk_store_lds(sbw + (int64_t)kt * 1024, sm + 2 * CF::STAGE + wave * 1024, s, lane);  // raw S
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
@@ -464,8 +483,10 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     if (more) {
       st.load(kb, db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
+#ifndef XDOT_AB_NO_S_LOAD
       if constexpr (LS)
         if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
+#endif
     }
     const float* ki = sm + (rt & 1) * CF::STAGE;
     const float* di = ki + CF::IMG;
@@ -474,7 +495,11 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
       f32x16 s;
+#ifdef XDOT_AB_NO_S_LOAD
+      if constexpr (LS) s = f32x16{};
+#else
       if constexpr (LS) s = scur;                        // S  (row x col), stored by the forward
+#endif
       else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
       f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
       uint32_t w = 0;
@@ -488,7 +513,9 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
         s[r] = p;
         dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
       }
-      if constexpr (LS) blk_store(sbc + rt * sstep, dp, lane);  // dS in place of S (row-kernel order)
+#ifndef XDOT_AB_NO_DS_STORE
+      if constexpr (LS) blk_store_lds(sbc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS in place of S
+#endif
       trprod<D>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
     }
@@ -615,6 +642,8 @@ __global__ __launch_bounds__(256) void rows_sum_kernel(BwdArgs a, int D) {
 }
 
 template <int D> constexpr int lds_bytes() { return 2 * Cfg<D>::STAGE * 4; }
+// + one 4-KiB transpose tile per wave for the score-buffer stores (blk_store_lds)
+template <int D> constexpr int lds_bytes_sb() { return lds_bytes<D>() + 4 * 4096; }
 
 }  // namespace fa32
 }  // namespace xdot
@@ -634,7 +663,7 @@ extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipS
   const int nrb = (a->R + 127) / 128;
   const dim3 grid(nrb * a->B * a->H * a->nsplit);
   if (a->sbuf) {
-#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
     XF32_DISPATCH(L)
 #undef L
   }
@@ -681,7 +710,7 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
   if (a->sbuf) {
-#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
     XF32_DISPATCH(L)
 #undef L
   }

@@ -649,7 +649,8 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     raw_barrier();
   }
   if (!col_ok) return;
-  const float sc = DQ ? a.scale : 1.f;
+  // dQ = scale · Σ dSᵀ K; a pre-scaled K image holds K · scale · log2 e, so that factor is 1 / log2 e
+  const float sc = DQ ? (a.prescaled ? LN2 : a.scale) : 1.f;
   char* base = reinterpret_cast<char*>(DQ ? a.dkc : a.dvc);
   const int64_t eo = ((int64_t)b * a.T + col) * a.ldg + h * D;
 #pragma unroll
