@@ -150,6 +150,16 @@ __device__ __forceinline__ float pair_sum(float v) {
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// Pin MFMA accumulators to AGPRs (an empty asm with an "a" constraint).  Where accumulators and
+// operand fragments together exceed the 256 VGPRs, the allocator otherwise keeps loop-carried
+// accumulators in VGPRs and copies them into AGPRs around every product (2 VALU moves per
+// register per product) or spills.
+template <int N>
+__device__ __forceinline__ void pin_agpr(f32x16 (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+a"(x[i]));
+}
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();

@@ -98,29 +98,71 @@ __device__ __forceinline__ void load_frag(float (&f)[D / 2], const float* p, boo
   }
 }
 
-// acc += img rows (lane&31) · fragᵀ over the head dim (A from the image, B from registers)
+// acc += img rows (lane&31) · fragᵀ over the head dim (A from the image, B from registers).
+// The image reads run one 4-MFMA group ahead, fenced by sched_barrier: with one wave per SIMD a
+// read issued right before its MFMAs exposes the whole LDS latency (XDOT_F32_NOPIPE: unfenced).
 template <int D>
 __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D / 2], f32x16 acc, int lane) {
   const float* p = img + (lane & 31) * Cfg<D>::P + 4 * (lane >> 5);
+#ifdef XDOT_F32_NOPIPE
 #pragma unroll
   for (int g = 0; g < D / 8; ++g) {
     const f32x4 a = *reinterpret_cast<const f32x4*>(p + 8 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc = mm(a[t], f[4 * g + t], acc);
   }
+#else
+  f32x4 a0 = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+  for (int g = 0; g < D / 8; ++g) {
+    f32x4 a1 = a0;
+    if (g + 1 < D / 8) a1 = *reinterpret_cast<const f32x4*>(p + 8 * (g + 1));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = mm(a0[t], f[4 * g + t], acc);
+    __builtin_amdgcn_sched_barrier(0);
+    a0 = a1;
+  }
+#endif
   return acc;
 }
 
 // out[db] += imgᵀ (d x tile index) · x (tile index x lane column), x = an accumulator tile
+// (the A operands of tile index s+1 are read while the MFMAs of s issue)
 template <int D>
 __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16 (&out)[D / 32], int lane) {
   const int hf = lane >> 5;
+  constexpr int DB = D / 32;
+#ifdef XDOT_F32_NOPIPE
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
     const float* row = img + ((s & 3) + 8 * (s >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db) out[db] = mm(row[db * 32], x[s], out[db]);
+    for (int db = 0; db < DB; ++db) out[db] = mm(row[db * 32], x[s], out[db]);
   }
+#else
+  float r0[DB];
+  {
+    const float* row = img + 4 * hf * Cfg<D>::P + (lane & 31);
+#pragma unroll
+    for (int db = 0; db < DB; ++db) r0[db] = row[db * 32];
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    float r1[DB];
+    if (s + 1 < 16) {
+      const float* row = img + (((s + 1) & 3) + 8 * ((s + 1) >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) r1[db] = row[db * 32];
+    }
+#pragma unroll
+    for (int db = 0; db < DB; ++db) out[db] = mm(r0[db], x[s], out[db]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < 16) {
+#pragma unroll
+      for (int db = 0; db < DB; ++db) r0[db] = r1[db];
+    }
+  }
+#endif
 }
 
 // tile index of accumulator register r for lane half hf
@@ -369,6 +411,7 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
   f32x16 dk[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+  if constexpr (D >= 128) fa::pin_agpr(dk);  // one wave per SIMD: accumulators in AGPRs
 
   Stager<D> st;
   if (kt_beg < kt_end) {
@@ -400,6 +443,7 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
         s[r] = ex2(x) * (dp[r] - dlt);  // dSᵀ / scale
       }
       trprod<D>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+      if constexpr (D >= 128) fa::pin_agpr(dk);
     }
     if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
     __syncthreads();
@@ -420,9 +464,11 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
 // backward, gathered side: dQ_cols = scale · Σ_rows dSᵀ · K_rows, dV_cols = Σ_rows Pᵀ · dO.
 // 4 waves x 32 columns of one (b, h); sweeps 32-row tiles of K_rows / dO + their lse2 / δ.
 // LS (score-buffer mode): S comes from a.sbuf (prefetched one tile ahead) instead of the
-// K·Qᵀ product, and each block is overwritten with dS / scale for the row kernel.
+// K·Qᵀ product, each block is overwritten with dS / scale for the row kernel, and dV is left to
+// bwd_cols_dv_kernel (run first): without the dV accumulators this dQ pass fits two waves per
+// SIMD at D <= 96 (one wave per SIMD exposed every LDS / barrier stall: MFMA 54 % busy with both).
 template <int D, bool LS>
-__global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -456,9 +502,17 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
   const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
   const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
-  f32x16 dq[DB], dv[DB];
+  f32x16 dq[DB], dv[LS ? 1 : DB];
 #pragma unroll
-  for (int i = 0; i < DB; ++i) { dq[i] = f32x16{}; dv[i] = f32x16{}; }
+  for (int i = 0; i < DB; ++i) dq[i] = f32x16{};
+  if constexpr (!LS) {
+#pragma unroll
+    for (int i = 0; i < DB; ++i) dv[i] = f32x16{};
+    // loop-carried accumulators live in AGPRs (unpinned they sit in VGPRs and are copied into
+    // AGPRs and back around every trprod: ~4 VALU moves per MFMA, VALU/MFMA 4.3 measured)
+    fa::pin_agpr(dq);
+    fa::pin_agpr(dv);
+  }
 
   // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
   auto aux_load = [&](int rt) -> float {
@@ -516,8 +570,12 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
 #ifndef XDOT_AB_NO_DS_STORE
       if constexpr (LS) blk_store_lds(sbc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS in place of S
 #endif
-      trprod<D>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
-      trprod<D>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+      if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
+      trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
+      if constexpr (!LS) {
+        fa::pin_agpr(dq);
+        fa::pin_agpr(dv);
+      }
     }
     if (more) {
       float* nx = sm + ((rt + 1) & 1) * CF::STAGE;
@@ -536,8 +594,9 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     for (int g = 0; g < 4; ++g) {
       *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) =
           f32x4{dq[db][4 * g] * sc, dq[db][4 * g + 1] * sc, dq[db][4 * g + 2] * sc, dq[db][4 * g + 3] * sc};
-      *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
-          f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+      if constexpr (!LS)
+        *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
+            f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
     }
 }
 
@@ -631,6 +690,92 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
           f32x4{dk[db][4 * g] * sc, dk[db][4 * g + 1] * sc, dk[db][4 * g + 2] * sc, dk[db][4 * g + 3] * sc};
 }
 
+// ------------------------------------------------------------------------------------------
+// backward, gathered side in score-buffer mode, pass 1 of 2: dV_cols = Σ_rows Pᵀ · dO with P
+// recomputed elementwise from the stored S (the dV product is the only one: a third of the
+// column work, no V / K traffic).  Runs BEFORE bwd_cols_kernel<D, true>, which overwrites S with
+// dS.  Same grid as the column kernel; stage = dO image + lse2[32].
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  constexpr int DB = CF::DB, STG = CF::IMG + 32;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = (a.T + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = lin % ncb, bh = lin / ncb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
+  const bool col_ok = col < a.T, sown = c0 < a.T;
+  const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
+  const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024;
+  const int64_t sstep = (int64_t)NKT32 * 1024;
+  const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
+  const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dv[i] = f32x16{};
+  auto aux_load = [&](int rt) -> float {  // lse2 (+inf past R: P = 0), threads 0..31
+    const int rr = rt * 32 + tid;
+    return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
+  };
+  Stager1<D> st;
+  f32x16 snext{};
+  float ax = 0.f;
+  if (NRT > 0) {
+    st.load(db_, C, 0, a.R - 1, tid);
+    ax = aux_load(0);
+    if (sown) snext = blk_load(sbc, lane);
+    st.store(sm, tid);
+    if (tid < 32) sm[CF::IMG + tid] = ax;
+    __syncthreads();
+  }
+  for (int rt = 0; rt < NRT; ++rt) {
+    const bool more = rt + 1 < NRT;
+    f32x16 s = snext;
+    if (more) {
+      st.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      ax = aux_load(rt + 1);
+      if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
+    }
+    const float* di = sm + (rt & 1) * STG;
+    const float* ls = di + CF::IMG;
+    int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      uint32_t w = 0;
+      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = tidx(r, hf);
+        float x = __builtin_fmaf(s[r], c2, -ls[i]);
+        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
+        s[r] = ex2(x);
+      }
+      trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
+    }
+    if (more) {
+      float* nx = sm + ((rt + 1) & 1) * STG;
+      st.store(nx, tid);
+      if (tid < 32) nx[CF::IMG + tid] = ax;
+    }
+    __syncthreads();
+  }
+  if (!col_ok) return;
+  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+}
+
 // sum a.nsplit slots of a.dpart into the fp32 row-side grad
 __global__ __launch_bounds__(256) void rows_sum_kernel(BwdArgs a, int D) {
   const int64_t total4 = (int64_t)a.B * a.R * a.H * D / 4;
@@ -709,8 +854,10 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
-  if (a->sbuf) {
-#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
+  if (a->sbuf) {  // dV from S first, then dQ (S -> dS in place)
+#define L(DV)                                                                                              \
+  hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a);        \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
     XF32_DISPATCH(L)
 #undef L
   }

@@ -36,18 +36,13 @@ using fa::pair_max;
 using fa::pair_sum;
 using fa::wait_vm;
 using fa::raw_barrier;
+using fa::pin_agpr;
 
 __device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
-// Pin output accumulators to AGPRs.  A wide head's D/2 accumulator registers plus its D/4..D/2
-// fragment registers exceed the 256 VGPRs; left alone the allocator keeps the accumulators in
-// VGPRs (the online-softmax rescale is VALU work on them) and spills.  Pinned, only that rare
-// rescale moves them through VGPRs.
-template <int N>
-__device__ __forceinline__ void pin_agpr(f32x16 (&x)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) asm volatile("" : "+a"(x[i]));
-}
+// Output accumulators are pinned to AGPRs (fa::pin_agpr): a wide head's D/2 accumulator
+// registers plus its D/4..D/2 fragment registers exceed the 256 VGPRs; left alone the allocator
+// keeps the accumulators in VGPRs (the online-softmax rescale is VALU work on them) and spills.
 // the first NA elements of a fragment array to AGPRs too (MFMA reads A/B operands from AGPRs):
 // what the accumulators leave of the 256 AGPRs takes the fragments' overflow past the VGPRs
 template <int NA, class F, int N>

@@ -356,6 +356,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
   f32x16 dk[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+  fa::pin_agpr(dk);  // loop-carried: AGPR-resident, no per-product copies
 
   Tile<D> tq, tv;
   if (kt_beg < kt_end) {
@@ -392,6 +393,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
         s[r] = ex2(x) * (dp[r] - dlt);  // dSᵀ / scale
       }
       trprod<D, true, true>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
+      fa::pin_agpr(dk);
     }
     if (more) {
       char* nx = smem + ((kt + 1 - kt_beg) & 1) * RL::STAGE;
@@ -458,6 +460,8 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     dq[i] = f32x16{};
     dv[i] = f32x16{};
   }
+  fa::pin_agpr(dq);  // loop-carried: AGPR-resident, no per-product copies
+  fa::pin_agpr(dv);
 
   // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
   auto aux_load = [&](int rt) -> float {
@@ -508,6 +512,8 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
       }
       trprod<D, true, true>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
       trprod<D, true, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+      fa::pin_agpr(dq);
+      fa::pin_agpr(dv);
     }
     if (more) put(smem + ((rt + 1) & 1) * KL::STAGE, tk, td, ax);
     __syncthreads();

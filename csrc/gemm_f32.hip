@@ -11,7 +11,7 @@
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (4 waves 2x2, each 64x64 = 2x2 blocks of
 // 32x32), K tiles of 32, staged global -> VGPR -> LDS (double-buffered, one barrier per K tile;
-// the next tile's global loads fly under the current tile's 64 MFMAs = 4096 cycles per wave).
+// global loads run two K tiles ahead in two register sets, ~8192 MFMA cycles per wave in flight).
 // A K tile's 16 MFMA k-steps pair k = s (lane half 0) with k = 16 + s (lane half 1) for both
 // operands.  Images keep the global storage order (coalesced loads, conflict-free 16-byte LDS
 // writes): a k-contiguous operand as [mn][32 + 4 k] (a lane's 4 k-steps are one ds_read_b128;
@@ -38,9 +38,28 @@ __device__ __forceinline__ f32x16 mm(float a, float b, const f32x16& c) {
 // One operand tile (128 mn x 32 k) global -> registers: 4 x 16 B per thread.
 //   k-contiguous (MC = false): thread loads 4 consecutive k of one mn row;
 //   mn-contiguous (MC = true): thread loads 4 consecutive mn of one k row.
+// Interior K tiles of 16-byte-aligned operands (VEC, k0 + BK <= K: wave-uniform) load without
+// per-element predicates: mn positions past MN only feed outputs that are never stored, so they
+// read a clamped valid address instead of zeros (an mn-contiguous chunk that starts below MN ends
+// inside its ld row: ld % 4 == 0 under VEC).  Only the K-tail tile zero-fills element by element.
 template <bool MC, bool VEC>
 __device__ __forceinline__ void load_tile(f32x4 (&r)[4], const float* __restrict__ base, int64_t ld, int mn0, int MN,
                                           int k0, int K, int tid) {
+  if (VEC && k0 + BK <= K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = tid + NT * i;
+      if (!MC) {
+        const int gm = min(mn0 + (v >> 3), MN - 1);
+        r[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)gm * ld + k0 + (v & 7) * 4);
+      } else {
+        int gm = mn0 + (v & 31) * 4;
+        gm = gm < MN ? gm : 0;
+        r[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)(k0 + (v >> 5)) * ld + gm);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int v = tid + NT * i;  // 0..1023
@@ -98,7 +117,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
   const int ntile = p.tiles_m * p.tiles_n;
   const int t_lin = xcd_remap(blockIdx.x, gridDim.x);
   if (t_lin >= ntile) return;
-  const int tile_m = t_lin / p.tiles_n, tile_n = t_lin % p.tiles_n;
+  // groups of GM tile rows walked column-major: an XCD's concurrent tiles share GM A panels and
+  // a few B panels in its L2 instead of streaming a fresh B panel per tile
+  constexpr int GM = 8;
+  const int gsz = GM * p.tiles_n, first_m = (t_lin / gsz) * GM;
+  const int gm_n = min(GM, p.tiles_m - first_m);
+  const int tile_m = first_m + (t_lin % gsz) % gm_n, tile_n = (t_lin % gsz) / gm_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int z = blockIdx.y, z1 = z / p.nb2, z2 = z % p.nb2;
   const float* A = reinterpret_cast<const float*>(p.A) + z1 * p.sA1 + z2 * p.sA2;
@@ -112,29 +136,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
-  f32x4 ra[4], rb[4];
-  auto load = [&](int t) {
-    const int seg = t / ktiles, k0 = (t % ktiles) * BK;
-    gf32::load_tile<A_MC, VEC>(ra, A + seg * p.sAseg, p.lda, m0, p.M, k0, p.K, tid);
-    gf32::load_tile<B_MC, VEC>(rb, B + seg * p.sBseg, p.ldb, n0, p.N, k0, p.K, tid);
-  };
-  auto store = [&](int buf) {
-    float* s = smf + buf * STAGE;
-    gf32::store_tile<A_MC>(s, ra, tid);
-    gf32::store_tile<B_MC>(s + IMG, rb, tid);
-  };
-  if (ntiles > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
   const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);  // + 32 i: the lane's fragment rows
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) load(t + 1);
+  // 16 k-steps of one LDS stage: 4 groups of 4, operand reads one group ahead
+  auto compute = [&](int cur) {
     const float* sa = smf + cur * STAGE;
     const float* sb = sa + IMG;
-    // 4 groups of 4 k-steps; operand reads one group ahead
     f32x4 a0[2], b0[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -164,9 +170,56 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
         b0[i] = b1[i];
       }
     }
-    if (t + 1 < ntiles) store(cur ^ 1);
+  };
+  struct Regs {
+    f32x4 a[4], b[4];
+  };
+  auto load = [&](Regs& r, int t) {
+    const int seg = t / ktiles, k0 = (t % ktiles) * BK;
+    gf32::load_tile<A_MC, VEC>(r.a, A + seg * p.sAseg, p.lda, m0, p.M, k0, p.K, tid);
+    gf32::load_tile<B_MC, VEC>(r.b, B + seg * p.sBseg, p.ldb, n0, p.N, k0, p.K, tid);
+  };
+  auto store = [&](const Regs& r, int buf) {
+    float* s = smf + buf * STAGE;
+    gf32::store_tile<A_MC>(s, r.a, tid);
+    gf32::store_tile<B_MC>(s + IMG, r.b, tid);
+  };
+#ifdef XDOT_GF32_PF1
+  Regs r0;
+  if (ntiles > 0) {
+    load(r0, 0);
+    store(r0, 0);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load(r0, t + 1);
+    compute(t & 1);
+    if (t + 1 < ntiles) store(r0, (t + 1) & 1);
     __syncthreads();
   }
+#else
+  // Global loads run TWO K tiles ahead (two register sets): a tile's loads get ~2 x 4096 MFMA
+  // cycles to land instead of one, which at one WG pair per CU is less than an HBM round trip
+  // under load.  Tile t computes from LDS stage t & 1 while set (t & 1) fetches tile t + 2; the
+  // set holding tile t + 1 then fills the other stage.
+  Regs r0, r1;
+  if (ntiles > 0) {
+    load(r0, 0);
+    store(r0, 0);
+    if (ntiles > 1) load(r1, 1);
+  }
+  __syncthreads();
+  auto step = [&](int t, Regs& mine, Regs& next) {
+    if (t + 2 < ntiles) load(mine, t + 2);
+    compute(t & 1);
+    if (t + 1 < ntiles) store(next, (t + 1) & 1);
+    __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, r0, r1);
+    if (t + 1 < ntiles) step(t + 1, r1, r0);
+  }
+#endif
 
   // epilogue: register r of block (i, j) = row wm*64 + 32i + (r&3) + 8(r>>2) + 4hf, column
   // wn*64 + 32j + (lane & 31)

@@ -2,7 +2,7 @@
 # Round 5 pass 4: score-buffer store variants (A/B via XDOT_EXT_PATH), fp32 GEMM PMC, remaining tests.
 set -o pipefail
 OUT=gpurun_out/r5s4; mkdir -p $OUT
-for v in "" _sbdirect _nods _nosload; do
+for v in "" _nopipe _sbdirect _nods _nosload; do
   XDOT_EXT_PATH=xdot/_C$v.so timeout -k 10 200 python benchmarks/bench_flash.py --dtype fp32 --fp32-mode exact --iters 5 --scores > $OUT/scores$v.log 2>&1 || exit $?
 done
 timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread \

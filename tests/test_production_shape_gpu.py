@@ -45,14 +45,14 @@ def test_flash_n1_production_shape_sampled(gpu, dtype):
         delta, lse2 = flash.bwd_prep(do, out, lse, H)
         dkv, _ = flash.bwd_cols(do, rows, kc, vc, out, lse, None, H, scale, delta, lse2=lse2, fp32_mode=0, sbuf=sb)
         drows = flash.bwd_rows(do, rows, kc, vc, lse, delta, None, H, scale, fp32_mode=0, sbuf=sb)
-        tol = dict(o=1e-5, dr=2e-5, dc=2e-5)  # fp32 sums over 25000 columns
+        tol = dict(o=1e-5, dr=2e-5, dc=2e-5, lse=1e-4)  # fp32 sums over 25000 columns
     else:
         rk = flash.prescale(rows, scale)
         out, lse = flash.fwd(rk, kc, vc, None, H, scale, prescaled=True)
         delta, lse2 = flash.bwd_prep(do, out, lse, H)
         dkv, _ = flash.bwd_cols(do, rk, kc, vc, out, lse, None, H, scale, delta, prescaled=True, lse2=lse2)
         drows = flash.bwd_rows(do, rk, kc, vc, lse, delta, None, H, scale, prescaled=True)
-        tol = dict(o=2e-2, dr=3e-2, dc=3e-2)
+        tol = dict(o=2e-2, dr=3e-2, dc=3e-2, lse=5e-3)  # bf16-rounded prescaled rows
     torch.cuda.synchronize()
     for h in range(H):
         sl = slice(h * D, (h + 1) * D)
@@ -63,7 +63,7 @@ def test_flash_n1_production_shape_sampled(gpu, dtype):
         p = torch.exp(s - lse_ref[:, None])
         o_ref = p @ V
         assert _rel(out[0, ri, sl], o_ref) <= tol["o"], f"head {h} out"
-        assert (lse[0, h, ri].double() - lse_ref).abs().max().item() < 1e-3
+        assert (lse[0, h, ri].double() - lse_ref).abs().max().item() < tol["lse"]
         dref = (dO[ri] * o_ref).sum(-1)
         ds = p * ((dO[ri] @ V.t()) - dref[:, None])
         assert _rel(drows[0, ri, sl], scale * (ds @ K)) <= tol["dr"], f"head {h} d rows"
@@ -71,7 +71,7 @@ def test_flash_n1_production_shape_sampled(gpu, dtype):
         sc = (Q @ K[cj].t()) * scale                                       # (R, 24)
         lse_all = torch.logsumexp((Q @ K.t()) * scale, -1) if h == 0 else None
         if lse_all is not None:  # the LSE of every row, once (head 0): the kernel's own
-            assert (lse[0, 0].double() - lse_all).abs().max().item() < 1e-3
+            assert (lse[0, 0].double() - lse_all).abs().max().item() < tol["lse"]
         pc = torch.exp(sc - lse[0, h].double()[:, None])
         dsc = pc * ((dO @ V[cj].t()) - delta[0, h].double()[:, None])
         assert _rel(dkv[0, cj, C + h * D:C + (h + 1) * D], pc.t() @ dO) <= tol["dc"], f"head {h} dv"
