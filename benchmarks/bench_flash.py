@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--no-prescale", action="store_true",
                     help="kernels scale every score (default: pre-scaled rows + seeded accumulators, the module's path)")
     ap.add_argument("--scores", action="store_true",
-                    help="exact fp32: score-buffer mode (forward stores S, bwd_cols reads S and writes dS, "
+                    help="fp32 (exact or split): score-buffer mode (forward stores S, bwd_cols reads S and writes dS, "
                          "bwd_rows reads dS; products 2 / 3 / 1 instead of 2 / 4 / 3)")
     ap.add_argument("--torch", action="store_true", help="also time torch SDPA (aotriton) on the same shape")
     ap.add_argument("--concurrent", action="store_true",
@@ -86,7 +86,7 @@ def main():
     rk = flash.prescale(rows, scale) if ps else rows
     sb = None
     if a.scores:
-        assert dt == torch.float32, "--scores is an exact-fp32 mode"
+        assert dt == torch.float32, "--scores is an fp32 (exact or split) mode"
         sb = flash.score_buffer(B, H, R, T, dev)
         assert sb is not None, "score buffer does not fit"
     # (timing only: after the first bwd_cols the buffer holds dS, which later calls read as S)

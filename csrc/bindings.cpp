@@ -293,6 +293,29 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
       gemm_library(A, B, C, M, N, K, nseg, nb1, nb2, lda, ldb, ldc, sA1, sA2, sB1, sB2, sC1, sC2, sAseg, sBseg, a_mc,
                    b_mc, alpha, beta))
     return;
+  // exact fp32: the persistent 256x256 LDS-DMA kernel (csrc/gemm2_f32.hip) where its layout rules
+  // hold and the output has at least one 128-wide tile in each direction; split-K
+  // (pick_splits over 32-deep k-tiles, partials <= 512 MB) when the tiles alone leave CUs idle.
+  // path 1 keeps the 128x128 kernel, path 2 forces this one.
+  if (A.scalar_type() == at::kFloat && C.scalar_type() == at::kFloat && vec && K > 0 && mode != 1) {
+    const bool ok = (a_mc || K % 4 == 0) && (b_mc || K % 4 == 0) && (!a_mc || M % 4 == 0) && (!b_mc || N % 4 == 0);
+    TORCH_CHECK(mode != 2 || ok, "xdot.gemm: path 2 (fp32 v2) needs K % 4 == 0 for k-contiguous operands and "
+                                 "an mn extent % 4 == 0 for mn-contiguous ones");
+    if (ok && (mode == 2 || (M >= 128 && N >= 128))) {
+      const int64_t nb = nb1 * nb2;
+      const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb;
+      int64_t S = pick_splits(tiles, nseg * ((K + 31) / 32));
+      while (S > 1 && S * nb * M * N > (128LL << 20)) --S;
+      at::Tensor ws;
+      if (S > 1) ws = at::empty({S * nb * M * N}, A.options().dtype(at::kFloat));
+      const int rc = xdot_gemm2_f32_launch(&g, (int)nb, a_mc, b_mc, (int)S, S > 1 ? ws.data_ptr<float>() : nullptr,
+                                           cur_stream(A));
+      if (rc == 0) {
+        check_launch(hipGetLastError(), "gemm2_f32");
+        return;
+      }
+    }
+  }
   const bool half = A.element_size() == 2;
   bool v2 = half && vec && mode != 1;
   if (v2 && (!a_mc || !b_mc)) v2 = K % 8 == 0;
@@ -565,12 +588,14 @@ bool head_heavy_plan(int64_t NB, int64_t T, int* whole, int* rem, int* split) {
   return true;
 }
 
-// exact-fp32 score buffer (flash_f32.hip): (B*H, ceil(R/32), ceil(T/32)) blocks of 1024 floats
+// fp32 score buffer (flash_f32.hip exact, flash_x3.hip split): (B*H, ceil(R/32), ceil(T/32)) blocks
+// of 1024 floats
 float* sbuf_ptr(const c10::optional<at::Tensor>& sbuf, const FlashGeom& g, int64_t H, const at::Tensor& rows,
                 int64_t fp32_mode, const char* what) {
   if (!sbuf.has_value() || !sbuf->defined()) return nullptr;
   const auto& t = *sbuf;
-  TORCH_CHECK(rows.scalar_type() == at::kFloat && fp32_mode == 0, what, ": the score buffer is an exact-fp32 feature");
+  TORCH_CHECK(rows.scalar_type() == at::kFloat && (fp32_mode == 0 || fp32_mode == 1), what,
+              ": the score buffer is an fp32 (exact or split) feature");
   const int64_t need = g.B * H * ((g.R + 31) / 32) * ((g.T + 31) / 32) * 1024;
   TORCH_CHECK(t.is_cuda() && t.device() == rows.device() && t.scalar_type() == at::kFloat && t.is_contiguous() &&
                   t.numel() == need && aligned16(t.data_ptr()),

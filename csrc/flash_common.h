@@ -150,6 +150,94 @@ __device__ __forceinline__ float pair_sum(float v) {
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// tile index of accumulator register r for lane half hf
+__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
+
+// Score-buffer block I/O (exact-fp32 / split-bf16 / wide flash families, kernels.h BwdArgs::sbuf).  A 32x32 accumulator x holds element (a, b) with a = lane & 31 (lane
+// index) and b = tidx(r, lane >> 5) (register r).  blk_store writes it TRANSPOSED into the
+// reader's accumulator order: element (a, b) to [lane' = b + 32((a>>2)&1)][r' = (a&3) + 4(a>>3)],
+// i.e. the reader whose lane index is b finds it in its register r' -> blk_load(blk, lane)[r'].
+// (forward: a = row, b = column -> the column kernel's order; column kernel: a = column,
+// b = row -> the row kernel's order.)  Per lane 16 scattered dword stores / 4 b128 loads.
+__device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane) {
+  const int a = lane & 31, hf = lane >> 5;
+  float* p = blk + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
+}
+// The same through a wave-private 4-KiB LDS tile: the scatter goes to LDS (16 ds_write_b32, the
+// 2-way bank conflicts of which cost nothing), then the block leaves as 4 coalesced 16-byte global
+// stores per lane (64 lanes x 64 B contiguous) instead of 16 dword stores in 64-byte pieces.
+// XDOT_SB_DIRECT: the direct scatter (A/B).
+__device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x16& x, int lane) {
+#ifdef XDOT_SB_DIRECT
+  blk_store(blk, x, lane);
+#else
+  const int a = lane & 31, hf = lane >> 5;
+  float* p = wl + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
+  const f32x4* q = reinterpret_cast<const f32x4*>(wl + 16 * lane);
+  f32x4* d = reinterpret_cast<f32x4*>(blk + 16 * lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = q[i];
+#endif
+}
+__device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
+  f32x16 x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 v = p[q];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) x[4 * q + t] = v[t];
+  }
+  return x;
+}
+
+// flag of (32-row block rb32, 64-col tile kt64): 0 none / 1 all / 2 some masked
+// The per-lane mask word of a partially masked tile, waited for INSIDE the `flag == 2` branch (an
+// empty asm use): otherwise the wait lands at the branch join and even unmasked tiles drain this
+// wave's whole vector-memory queue (the score-block and staging prefetches) every tile.
+__device__ __forceinline__ uint32_t settle(uint32_t w) {
+  asm volatile("" : "+v"(w));
+  return w;
+}
+// A SCALAR load (constant address space, wave-uniform index; NKT4 % 4 == 0 keeps each flag row
+// dword-aligned): it waits on lgkmcnt.  As a vector byte load it joined the in-order vector-memory
+// queue behind the tile's prefetches, and its wait (at the join of the `mflags ? ... : 0` branch,
+// so even without a mask) drained every prefetch each tile.
+__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
+  const int64_t idx = ((int64_t)b * NRB32 + rb32) * NKT4 + kt64;
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  const uint32_t w = reinterpret_cast<cu32*>(reinterpret_cast<uintptr_t>(flags))[idx >> 2];
+  return (int)((w >> (8 * (idx & 3))) & 0xffu);
+}
+
+// Deep prefetch of a strided stream of score blocks (score-buffer kernels): XDOT_SB_PF blocks in
+// flight per wave in a register ring.  The loop is unrolled by the ring depth so that each step's
+// slot is a compile-time index: no in-flight register is ever copied (a copy would wait for its
+// load).  body(i, J) handles stream element i from slot J::value, then refills that slot with
+// element i + PF.  One 4-KiB block per tile is too little to cover HBM latency when the tile's
+// products are short (the dV and dK passes: one product per tile).
+#ifndef XDOT_SB_PF
+#define XDOT_SB_PF 2
+#endif
+template <int N> struct Ic { static constexpr int value = N; };
+template <int PF, class F> __device__ __forceinline__ void ring_loop(int beg, int end, F&& body) {
+  static_assert(PF >= 1 && PF <= 4, "ring depth");
+  for (int i0 = beg; i0 < end; i0 += PF) {
+    body(i0, Ic<0>{});
+    if constexpr (PF > 1)
+      if (i0 + 1 < end) body(i0 + 1, Ic<1>{});
+    if constexpr (PF > 2)
+      if (i0 + 2 < end) body(i0 + 2, Ic<2>{});
+    if constexpr (PF > 3)
+      if (i0 + 3 < end) body(i0 + 3, Ic<3>{});
+  }
+}
+
 // Pin MFMA accumulators to AGPRs (an empty asm with an "a" constraint).  Where accumulators and
 // operand fragments together exceed the 256 VGPRs, the allocator otherwise keeps loop-carried
 // accumulators in VGPRs and copies them into AGPRs around every product (2 VALU moves per

@@ -48,6 +48,11 @@ using fa::LOG2E;
 using fa::LN2;
 using fa::pair_max;
 using fa::pair_sum;
+using fa::tidx;
+using fa::flag_at;
+using fa::blk_store;
+using fa::blk_store_lds;
+using fa::blk_load;
 
 __device__ __forceinline__ f32x16 mm(float a, float b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -165,57 +170,6 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
 #endif
 }
 
-// tile index of accumulator register r for lane half hf
-__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
-
-// Score-buffer block I/O.  A 32x32 accumulator x holds element (a, b) with a = lane & 31 (lane
-// index) and b = tidx(r, lane >> 5) (register r).  blk_store writes it TRANSPOSED into the
-// reader's accumulator order: element (a, b) to [lane' = b + 32((a>>2)&1)][r' = (a&3) + 4(a>>3)],
-// i.e. the reader whose lane index is b finds it in its register r' -> blk_load(blk, lane)[r'].
-// (forward: a = row, b = column -> the column kernel's order; column kernel: a = column,
-// b = row -> the row kernel's order.)  Per lane 16 scattered dword stores / 4 b128 loads.
-__device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane) {
-  const int a = lane & 31, hf = lane >> 5;
-  float* p = blk + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
-}
-// The same through a wave-private 4-KiB LDS tile: the scatter goes to LDS (16 ds_write_b32, the
-// 2-way bank conflicts of which cost nothing), then the block leaves as 4 coalesced 16-byte global
-// stores per lane (64 lanes x 64 B contiguous) instead of 16 dword stores in 64-byte pieces.
-// XDOT_SB_DIRECT: the direct scatter (A/B).
-__device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x16& x, int lane) {
-#ifdef XDOT_SB_DIRECT
-  blk_store(blk, x, lane);
-#else
-  const int a = lane & 31, hf = lane >> 5;
-  float* p = wl + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
-  const f32x4* q = reinterpret_cast<const f32x4*>(wl + 16 * lane);
-  f32x4* d = reinterpret_cast<f32x4*>(blk + 16 * lane);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) d[i] = q[i];
-#endif
-}
-__device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
-  const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
-  f32x16 x;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 v = p[q];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) x[4 * q + t] = v[t];
-  }
-  return x;
-}
-
-// flag of (32-row block rb32, 64-col tile kt64): 0 none / 1 all / 2 some masked
-__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
-  return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
-}
-
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
 // SS: store the raw scores into a.sbuf (score-buffer mode)
@@ -271,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
-        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+        if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = tidx(r, hf);
@@ -432,7 +386,7 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
       const int valid = a.T - kt * 32;
       uint32_t w = 0;
       const bool chk = flag == 2 || valid < 32;
-      if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+      if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float x = __builtin_fmaf(s[r], c2, -lse2);
@@ -557,7 +511,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
       f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
       uint32_t w = 0;
-      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = tidx(r, hf);
@@ -648,21 +602,23 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
 
+  constexpr int PF = XDOT_SB_PF;
   Stager1<D> st;
-  f32x16 dnext{};
+  f32x16 q[PF];
   if (kt_beg < kt_end) {
     st.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
-    if (wave_ok) dnext = blk_load(sbr + (int64_t)kt_beg * 1024, lane);
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (wave_ok && kt_beg + j < kt_end) q[j] = blk_load(sbr + (int64_t)(kt_beg + j) * 1024, lane);
     st.store(sm, tid);
     __syncthreads();
   }
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
+  fa::ring_loop<PF>(kt_beg, kt_end, [&](int kt, auto J) {
+    constexpr int j = decltype(J)::value;
     const bool more = kt + 1 < kt_end;
-    f32x16 ds = dnext;
-    if (more) {
-      st.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
-      if (wave_ok) dnext = blk_load(sbr + (int64_t)(kt + 1) * 1024, lane);
-    }
+    f32x16 ds = q[j];
+    if (more) st.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    if (wave_ok && kt + PF < kt_end) q[j] = blk_load(sbr + (int64_t)(kt + PF) * 1024, lane);
     const float* qi = sm + ((kt - kt_beg) & 1) * CF::IMG;
     int flag = !wave_ok ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
@@ -677,7 +633,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
     }
     if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::IMG, tid);
     __syncthreads();
-  }
+  });
   if (!row_ok) return;
   float* op = (a.nsplit > 1 || a.force_partial) ? a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D
                                                 : reinterpret_cast<float*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
@@ -724,32 +680,36 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     const int rr = rt * 32 + tid;
     return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
   };
+  constexpr int PF = XDOT_SB_PF;
   Stager1<D> st;
-  f32x16 snext{};
+  f32x16 q[PF];
   float ax = 0.f;
   if (NRT > 0) {
     st.load(db_, C, 0, a.R - 1, tid);
     ax = aux_load(0);
-    if (sown) snext = blk_load(sbc, lane);
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (sown && j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
     st.store(sm, tid);
     if (tid < 32) sm[CF::IMG + tid] = ax;
     __syncthreads();
   }
-  for (int rt = 0; rt < NRT; ++rt) {
+  fa::ring_loop<PF>(0, NRT, [&](int rt, auto J) {
+    constexpr int j = decltype(J)::value;
     const bool more = rt + 1 < NRT;
-    f32x16 s = snext;
+    f32x16 s = q[j];
     if (more) {
       st.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
-      if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
+    if (sown && rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);
     const float* di = sm + (rt & 1) * STG;
     const float* ls = di + CF::IMG;
     int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
       uint32_t w = 0;
-      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = tidx(r, hf);
@@ -765,7 +725,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
       if (tid < 32) nx[CF::IMG + tid] = ax;
     }
     __syncthreads();
-  }
+  });
   if (!col_ok) return;
   float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
 #pragma unroll

@@ -37,8 +37,11 @@ using fa::pair_sum;
 using fa::wait_vm;
 using fa::raw_barrier;
 using fa::pin_agpr;
+using fa::tidx;
+using fa::flag_at;
+using fa::blk_store;
+using fa::blk_load;
 
-__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
 // Output accumulators are pinned to AGPRs (fa::pin_agpr): a wide head's D/2 accumulator
 // registers plus its D/4..D/2 fragment registers exceed the 256 VGPRs; left alone the allocator
@@ -222,30 +225,6 @@ template <class Pl> struct Dma32 {
   }
 };
 
-// flag of (32-row block rb32, 64-col tile kt64): 0 none / 1 all / 2 some masked
-__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
-  return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
-}
-
-// score-buffer blocks (flash_f32.hip): writer scatters into the reader's accumulator order
-__device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane) {
-  const int a = lane & 31, hf = lane >> 5;
-  float* p = blk + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
-}
-__device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
-  const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
-  f32x16 x;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 v = p[q];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) x[4 * q + t] = v[t];
-  }
-  return x;
-}
-
 // two images per stage fit LDS twice (double-buffered) unless fp32 D = 384
 template <class Pl> constexpr bool dbl2() { return 4 * Dma32<Pl>::SLOT + 1024 <= 160 * 1024; }
 
@@ -320,7 +299,7 @@ __global__ __launch_bounds__(256, 1) void fwd_kernel(FwdArgs a) {
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
-        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+        if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = tidx(r, hf);
@@ -471,7 +450,7 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
         f32x16 dp = Pl::rowprod(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
         uint32_t w = 0;
         const bool chk = flag == 2 || valid < 32;
-        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+        if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float x = __builtin_fmaf(s[r], c2, -lse2);
@@ -610,7 +589,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
       if constexpr (DQ) dp = Pl::rowprod(doimg(rt), vf, f32x16{}, L);  // dP (row x col)
       pin_frags();
       uint32_t w = 0;
-      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
       const int vr = a.R - rt * 32;  // valid rows of this tile
 #pragma unroll
       for (int r = 0; r < 16; ++r) {

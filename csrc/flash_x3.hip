@@ -33,6 +33,10 @@ using fa::LN2;
 using fa::LOG2E;
 using fa::pair_max;
 using fa::pair_sum;
+using fa::tidx;
+using fa::flag_at;
+using fa::blk_store_lds;
+using fa::blk_load;
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
 
@@ -87,7 +91,6 @@ template <int D, bool RMF, bool TRF> struct Img {
 // tile row c (0..31) -> slot of the transposed image (inverse of K step j, half h, t = 0..7
 // <-> row tidx(8j + t, h) = (t & 3) + 16j + 8(t >> 2) + 4h)
 __device__ __forceinline__ int slot_of(int c) { return 16 * (c >> 4) + 8 * ((c >> 2) & 1) + (c & 3) + 4 * ((c >> 3) & 1); }
-__device__ __forceinline__ int tidx(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
 // one 32-row fp32 tile global -> registers (rows row0.., clamped to row0 + rmax) -> split images
 template <int D> struct Tile {
@@ -186,9 +189,6 @@ __device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 
     }
 }
 
-__device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, int NKT4, int rb32, int kt64) {
-  return flags[((int64_t)b * NRB32 + rb32) * NKT4 + kt64];
-}
 
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
@@ -197,9 +197,11 @@ template <int D> struct FwdL {
   using V = Img<D, false, true>;
   static constexpr int STAGE = Q::BYTES + V::BYTES;
   static constexpr int LDS = 2 * STAGE;
+  static constexpr int LDS_SB = LDS + 4 * 4096;  // + a 4-KiB transpose tile per wave (blk_store_lds)
 };
 
-template <int D>
+// SS: store the raw scores into a.sbuf (score-buffer mode, same block format as flash_f32.hip)
+template <int D, bool SS>
 __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
   using CF = Cfg<D>;
   using FL = FwdL<D>;
@@ -230,6 +232,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
   f32x16 o[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) o[i] = f32x16{};
+  // score buffer: this wave's row of 32x32 blocks (r0 < R: waves past R never store)
+  float* sbw = SS ? a.sbuf + ((int64_t)bh * NRB32 + (r0 >> 5)) * NKT32 * 1024 : nullptr;
 
   Tile<D> tq, tv;
   if (kt_beg < kt_end) {
@@ -251,10 +255,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
       f32x16 s = rowprod<D, true, false>(qi, kh, kl, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
+      if constexpr (SS) blk_store_lds(sbw + kt * 1024, reinterpret_cast<float*>(smem + FL::LDS) + wave * 1024, s, lane);
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
-        if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+        if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = tidx(r, hf);
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
       const int valid = a.T - kt * 32;
       uint32_t w = 0;
       const bool chk = flag == 2 || valid < 32;
-      if (flag == 2 && row_ok) w = (uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1)));
+      if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float x = __builtin_fmaf(s[r], c2, -lse2);
@@ -417,17 +422,21 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
 // ------------------------------------------------------------------------------------------
 // backward, gathered side: dQ_cols = scale · Σ_rows dSᵀ · K_rows, dV_cols = Σ_rows Pᵀ · dO.
 // 4 waves x 32 columns of one (b, h); sweeps 32-row tiles of K_rows / dO + their lse2 / δ.
-template <int D> struct ColsL {
-  using K = Img<D, true, true>;
+// LS (score-buffer mode): S comes from a.sbuf (prefetched one tile ahead) instead of the K·Qᵀ
+// product, each block is overwritten with dS / scale for bwd_rows_ds_kernel, and dV is left to
+// bwd_cols_dv_kernel (run first).  K then needs only its transposed image, dO its row-major one.
+template <int D, bool LS> struct ColsL {
+  using K = Img<D, !LS, true>;
+  using DO = Img<D, true, !LS>;
   static constexpr int AUX = 256;  // lse2[32], δ[32] (fp32)
-  static constexpr int STAGE = 2 * K::BYTES + AUX;
-  static constexpr int LDS = 2 * STAGE;
+  static constexpr int STAGE = K::BYTES + DO::BYTES + AUX;
+  static constexpr int LDS = 2 * STAGE + (LS ? 4 * 4096 : 0);
 };
 
-template <int D>
-__global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
+template <int D, bool LS>
+__global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
-  using KL = ColsL<D>;
+  using KL = ColsL<D, LS>;
   constexpr int DB = CF::DB;
   using fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
@@ -443,25 +452,33 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32;
 
-  u32x4 qh[CF::KS], ql[CF::KS], vh[CF::KS], vl[CF::KS];
+  constexpr int QS = LS ? 1 : CF::KS;
+  u32x4 qh[QS], ql[QS], vh[CF::KS], vl[CF::KS];
   {
     const int64_t off = ((int64_t)b * a.T + (col_ok ? col : 0)) * a.ldkv + h * D + 8 * hf;
-    load_frag<D>(qh, ql, reinterpret_cast<const float*>(a.kc) + off, col_ok);
+    if constexpr (!LS) load_frag<D>(qh, ql, reinterpret_cast<const float*>(a.kc) + off, col_ok);
     load_frag<D>(vh, vl, reinterpret_cast<const float*>(a.vc) + off, col_ok);
   }
+  const int NKT32 = (a.T + 31) / 32;
+  const bool sown = LS && c0 < a.T;
+  float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024 : nullptr;
+  const int64_t sstep = (int64_t)NKT32 * 1024;
+  f32x16 snext{};
+  if (sown && NRT > 0) snext = blk_load(sbc, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
   const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
   const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
-  f32x16 dq[DB], dv[DB];
+  f32x16 dq[DB], dv[LS ? 1 : DB];
 #pragma unroll
-  for (int i = 0; i < DB; ++i) {
-    dq[i] = f32x16{};
-    dv[i] = f32x16{};
+  for (int i = 0; i < DB; ++i) dq[i] = f32x16{};
+  if constexpr (!LS) {
+#pragma unroll
+    for (int i = 0; i < DB; ++i) dv[i] = f32x16{};
+    fa::pin_agpr(dq);  // loop-carried: AGPR-resident, no per-product copies
+    fa::pin_agpr(dv);
   }
-  fa::pin_agpr(dq);  // loop-carried: AGPR-resident, no per-product copies
-  fa::pin_agpr(dv);
 
   // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
   auto aux_load = [&](int rt) -> float {
@@ -471,9 +488,9 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     return 0.f;
   };
   auto put = [&](char* st, const Tile<D>& tk, const Tile<D>& td, float ax) {
-    tk.template store<true, true>(st, tid);
-    td.template store<true, true>(st + KL::K::BYTES, tid);
-    if (tid < 64) reinterpret_cast<float*>(st + 2 * KL::K::BYTES)[tid] = ax;
+    tk.template store<!LS, true>(st, tid);
+    td.template store<true, !LS>(st + KL::K::BYTES, tid);
+    if (tid < 64) reinterpret_cast<float*>(st + KL::K::BYTES + KL::DO::BYTES)[tid] = ax;
   };
   Tile<D> tk, td;
   float ax = 0.f;
@@ -486,21 +503,27 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   }
   for (int rt = 0; rt < NRT; ++rt) {
     const bool more = rt + 1 < NRT;
+    f32x16 scur;
+    if constexpr (LS) scur = snext;
     if (more) {
       tk.load(kb, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       td.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
+      if constexpr (LS)
+        if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
     const char* ki = smem + (rt & 1) * KL::STAGE;
     const char* di = ki + KL::K::BYTES;
-    const float* ls = reinterpret_cast<const float*>(ki + 2 * KL::K::BYTES);  // lse2[32], δ[32]
+    const float* ls = reinterpret_cast<const float*>(di + KL::DO::BYTES);  // lse2[32], δ[32]
     int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
-      f32x16 s = rowprod<D, true, true>(ki, qh, ql, f32x16{}, lane);   // S  (row x col)
-      f32x16 dp = rowprod<D, true, true>(di, vh, vl, f32x16{}, lane);  // dP (row x col)
+      f32x16 s;
+      if constexpr (LS) s = scur;                                     // S  (row x col), stored by the forward
+      else s = rowprod<D, !LS, true>(ki, qh, ql, f32x16{}, lane);     // S  (row x col)
+      f32x16 dp = rowprod<D, true, !LS>(di, vh, vl, f32x16{}, lane);  // dP (row x col)
       uint32_t w = 0;
-      if (flag == 2 && col_ok) w = (uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)));
+      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = tidx(r, hf);
@@ -510,10 +533,15 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
         s[r] = p;
         dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
       }
-      trprod<D, true, true>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
-      trprod<D, true, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
-      fa::pin_agpr(dq);
-      fa::pin_agpr(dv);
+      if constexpr (LS) {
+        blk_store_lds(sbc + rt * sstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
+        trprod<D, false, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+      } else {
+        trprod<D, true, true>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
+        trprod<D, true, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
+        fa::pin_agpr(dq);
+        fa::pin_agpr(dv);
+      }
     }
     if (more) put(smem + ((rt + 1) & 1) * KL::STAGE, tk, td, ax);
     __syncthreads();
@@ -528,9 +556,185 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     for (int g = 0; g < 4; ++g) {
       *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) =
           f32x4{dq[db][4 * g] * sc, dq[db][4 * g + 1] * sc, dq[db][4 * g + 2] * sc, dq[db][4 * g + 3] * sc};
+      if constexpr (!LS)
+        *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
+            f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Score-buffer mode, gathered side pass 1 of 2: dV_cols = Σ_rows Pᵀ · dO with P recomputed
+// elementwise from the stored S (one product per tile, dO's transposed image only).  Runs BEFORE
+// bwd_cols_kernel<D, true>, which overwrites S with dS.  Stage = dO image + lse2[32].
+template <int D> struct DvL {
+  using DO = Img<D, false, true>;
+  static constexpr int STAGE = DO::BYTES + 128;
+  static constexpr int LDS = 2 * STAGE;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  using VL = DvL<D>;
+  constexpr int DB = CF::DB;
+  using fa::smem;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = (a.T + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = lin % ncb, bh = lin / ncb;
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
+  const bool col_ok = col < a.T, sown = c0 < a.T;
+  const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
+  const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024;
+  const int64_t sstep = (int64_t)NKT32 * 1024;
+  const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
+  const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
+  const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
+  f32x16 dv[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dv[i] = f32x16{};
+  auto aux_load = [&](int rt) -> float {  // lse2 (+inf past R: P = 0), threads 0..31
+    const int rr = rt * 32 + tid;
+    return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
+  };
+  constexpr int PF = XDOT_SB_PF;
+  Tile<D> td;
+  f32x16 q[PF];
+  float ax = 0.f;
+  if (NRT > 0) {
+    td.load(db_, C, 0, a.R - 1, tid);
+    ax = aux_load(0);
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (sown && j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
+    td.template store<false, true>(smem, tid);
+    if (tid < 32) reinterpret_cast<float*>(smem + VL::DO::BYTES)[tid] = ax;
+    __syncthreads();
+  }
+  fa::ring_loop<PF>(0, NRT, [&](int rt, auto J) {
+    constexpr int j = decltype(J)::value;
+    const bool more = rt + 1 < NRT;
+    f32x16 s = q[j];
+    if (more) {
+      td.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      ax = aux_load(rt + 1);
+    }
+    if (sown && rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);
+    const char* di = smem + (rt & 1) * VL::STAGE;
+    const float* ls = reinterpret_cast<const float*>(di + VL::DO::BYTES);
+    int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      uint32_t w = 0;
+      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = tidx(r, hf);
+        float x = __builtin_fmaf(s[r], c2, -ls[i]);
+        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
+        s[r] = ex2(x);
+      }
+      trprod<D, false, true>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
+    }
+    if (more) {
+      char* nx = smem + ((rt + 1) & 1) * VL::STAGE;
+      td.template store<false, true>(nx, tid);
+      if (tid < 32) reinterpret_cast<float*>(nx + VL::DO::BYTES)[tid] = ax;
+    }
+    __syncthreads();
+  });
+  if (!col_ok) return;
+  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
       *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
           f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+}
+
+// ------------------------------------------------------------------------------------------
+// Score-buffer mode, row side: dK = scale · Σ_cols dS · Q_cols with dS from the buffer the
+// column kernel wrote (one product per tile; Q's transposed image only).  Same grid, column split
+// and partial protocol as bwd_rows_kernel.
+template <int D> struct RowsDsL {
+  using Q = Img<D, false, true>;
+  static constexpr int LDS = 2 * Q::BYTES;
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
+  using CF = Cfg<D>;
+  using RL = RowsDsL<D>;
+  constexpr int DB = CF::DB;
+  using fa::smem;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nrb = (a.R + 127) / 128;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lin % nrb, bhs = lin / nrb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  const int b = bh / a.H, h = bh % a.H;
+  const int C = a.H * D;
+  const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
+  const bool row_ok = row < a.R, wave_ok = r0 < a.R;
+  const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
+  const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
+  const float* sbr = a.sbuf + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
+  f32x16 dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
+
+  constexpr int PF = XDOT_SB_PF;
+  Tile<D> tq;
+  f32x16 q[PF];
+  if (kt_beg < kt_end) {
+    tq.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (wave_ok && kt_beg + j < kt_end) q[j] = blk_load(sbr + (int64_t)(kt_beg + j) * 1024, lane);
+    tq.template store<false, true>(smem, tid);
+    __syncthreads();
+  }
+  fa::ring_loop<PF>(kt_beg, kt_end, [&](int kt, auto J) {
+    constexpr int j = decltype(J)::value;
+    const bool more = kt + 1 < kt_end;
+    f32x16 ds = q[j];
+    if (more) tq.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    if (wave_ok && kt + PF < kt_end) q[j] = blk_load(sbr + (int64_t)(kt + PF) * 1024, lane);
+    const char* qi = smem + ((kt - kt_beg) & 1) * RL::Q::BYTES;
+    int flag = !wave_ok ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
+    flag = __builtin_amdgcn_readfirstlane(flag);
+    if (flag != 1) {
+      const int valid = a.T - kt * 32;
+      if (valid < 32) {  // columns past T: the column kernel's values there are not gradients
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (tidx(r, hf) >= valid) ds[r] = 0.f;
+      }
+      trprod<D, false, true>(qi, ds, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
     }
+    if (more) tq.template store<false, true>(smem + ((kt + 1 - kt_beg) & 1) * RL::Q::BYTES, tid);
+    __syncthreads();
+  });
+  if (!row_ok) return;
+  float* op = (a.nsplit > 1 || a.force_partial) ? a.dpart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D
+                                                : reinterpret_cast<float*>(a.drows) + ((int64_t)b * a.R + row) * C + h * D;
+  const float sc = a.scale;
+#pragma unroll
+  for (int db = 0; db < DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
+          f32x4{dk[db][4 * g] * sc, dk[db][4 * g + 1] * sc, dk[db][4 * g + 2] * sc, dk[db][4 * g + 3] * sc};
 }
 
 }  // namespace fa3
@@ -549,7 +753,12 @@ extern "C" int xdot_flash_fwd_x3_launch(const xdot::fa::FwdArgs* a, int D, hipSt
   using namespace xdot::fa3;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
   const dim3 grid(((a->R + 127) / 128) * a->B * a->H * a->nsplit);
-#define L(DV) hipLaunchKernelGGL(fwd_kernel<DV>, grid, dim3(256), FwdL<DV>::LDS, st, *a)
+  if (a->sbuf) {
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true>), grid, dim3(256), FwdL<DV>::LDS_SB, st, *a)
+    X3_DISPATCH(L)
+#undef L
+  }
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, false>), grid, dim3(256), FwdL<DV>::LDS, st, *a)
   X3_DISPATCH(L)
 #undef L
 }
@@ -559,6 +768,11 @@ extern "C" int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled) return -1;
   const dim3 grid(((a->R + 127) / 128) * a->B * a->H * a->nsplit);
+  if (a->sbuf) {  // score-buffer mode: dS from the column kernel, Q image only
+#define L(DV) hipLaunchKernelGGL(bwd_rows_ds_kernel<DV>, grid, dim3(256), RowsDsL<DV>::LDS, st, *a)
+    X3_DISPATCH(L)
+#undef L
+  }
 #define L(DV) hipLaunchKernelGGL(bwd_rows_kernel<DV>, grid, dim3(256), RowsL<DV>::LDS, st, *a)
   X3_DISPATCH(L)
 #undef L
@@ -569,7 +783,14 @@ extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
-#define L(DV) hipLaunchKernelGGL(bwd_cols_kernel<DV>, grid, dim3(256), ColsL<DV>::LDS, st, *a)
+  if (a->sbuf) {  // dV from S first, then dQ (S -> dS in place)
+#define L(DV)                                                                                  \
+  hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), DvL<DV>::LDS, st, *a);            \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), (ColsL<DV, true>::LDS), st, *a)
+    X3_DISPATCH(L)
+#undef L
+  }
+#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), (ColsL<DV, false>::LDS), st, *a)
   X3_DISPATCH(L)
 #undef L
 }

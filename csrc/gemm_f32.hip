@@ -11,7 +11,9 @@
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (4 waves 2x2, each 64x64 = 2x2 blocks of
 // 32x32), K tiles of 32, staged global -> VGPR -> LDS (double-buffered, one barrier per K tile;
-// global loads run two K tiles ahead in two register sets, ~8192 MFMA cycles per wave in flight).
+// the next tile's global loads fly under the current tile's 64 MFMAs = 4096 cycles per wave;
+// a two-tile-ahead register ring measured no better).  Large products take the persistent
+// 256x256 LDS-DMA kernel of csrc/gemm2_f32.hip; this one keeps small / unaligned ones.
 // A K tile's 16 MFMA k-steps pair k = s (lane half 0) with k = 16 + s (lane half 1) for both
 // operands.  Images keep the global storage order (coalesced loads, conflict-free 16-byte LDS
 // writes): a k-contiguous operand as [mn][32 + 4 k] (a lane's 4 k-steps are one ds_read_b128;
@@ -184,7 +186,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
     gf32::store_tile<A_MC>(s, r.a, tid);
     gf32::store_tile<B_MC>(s + IMG, r.b, tid);
   };
-#ifdef XDOT_GF32_PF1
   Regs r0;
   if (ntiles > 0) {
     load(r0, 0);
@@ -197,29 +198,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
     if (t + 1 < ntiles) store(r0, (t + 1) & 1);
     __syncthreads();
   }
-#else
-  // Global loads run TWO K tiles ahead (two register sets): a tile's loads get ~2 x 4096 MFMA
-  // cycles to land instead of one, which at one WG pair per CU is less than an HBM round trip
-  // under load.  Tile t computes from LDS stage t & 1 while set (t & 1) fetches tile t + 2; the
-  // set holding tile t + 1 then fills the other stage.
-  Regs r0, r1;
-  if (ntiles > 0) {
-    load(r0, 0);
-    store(r0, 0);
-    if (ntiles > 1) load(r1, 1);
-  }
-  __syncthreads();
-  auto step = [&](int t, Regs& mine, Regs& next) {
-    if (t + 2 < ntiles) load(mine, t + 2);
-    compute(t & 1);
-    if (t + 1 < ntiles) store(next, (t + 1) & 1);
-    __syncthreads();
-  };
-  for (int t = 0; t < ntiles; t += 2) {
-    step(t, r0, r1);
-    if (t + 1 < ntiles) step(t + 1, r1, r0);
-  }
-#endif
 
   // epilogue: register r of block (i, j) = row wm*64 + 32i + (r&3) + 8(r>>2) + 4hf, column
   // wn*64 + 32j + (lane & 31)

@@ -158,6 +158,12 @@ int xdot_gemm_f32_launch(const xdot::GemmArgs* a, int batches, int a_mc, int b_m
 // 256x256 LDS-DMA 16-bit GEMM (csrc/gemm2.hip); splits > 1 needs ws: splits*batches*M*N fp32
 int xdot_gemm2_launch(const xdot::GemmArgs* a, int batches, int dt_in, int dt_out, int a_mc, int b_mc,
                       int splits, float* ws, hipStream_t st);
+// persistent 256x256 LDS-DMA exact-fp32 GEMM (csrc/gemm2_f32.hip); eligibility in the file;
+// splits > 1 needs ws (splits*batches*M*N fp32) and runs the ordered sum itself
+int xdot_gemm2_f32_launch(const xdot::GemmArgs* a, int batches, int a_mc, int b_mc, int splits, float* ws,
+                          hipStream_t st);
+// compute units of the current device (csrc/gemm2.hip)
+int xdot_num_cus();
 // C = alpha * (ordered sum of `splits` fp32 partials ws[s][z][M][N]) + beta * C  (csrc/gemm2.hip)
 int xdot_gemm_reduce_launch(const xdot::GemmArgs* a, const float* ws, int splits, int batches, int dt_out,
                             hipStream_t st);

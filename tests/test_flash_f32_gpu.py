@@ -129,17 +129,18 @@ def test_flash_f32_score_buffer_bitwise(gpu, case, mask_kind, nsplit):
 
 
 def test_flash_f32_score_buffer_checks(gpu):
-    """Wrong-sized buffers and non-exact modes are refused on the host."""
+    """Wrong-sized buffers and non-fp32 inputs are refused on the host."""
     from xdot.ops import flash
 
     rows = torch.randn(1, 64, 128, device=gpu)
     kc = torch.randn(1, 96, 128, device=gpu)
     n = flash.score_buffer_numel(1, 2, 64, 96)
     assert n == 2 * 2 * 3 * 1024
-    with pytest.raises(RuntimeError, match="score buffer"):
-        flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=0, sbuf=torch.empty(n - 1, device=gpu))
-    with pytest.raises(RuntimeError, match="exact-fp32"):
-        flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=1, sbuf=torch.empty(n, device=gpu))
+    for fm in (0, 1):
+        with pytest.raises(RuntimeError, match="score buffer"):
+            flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=fm, sbuf=torch.empty(n - 1, device=gpu))
+    with pytest.raises(RuntimeError, match="fp32"):
+        flash.fwd(rows.bfloat16(), kc.bfloat16(), kc.bfloat16(), None, 2, 0.1, sbuf=torch.empty(n, device=gpu))
 
 
 def test_module_fp32_score_buffer_matches_recompute(gpu):
@@ -287,6 +288,39 @@ def test_flash_split_fwd_bwd(gpu, case, mask_kind):
                            ("d cols (q)", dkc, _to_gathered(q.grad, N, B, Rc, H * D)),
                            ("d cols (v)", dvc, _to_gathered(v.grad, N, B, Rc, H * D))):
         assert got.dtype == torch.float32
+        assert _rel(got, ref) <= SPLIT_TOL, f"{what}: {_rel(got, ref):.2e}"
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
+@pytest.mark.parametrize("nsplit", [0, 3])
+def test_flash_split_score_buffer(gpu, case, mask_kind, nsplit):
+    """Split mode with the score buffer (forward stores S, dV pass + dQ pass read it and write
+    dS, the row kernel reads dS): within the split bound of the fp64 reference.  Not bitwise
+    equal to the recompute path: its column kernel recomputes S with the operand roles of the
+    3-term split swapped (another rounding order); the buffer carries the forward's own S."""
+    from xdot.ops import flash
+
+    B, R, N, Rc, H, D = case
+    T = N * Rc
+    rows, kc, vc, do, mask = _inputs(case, mask_kind, gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)  # no stale zeros
+    out, lse = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=nsplit, fp32_mode=1, sbuf=sb)
+    o1, l1 = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=nsplit, fp32_mode=1)
+    assert torch.equal(out, o1) and torch.equal(lse, l1)  # storing S changes nothing
+    k, q, v, ref_o, ref_lse = _ref64(rows, kc, vc, mask, H, scale)
+    dkv, delta = flash.bwd_cols(do, rows, kb, vb, out, lse, mk, H, scale, fp32_mode=1, sbuf=sb)
+    drows = flash.bwd_rows(do, rows, kb, vb, lse, delta, mk, H, scale, nsplit=nsplit, fp32_mode=1, sbuf=sb)
+    C = H * D
+    dkc, dvc = flash.btc_to_rank_major(dkv[..., :C], N), flash.btc_to_rank_major(dkv[..., C:], N)
+    ref_o.backward(do.double())
+    for what, got, ref in (("d rows", drows, k.grad.transpose(1, 2).reshape(B, R, H * D)),
+                           ("d cols (q)", dkc, _to_gathered(q.grad, N, B, Rc, H * D)),
+                           ("d cols (v)", dvc, _to_gathered(v.grad, N, B, Rc, H * D))):
+        assert torch.isfinite(got).all(), what
         assert _rel(got, ref) <= SPLIT_TOL, f"{what}: {_rel(got, ref):.2e}"
 
 

@@ -37,6 +37,53 @@ def test_gemm_f32_layouts(gpu, a_mc, b_mc, M, N, K):
     assert _rel(C, ref) <= 2e-6
 
 
+def _eligible_v2(M, N, K, a_mc, b_mc):
+    return (a_mc or K % 4 == 0) and (b_mc or K % 4 == 0) and (not a_mc or M % 4 == 0) and (not b_mc or N % 4 == 0)
+
+
+@pytest.mark.parametrize("a_mc", [False, True])
+@pytest.mark.parametrize("b_mc", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 100), (516, 1000, 36), (64, 36, 4), (1024, 768, 2048),
+                                   (768, 520, 12500)])
+def test_gemm2_f32_layouts(gpu, a_mc, b_mc, M, N, K):
+    """The persistent 256x256 LDS-DMA kernel (path 2, csrc/gemm2_f32.hip): ragged M / N tiles,
+    K tails (K % 32) zero-patched in LDS, alpha / beta, every storage order; the long-K shape
+    goes split-K through path 0 (ordered fp32 partial sum)."""
+    from xdot.ops.gemm import strided_gemm
+
+    if not _eligible_v2(M, N, K, a_mc, b_mc):
+        pytest.skip("layout rules of the 256x256 kernel")
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N + K)
+    A = torch.randn((K, M) if a_mc else (M, K), device=gpu, generator=g)
+    B = torch.randn((K, N) if b_mc else (N, K), device=gpu, generator=g)
+    C = torch.randn(M, N, device=gpu, generator=g)
+    C0 = C.clone()
+    path = 0 if K > 4096 else 2
+    strided_gemm(A, B, C, M=M, N=N, K=K, lda=A.shape[1], ldb=B.shape[1], ldc=N, a_mc=a_mc, b_mc=b_mc,
+                 alpha=0.5, beta=-2.0, path=path)
+    opA = A.double().t() if a_mc else A.double()
+    opB = B.double() if b_mc else B.double().t()
+    assert _rel(C, 0.5 * opA @ opB - 2.0 * C0.double()) <= 2e-6
+
+
+def test_gemm2_f32_batched_segments_exact_ints(gpu):
+    """Two batch levels + K segments with a K tail per segment (K = 36) on the 256x256 kernel and
+    through the automatic route (split-K): integer data, exact."""
+    from xdot.ops.gemm import strided_gemm
+
+    g = torch.Generator(device=gpu).manual_seed(3)
+    nb1, nb2, nseg, M, N, K = 2, 2, 3, 260, 132, 36
+    A = torch.randint(-3, 4, (nb1, nb2, nseg, K, M), device=gpu, generator=g).float()  # mn-contiguous
+    B = torch.randint(-3, 4, (nb1, nb2, nseg, N, K), device=gpu, generator=g).float()  # k-contiguous
+    ref = torch.einsum("xyskm,xysnk->xymn", A.double(), B.double())
+    for path in (2, 0):
+        C = torch.full((nb1, nb2, M, N), float("nan"), device=gpu)
+        strided_gemm(A, B, C, M=M, N=N, K=K, nseg=nseg, nb1=nb1, nb2=nb2, lda=M, ldb=K, ldc=N,
+                     sA1=nb2 * nseg * K * M, sA2=nseg * K * M, sB1=nb2 * nseg * N * K, sB2=nseg * N * K,
+                     sC1=nb2 * M * N, sC2=M * N, sAseg=K * M, sBseg=N * K, a_mc=True, path=path)
+        assert torch.equal(C.double(), ref), f"path {path}"
+
+
 def test_gemm_f32_batched_segments_exact_ints(gpu):
     """2-level batch + K segments (the `all` product's rank segments) on integer data: exact."""
     from xdot.ops.gemm import strided_gemm

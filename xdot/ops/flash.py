@@ -205,12 +205,12 @@ def fp32_code(dtype: torch.dtype, mode: Optional[str] = None) -> int:
 
 
 def score_buffer_numel(B: int, H: int, R: int, T: int) -> int:
-    """Floats of the exact-fp32 score buffer: (B*H, ceil(R/32), ceil(T/32)) blocks of 32x32."""
+    """Floats of the fp32 score buffer: (B*H, ceil(R/32), ceil(T/32)) blocks of 32x32."""
     return B * H * ((R + 31) // 32) * ((T + 31) // 32) * 1024
 
 
 def score_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tensor]:
-    """The exact-fp32 score buffer (``csrc/flash_f32.hip``, score-buffer mode) or None.
+    """The fp32 score buffer (``csrc/flash_f32.hip`` exact, ``csrc/flash_x3.hip`` split; score-buffer mode) or None.
 
     The forward stores every computed score tile there; the backward's column kernel reads S
     instead of recomputing it and overwrites it with dS, which the row kernel reads: 6 fp32
@@ -236,7 +236,7 @@ def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[Pac
 
     ``nsplit``: column splits (0 = auto: split only when R is too small to fill the GPU).
     ``prescaled``: ``rows`` is :func:`prescale` output.  ``fp32_mode``: :func:`fp32_code`
-    (None: from ``XDOT_FP32_MODE``).  ``sbuf``: exact fp32 only, a :func:`score_buffer` the
+    (None: from ``XDOT_FP32_MODE``).  ``sbuf``: fp32 (exact or split) only, a :func:`score_buffer` the
     raw scores are stored into for :func:`bwd_cols` / :func:`bwd_rows`."""
     bits, flags = _mask_args(mk)
     fm = fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode)

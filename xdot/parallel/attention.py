@@ -499,10 +499,10 @@ class SeqParallelAttention(torch.autograd.Function):
         mask = getattr(mask, "raw", mask)
         segmented = n > 1 and (FLAGS.local_first or len(chunks) > 1)
         sbuf = None
-        if use_hip and k.dtype == torch.float32 and fm == 0 and (len(chunks) == 1 or B == 1):
-            # exact fp32: score buffer (flash.score_buffer) when it fits: the backward then reads
-            # S / dS instead of recomputing them.  One kernel over the whole gathered side (in fp32
-            # the own-block-first segmentation hides < 5 % of a rank's forward)
+        if use_hip and k.dtype == torch.float32 and (len(chunks) == 1 or B == 1):
+            # fp32 (exact or split): score buffer (flash.score_buffer) when it fits: the backward
+            # then reads S / dS instead of recomputing them.  One kernel over the whole gathered
+            # side (in fp32 the own-block-first segmentation hides < 5 % of a rank's forward)
             sbuf = flash.score_buffer(B, H, R, n * qv.shape[1], k.device)
             if sbuf is not None:
                 segmented = False

@@ -44,7 +44,7 @@ variable                    default   effect
                                       relative vs fp64: the reference's precision) or ``split``
                                       (opt-in, like TF32: hi/lo bf16 halves, 3 bf16 products:
                                       <= 9e-6 flash, <= 2e-5 GEMM; profiles/r3_fp32_split.md)
-``XDOT_FP32_SCORES``        1         exact fp32 flash: the forward stores the raw scores and the
+``XDOT_FP32_SCORES``        1         fp32 flash (exact and split): the forward stores the raw scores and the
                                       backward reads S / dS instead of recomputing them (6 fp32
                                       products per step instead of 9; needs R*T*H*4 bytes)
 ``XDOT_FP32_SCORES_FRAC``   0.5       ... only when that fits this fraction of the free device memory
