@@ -301,9 +301,12 @@ void gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int64_t M, in
     const bool ok = (a_mc || K % 4 == 0) && (b_mc || K % 4 == 0) && (!a_mc || M % 4 == 0) && (!b_mc || N % 4 == 0);
     TORCH_CHECK(mode != 2 || ok, "xdot.gemm: path 2 (fp32 v2) needs K % 4 == 0 for k-contiguous operands and "
                                  "an mn extent % 4 == 0 for mn-contiguous ones");
-    if (ok && (mode == 2 || (M >= 128 && N >= 128))) {
-      const int64_t nb = nb1 * nb2;
-      const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb;
+    const int64_t nb = nb1 * nb2;
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * nb;
+    // auto: >= 2 rounds of 256x256 tiles, or a long K (split-K fills the GPU).  Short-K products
+    // with few tiles (the 25000 x 768 x 768 projections: 294 tiles, K = 768) stay on the 128x128
+    // kernel: 82-94 TF/s there vs 63-65 for this one split 4-6 ways (r5s9)
+    if (ok && (mode == 2 || (M >= 128 && N >= 128 && (tiles >= 2 * 256 || (int64_t)K * nseg >= 4096)))) {
       int64_t S = pick_splits(tiles, nseg * ((K + 31) / 32));
       while (S > 1 && S * nb * M * N > (128LL << 20)) --S;
       at::Tensor ws;

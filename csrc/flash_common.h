@@ -222,7 +222,7 @@ __device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, i
 // element i + PF.  One 4-KiB block per tile is too little to cover HBM latency when the tile's
 // products are short (the dV and dK passes: one product per tile).
 #ifndef XDOT_SB_PF
-#define XDOT_SB_PF 2
+#define XDOT_SB_PF 1  // 1 / 2 / 3 measured equal (profiles/r5_fp32.md): no ring copies at 1
 #endif
 template <int N> struct Ic { static constexpr int value = N; };
 template <int PF, class F> __device__ __forceinline__ void ring_loop(int beg, int end, F&& body) {

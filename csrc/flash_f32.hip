@@ -510,16 +510,18 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
 #endif
       else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
       f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
-      uint32_t w = 0;
-      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = tidx(r, hf);
-        float x = __builtin_fmaf(s[r], c2, -ls[i]);
-        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
-        const float p = ex2(x);
+        const float p = ex2(__builtin_fmaf(s[r], c2, -ls[i]));
         s[r] = p;
         dp[r] = p * (dp[r] - ls[32 + i]);  // dS / scale
+      }
+      if (flag == 2) {  // masked entries: P = dS = 0 (the unmasked loop stays select-free)
+        const uint32_t w = col_ok ? fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)))) : 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
 #ifndef XDOT_AB_NO_DS_STORE
       if constexpr (LS) blk_store_lds(sbc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS in place of S
@@ -708,14 +710,13 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
     if (flag != 1) {
-      uint32_t w = 0;
-      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = tidx(r, hf);
-        float x = __builtin_fmaf(s[r], c2, -ls[i]);
-        if (flag == 2 && ((w >> i) & 1u)) x = NEG_INF;
-        s[r] = ex2(x);
+      for (int r = 0; r < 16; ++r) s[r] = ex2(__builtin_fmaf(s[r], c2, -ls[tidx(r, hf)]));
+      if (flag == 2) {  // masked entries: P = 0
+        const uint32_t w = col_ok ? fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)))) : 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((w >> tidx(r, hf)) & 1u) s[r] = 0.f;
       }
       trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
     }
