@@ -72,9 +72,11 @@ variable                    default   effect
 ``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
                                       (two xGMI links per hop), 16-bit accumulators  [collective]
 ``XDOT_ROCTX`` (C++)        0         roctx ranges around every native op (rocprofv3 markers)
-``XDOT_GEMM_LIB`` (C++)     fp32      which plain large products may run on the library GEMM
-                                      (hipBLASLt, ``csrc/bindings.cpp``): unset = exact-fp32 ones only,
-                                      0 = none (every product on the xdot kernels), 1 = 16-bit too
+``XDOT_GEMM_LIB`` (C++)     0         which plain large products may run on the library GEMM
+                                      (hipBLASLt, ``csrc/bindings.cpp``): unset / 0 = none (every
+                                      product on the xdot kernels: exact fp32 on csrc/gemm2_f32.hip
+                                      / gemm_f32.hip), ``fp32`` = exact-fp32 ones (the round-4
+                                      default, kept for A/B), 1 = 16-bit ones too
 ``XDOT_GEMM3`` (C++)        1         16-bit products with M, N >= 256 and beta = 0 run the 8-phase
                                       16x16x32 kernel (``csrc/gemm3.hip``; 0: the 256x256 v2 kernel)
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
