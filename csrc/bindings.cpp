@@ -682,16 +682,30 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
                                                               bool fp32_out, bool prescaled,
                                                               const c10::optional<at::Tensor>& lse2_in,
                                                               int64_t fp32_mode,
-                                                              const c10::optional<at::Tensor>& sbuf) {
+                                                              const c10::optional<at::Tensor>& sbuf,
+                                                              const c10::optional<at::Tensor>& dsbuf, int64_t passes,
+                                                              const c10::optional<at::Tensor>& dkv_out) {
   Range rr_("xdot.flash_bwd_cols");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols");
+  float* dsb = sbuf_ptr(dsbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols (dS buffer)");
+  TORCH_CHECK(!dsb || sb, "xdot.flash_bwd_cols: a dS buffer needs the score buffer");
+  TORCH_CHECK(passes >= 1 && passes <= 3 && (passes == 3 || (sb && dsb)),
+              "xdot.flash_bwd_cols: single passes (1 = dV, 2 = dQ) need the score and dS buffers");
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   a.prescaled = prescaled ? 1 : 0;
   a.fp32_mode = (int)fp32_mode;
-  auto dkv = at::empty({g.B, g.T, 2 * g.C}, fp32_out ? kc.options().dtype(at::kFloat) : kc.options());
+  at::Tensor dkv;
+  if (dkv_out.has_value() && dkv_out->defined()) {  // the other pass's output, completed in place
+    dkv = *dkv_out;
+    TORCH_CHECK(dkv.is_contiguous() && dkv.sizes() == at::IntArrayRef({g.B, g.T, 2 * g.C}) &&
+                    dkv.scalar_type() == (fp32_out ? at::kFloat : kc.scalar_type()) && dkv.device() == rows.device(),
+                "xdot.flash_bwd_cols: dkv_out");
+  } else {
+    dkv = at::empty({g.B, g.T, 2 * g.C}, fp32_out ? kc.options().dtype(at::kFloat) : kc.options());
+  }
   const bool have_delta = delta_in.has_value() && delta_in->defined();
   at::Tensor delta;
   if (have_delta) {
@@ -716,6 +730,8 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   }
   a.lse2 = lse2.data_ptr<float>();
   a.sbuf = sb;
+  a.dsbuf = dsb;
+  a.sb_passes = (int)passes;
   c10::DeviceGuard guard(rows.device());
   const int dt = dt_code(rows.scalar_type());
   // prep: lse2 (+ δ unless given)
@@ -1038,10 +1054,13 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_prep(const at::Tensor& dout, const 
 at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const at::Tensor& kc, const at::Tensor& vc,
                           const at::Tensor& lse, const at::Tensor& delta, const c10::optional<at::Tensor>& bits,
                           const c10::optional<at::Tensor>& flags, int64_t H, double scale, int64_t nsplit,
-                          bool prescaled, int64_t fp32_mode, const c10::optional<at::Tensor>& sbuf) {
+                          bool prescaled, int64_t fp32_mode, const c10::optional<at::Tensor>& sbuf,
+                          const c10::optional<at::Tensor>& dsbuf) {
   Range rr_("xdot.flash_bwd_rows");
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_rows");
+  float* dsb = sbuf_ptr(dsbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_rows (dS buffer)");
+  TORCH_CHECK(!dsb || sb, "xdot.flash_bwd_rows: a dS buffer needs the score buffer");
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
               "xdot.flash_bwd_rows: delta");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
@@ -1054,6 +1073,7 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   a.prescaled = prescaled ? 1 : 0;
   a.fp32_mode = (int)fp32_mode;
   a.sbuf = sb;
+  a.dsbuf = dsb;
   c10::DeviceGuard guard(rows.device());
   TORCH_CHECK(xdot_flash_bwd_rows_launch(&a, dt_code(rows.scalar_type()), (int)g.D, cur_stream(rows)) == 0,
               "xdot.flash_bwd_rows: config");
@@ -1356,7 +1376,8 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_fwd(Tensor rows, Tensor kc, Tensor vc, Tensor? bits, Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor(a!)? sbuf=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_cols(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor out, Tensor lse, Tensor? bits, "
         "Tensor? flags, int H, float scale, Tensor? delta=None, bool fp32_out=True, bool prescaled=False, "
-        "Tensor? lse2=None, int fp32_mode=0, Tensor(a!)? sbuf=None) -> (Tensor, Tensor)");
+        "Tensor? lse2=None, int fp32_mode=0, Tensor(a!)? sbuf=None, Tensor(b!)? dsbuf=None, int passes=3, "
+        "Tensor(c!)? dkv_out=None) -> (Tensor, Tensor)");
   m.def("flash_bwd_prep(Tensor dout, Tensor out, Tensor lse, int H) -> (Tensor, Tensor)");
   m.def("flash_bwd_delta(Tensor dout, Tensor out, int H) -> Tensor");
   m.def("sum_partials(Tensor part, ScalarType out_dtype) -> Tensor");
@@ -1372,7 +1393,8 @@ TORCH_LIBRARY(xdot, m) {
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
-        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor? sbuf=None) -> Tensor");
+        "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor? sbuf=None, "
+        "Tensor? dsbuf=None) -> Tensor");
   m.def("flash_prescale(Tensor x, float scale) -> Tensor");
   m.def("mse_fwd(Tensor y, Tensor t) -> (Tensor, Tensor)");
   m.def("proj(Tensor x, Tensor w, Tensor? bias, bool nn, Tensor(a!)? out=None, int force=0, float alpha=1.0) -> Tensor");

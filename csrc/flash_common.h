@@ -173,6 +173,7 @@ __device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x1
 #ifdef XDOT_SB_DIRECT
   blk_store(blk, x, lane);
 #else
+#ifdef XDOT_SB_NOSWZ
   const int a = lane & 31, hf = lane >> 5;
   float* p = wl + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
 #pragma unroll
@@ -182,6 +183,23 @@ __device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x1
   f32x4* d = reinterpret_cast<f32x4*>(blk + 16 * lane);
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = q[i];
+#else
+  // The tile position q of logical float q is q ^ 16 ((q >> 6) & 1) ^ 32 ((q >> 9) & 1): the 16
+  // scatter writes then cover all 64 banks (unswizzled: 16 banks, 4-way conflicts), and each
+  // reader lane's 16 floats stay one contiguous 64-byte slot (slot l ^ ((l >> 2) & 1) ^
+  // 2 ((l >> 5) & 1)), read chunk-rotated so every 16-lane b128 phase hits 16 bank quads.
+  const int a = lane & 31, hf = lane >> 5, sa = (a >> 2) & 1, k = hf + 2 * sa;
+  float* p = wl + 512 * sa + (a & 3) + 4 * (a >> 3) + 64 * hf;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[128 * (r >> 2) + 16 * ((r & 3) ^ k)] = x[r];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
+  const int slot = lane ^ ((lane >> 2) & 1) ^ (2 * ((lane >> 5) & 1));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = (i + (lane >> 2)) & 3;
+    *reinterpret_cast<f32x4*>(blk + 16 * lane + 4 * c) = *reinterpret_cast<const f32x4*>(wl + 16 * slot + 4 * c);
+  }
+#endif
 #endif
 }
 __device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {

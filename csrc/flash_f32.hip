@@ -448,6 +448,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   // score buffer column of this wave: block (bh, rt, c0/32) at sbc + rt * NKT32 * 1024
   const bool sown = LS && c0 < a.T;
   float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
+  float* dsc = LS ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
   const int64_t sstep = (int64_t)NKT32 * 1024;
   f32x16 snext{};
   if (sown && NRT > 0) snext = blk_load(sbc, lane);
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
           if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
 #ifndef XDOT_AB_NO_DS_STORE
-      if constexpr (LS) blk_store_lds(sbc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS in place of S
+      if constexpr (LS) blk_store_lds(dsc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS (over S or apart)
 #endif
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
@@ -599,7 +600,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
   const bool row_ok = row < a.R, wave_ok = r0 < a.R;
   const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
-  const float* sbr = a.sbuf + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
+  const float* sbr = (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
   f32x16 dk[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
@@ -815,12 +816,19 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
-  if (a->sbuf) {  // dV from S first, then dQ (S -> dS in place)
-#define L(DV)                                                                                              \
-  hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a);        \
-  hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
+  if (a->sbuf) {  // in place: dV from S first, then dQ (S -> dS); with a dS buffer dQ first
+    const int ps = a->sb_passes ? a->sb_passes : 3;
+    const bool dv_first = !a->dsbuf;
+#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a)
+#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
+#define L(DV)                            \
+  if ((ps & 1) && dv_first) LDV(DV);     \
+  if (ps & 2) LDQ(DV);                   \
+  if ((ps & 1) && !dv_first) LDV(DV)
     XF32_DISPATCH(L)
 #undef L
+#undef LDQ
+#undef LDV
   }
 #define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), lds_bytes<DV>(), st, *a)
   XF32_DISPATCH(L)

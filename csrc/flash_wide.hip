@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
   dm.init(wave, lane, ldb);
   auto stage = [&](int t) { return sm + ((t - kt_beg) & 1) * NIMG * SLOT; };
   const float c2 = a.prescaled ? 1.f : a.scale * LOG2E, NEG_INF = -__builtin_inff();
-  const float* sbr = LD ? a.sbuf + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024 : nullptr;
+  const float* sbr = LD ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024 : nullptr;
   f32x16 dk[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
@@ -552,6 +552,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   pin_agpr(acc);
   const bool sown = LS && c0 < a.T;
   float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
+  float* dsc = LS ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
   const int64_t sstep = (int64_t)NKT32 * 1024;
 
   // first-used image(s) + the row constants of tile t (rows past R clamp: masked below): lse2 of
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
         if constexpr (DQ) dp[r] = p * (dp[r] - ls[64 + i]);  // dS / scale
         else s[r] = p;
       }
-      if constexpr (DQ && LS) blk_store(sbc + rt * sstep, dp, lane);  // dS in place of S (row-kernel order)
+      if constexpr (DQ && LS) blk_store(dsc + rt * sstep, dp, lane);  // dS over S or apart (row-kernel order)
       if constexpr (!DQ) Pl::trprod(doimg(rt), s, acc, L);  // dVᵀ += dOᵀ · P
     }
     if constexpr (DQ) {
@@ -709,9 +710,15 @@ int wide_cols(const xdot::fa::BwdArgs* a, hipStream_t st) {
   using Pl = Pol<DT, D>;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
   if constexpr (DT == xdot::DT_F32) {
-    if (a->sbuf) {  // dV first: the dQ pass overwrites S with dS
-      hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, true>), grid, dim3(256), (cols_lds<Pl, false, true>()), st, *a);
-      hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, true>), grid, dim3(256), (cols_lds<Pl, true, true>()), st, *a);
+    if (a->sbuf) {  // in place: dV first (the dQ pass overwrites S with dS); with a dS buffer dQ first
+      const int ps = a->sb_passes ? a->sb_passes : 3;
+      const bool dv_first = !a->dsbuf;
+      if ((ps & 1) && dv_first)
+        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, true>), grid, dim3(256), (cols_lds<Pl, false, true>()), st, *a);
+      if (ps & 2)
+        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, true>), grid, dim3(256), (cols_lds<Pl, true, true>()), st, *a);
+      if ((ps & 1) && !dv_first)
+        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, true>), grid, dim3(256), (cols_lds<Pl, false, true>()), st, *a);
       return 0;
     }
   }

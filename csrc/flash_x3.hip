@@ -462,6 +462,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int NKT32 = (a.T + 31) / 32;
   const bool sown = LS && c0 < a.T;
   float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024 : nullptr;
+  float* dsc = LS ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024 : nullptr;
   const int64_t sstep = (int64_t)NKT32 * 1024;
   f32x16 snext{};
   if (sown && NRT > 0) snext = blk_load(sbc, lane);
@@ -536,7 +537,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
           if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
       if constexpr (LS) {
-        blk_store_lds(sbc + rt * sstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
+        blk_store_lds(dsc + rt * sstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
         trprod<D, false, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
       } else {
         trprod<D, true, true>(di, s, dv, lane);   // dVᵀ += dOᵀ · P
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
   const bool row_ok = row < a.R, wave_ok = r0 < a.R;
   const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const float* qb = reinterpret_cast<const float*>(a.kc) + (int64_t)b * a.T * a.ldkv + h * D;
-  const float* sbr = a.sbuf + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
+  const float* sbr = (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 + (wave_ok ? r0 >> 5 : 0)) * NKT32 * 1024;
   f32x16 dk[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
@@ -784,12 +785,19 @@ extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
   const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
-  if (a->sbuf) {  // dV from S first, then dQ (S -> dS in place)
-#define L(DV)                                                                                  \
-  hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), DvL<DV>::LDS, st, *a);            \
-  hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), (ColsL<DV, true>::LDS), st, *a)
+  if (a->sbuf) {  // in place: dV from S first, then dQ (S -> dS); with a dS buffer dQ first
+    const int ps = a->sb_passes ? a->sb_passes : 3;
+    const bool dv_first = !a->dsbuf;
+#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), DvL<DV>::LDS, st, *a)
+#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), (ColsL<DV, true>::LDS), st, *a)
+#define L(DV)                            \
+  if ((ps & 1) && dv_first) LDV(DV);     \
+  if (ps & 2) LDQ(DV);                   \
+  if ((ps & 1) && !dv_first) LDV(DV)
     X3_DISPATCH(L)
 #undef L
+#undef LDQ
+#undef LDV
   }
 #define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), (ColsL<DV, false>::LDS), st, *a)
   X3_DISPATCH(L)

@@ -90,9 +90,14 @@ struct BwdArgs {
   int force_partial;       // 1: write partials even with nsplit == 1 (summed separately)
   int prescaled;           // 1: rows hold K * scale * log2(e) (same buffer as the forward's)
   int fp32_mode;           // fp32 inputs: 0 exact (flash_f32.hip), 1 split-bf16 (flash_x3.hip)
-  // exact fp32 only: the forward's score buffer (FwdArgs::sbuf).  The column kernel reads S from it
-  // instead of recomputing it and overwrites each block with dS; the row kernel then reads dS
+  // fp32 (exact / split): the forward's score buffer (FwdArgs::sbuf).  The column kernel reads S
+  // from it instead of recomputing it and writes dS; the row kernel then reads dS
   float* sbuf;
+  // dS buffer (same block layout), or nullptr: dS overwrites S in place (the dV pass must then
+  // run before the dQ pass).  With it the dV pass can run after the dQ pass, concurrently with the
+  // row kernel (D <= 128 kernels)
+  float* dsbuf;
+  int sb_passes;           // column launch in score-buffer mode: bit 0 dV pass, bit 1 dQ pass (0: both)
 };
 
 }  // namespace fa

@@ -229,6 +229,27 @@ def score_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tenso
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
+def score_buffers(B: int, H: int, R: int, T: int, device):
+    """(S buffer, dS buffer) for the backward's concurrent schedule, (S buffer, None) for the
+    in-place one, or None (recompute): like :func:`score_buffer`, the dS buffer only when both fit
+    within ``XDOT_FP32_SCORES_FRAC`` of the free device memory.  With a separate dS buffer the
+    column side runs its dQ pass first (S -> dS), then its dV pass (reads S) CONCURRENTLY with the
+    row kernel (reads dS): two one-product kernels side by side instead of back to back."""
+    if not FLAGS.fp32_scores:
+        return None
+    n = score_buffer_numel(B, H, R, T)
+    dev = torch.device(device)
+    free, _ = torch.cuda.mem_get_info(dev)
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    room = FLAGS.fp32_scores_frac * (free + cached)
+    if 8 * n <= room and FLAGS.fp32_scores_dsbuf:
+        both = torch.empty(2 * n, dtype=torch.float32, device=dev)
+        return both[:n], both[n:]
+    if 4 * n <= room:
+        return torch.empty(n, dtype=torch.float32, device=dev), None
+    return None
+
+
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
         scale: float, nsplit: int = 0, prescaled: bool = False,
         fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -257,31 +278,37 @@ def bwd_prep(dout: torch.Tensor, out: torch.Tensor, lse: torch.Tensor, H: int):
 def bwd_cols(dout, rows, kc, vc, out, lse, mk: Optional[PackedMask], H: int, scale: float,
              delta: Optional[torch.Tensor] = None, fp32_out: bool = True, prescaled: bool = False,
              lse2: Optional[torch.Tensor] = None, fp32_mode: Optional[int] = None,
-             sbuf: Optional[torch.Tensor] = None):
+             sbuf: Optional[torch.Tensor] = None, dsbuf: Optional[torch.Tensor] = None, passes: int = 3,
+             out_dkv: Optional[torch.Tensor] = None):
     """Gathered-side grads -> (packed [d_kc | d_vc] (B, T, 2*H*D), delta (B, H, R)).
 
     ``delta`` (from :func:`bwd_delta`) is computed here when not given; with ``lse2`` too (both
     from :func:`bwd_prep`) no prep pass is launched here.  The grads are fp32
     (``fp32_out``) or rounded once to the input dtype in the kernel epilogue.  ``sbuf``: the
-    forward's :func:`score_buffer`; S is read from it and it is OVERWRITTEN with dS for
-    :func:`bwd_rows` (run once per forward)."""
+    forward's :func:`score_buffer`; S is read from it and, without ``dsbuf``, it is OVERWRITTEN
+    with dS for :func:`bwd_rows` (run once per forward).  ``dsbuf`` (:func:`score_buffers`): dS
+    goes there instead; then ``passes`` may run one pass per call (2 = dQ, which writes dS; 1 = dV)
+    with ``out_dkv`` = the first call's output, completed in place."""
     bits, flags = (mk.bits_t, mk.flags) if mk is not None else (None, None)
     return _ext.ops().flash_bwd_cols(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      out.contiguous(), lse.contiguous(), bits, flags, int(H), float(scale), delta,
                                      bool(fp32_out), bool(prescaled), lse2,
-                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf)
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf, dsbuf,
+                                     int(passes), out_dkv)
 
 
 def bwd_rows(dout, rows, kc, vc, lse, delta, mk: Optional[PackedMask], H: int, scale: float, nsplit: int = 0,
-             prescaled: bool = False, fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None):
+             prescaled: bool = False, fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None,
+             dsbuf: Optional[torch.Tensor] = None):
     """Row-side grad (B, R, H*D) in rows.dtype.  ``nsplit`` 0: the launcher's occupancy model
     (column splits so the row kernel fills the GPU; 1 measured 7 % / 32 % slower at N = 1 / 8).
-    ``sbuf``: the score buffer after :func:`bwd_cols` wrote dS into it (dK is then its only product)."""
+    ``sbuf``: the score buffer after :func:`bwd_cols` wrote dS into it (dK is then its only product);
+    with ``dsbuf`` dS is read from there."""
     bits, flags = _mask_args(mk)
     return _ext.ops().flash_bwd_rows(dout.contiguous(), rows.contiguous(), _kv(kc), _kv(vc),
                                      lse.contiguous(), delta.contiguous(), bits, flags, int(H), float(scale),
                                      int(nsplit), bool(prescaled),
-                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf)
+                                     fp32_code(rows.dtype) if fp32_mode is None else int(fp32_mode), sbuf, dsbuf)
 
 
 def bwd(dout: torch.Tensor, rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, out: torch.Tensor,

@@ -498,13 +498,14 @@ class SeqParallelAttention(torch.autograd.Function):
                 mask = mask.raw
         mask = getattr(mask, "raw", mask)
         segmented = n > 1 and (FLAGS.local_first or len(chunks) > 1)
-        sbuf = None
+        sbuf = dsbuf = None
         if use_hip and k.dtype == torch.float32 and (len(chunks) == 1 or B == 1):
             # fp32 (exact or split): score buffer (flash.score_buffer) when it fits: the backward
             # then reads S / dS instead of recomputing them.  One kernel over the whole gathered
             # side (in fp32 the own-block-first segmentation hides < 5 % of a rank's forward)
-            sbuf = flash.score_buffer(B, H, R, n * qv.shape[1], k.device)
-            if sbuf is not None:
+            sbs = flash.score_buffers(B, H, R, n * qv.shape[1], k.device)
+            if sbs is not None:
+                sbuf, dsbuf = sbs
                 segmented = False
         if use_hip and k.dtype == torch.float32 and D > WIDE_F32_NEEDS_SCORES and sbuf is None:
             # no kernel recomputes an fp32 head this wide (three D-wide register sets): the torch path
@@ -537,7 +538,7 @@ class SeqParallelAttention(torch.autograd.Function):
         ctx.save_for_backward(k, o, lse, *bufs)
         ctx.mks, ctx.mask, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, mask, chunks, H, scale, comm, use_hip
         ctx.prescaled, ctx.fp32_mode = prescaled, fm
-        ctx.sbuf = sbuf  # consumed (overwritten with dS) by the first backward
+        ctx.sbuf = (sbuf, dsbuf)  # consumed by the first backward (in place: S overwritten with dS)
         return o
 
     @staticmethod
@@ -586,7 +587,8 @@ class SeqParallelAttention(torch.autograd.Function):
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
             # score buffer: S -> dS in the column kernel, then dK from dS; a second backward through
             # a retained graph recomputes (the buffer no longer holds S)
-            sbuf, ctx.sbuf = getattr(ctx, "sbuf", None), None
+            sbuf, dsbuf = getattr(ctx, "sbuf", None) or (None, None)
+            ctx.sbuf = None
             ev_cols = None
             with _on_stream(hi, cur):
                 delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
@@ -599,12 +601,23 @@ class SeqParallelAttention(torch.autograd.Function):
                 # keeps fp32): half the epilogue stores and half the reduce-scatter bytes
                 if one:
                     g = bufs[0]
-                    dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                            fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
-                                            fp32_mode=ctx.fp32_mode, sbuf=sbuf)
-                    if sbuf is not None:  # the row kernel reads the dS this kernel wrote
+                    cargs = dict(fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
+                                 fp32_mode=ctx.fp32_mode, sbuf=sbuf)
+                    if dsbuf is not None:
+                        # dQ pass (S -> dS), then the row kernel (reads dS) on `cur` concurrently
+                        # with the dV pass (reads S) here
+                        dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
+                                                dsbuf=dsbuf, passes=2, **cargs)
                         ev_cols = torch.cuda.Event()
                         ev_cols.record(hi)
+                        flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
+                                       dsbuf=dsbuf, passes=1, out_dkv=dkv, **cargs)
+                    else:
+                        dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
+                                                **cargs)
+                        if sbuf is not None:  # the row kernel reads the dS this kernel wrote
+                            ev_cols = torch.cuda.Event()
+                            ev_cols.record(hi)
                     off = 0
                     for r0, rc in chunks:  # (chunk, rank, row) order: chunk c's ranks are contiguous
                         part = dkv if len(chunks) == 1 else dkv[:, off:off + n * rc]
@@ -631,9 +644,11 @@ class SeqParallelAttention(torch.autograd.Function):
                 g = bufs[0]
                 dk = flash.bwd_rows(do, k, g[..., :C], g[..., C:], lse, delta, mks[0], H, scale,
                                     nsplit=FLAGS.rows_split, prescaled=ctx.prescaled, fp32_mode=ctx.fp32_mode,
-                                    sbuf=sbuf)
+                                    sbuf=sbuf, dsbuf=dsbuf)
                 if sbuf is not None:
                     sbuf.record_stream(cur)
+                if dsbuf is not None:
+                    dsbuf.record_stream(cur)
             else:
                 ops = _ext.ops()
                 ns = int(ops.flash_splits(B, R, n * chunks[0][1], H, True))

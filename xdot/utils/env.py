@@ -48,6 +48,8 @@ variable                    default   effect
                                       backward reads S / dS instead of recomputing them (6 fp32
                                       products per step instead of 9; needs R*T*H*4 bytes)
 ``XDOT_FP32_SCORES_FRAC``   0.5       ... only when that fits this fraction of the free device memory
+``XDOT_FP32_SCORES_DS``     1         ... and a second buffer for dS when both fit: the column side's
+                                      dV pass then runs concurrently with the row kernel
 ``XDOT_FUSED_MODULE``       1         the module's flash path as ONE autograd node (projections +
                                       attention + output projection, xdot/models/fused.py; 0: one
                                       node per op)
@@ -136,6 +138,7 @@ class _Flags:
         self.mask_async = _flag("XDOT_MASK_ASYNC")
         self.fp32_scores = _flag("XDOT_FP32_SCORES", default="1")
         self.fp32_scores_frac = _num("XDOT_FP32_SCORES_FRAC", 0.5)
+        self.fp32_scores_dsbuf = _flag("XDOT_FP32_SCORES_DS", default="1")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _num("XDOT_PROJ", 1, int)
