@@ -131,6 +131,9 @@ __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D /
   return acc;
 }
 
+#ifndef XDOT_F32_TRPD
+#define XDOT_F32_TRPD 1  // trprod operand read distance (tile indices ahead; A/B knob)
+#endif
 // out[db] += imgᵀ (d x tile index) · x (tile index x lane column), x = an accumulator tile
 // (the A operands of tile index s+1 are read while the MFMAs of s issue)
 template <int D>
@@ -145,27 +148,23 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
     for (int db = 0; db < DB; ++db) out[db] = mm(row[db * 32], x[s], out[db]);
   }
 #else
-  float r0[DB];
-  {
-    const float* row = img + 4 * hf * Cfg<D>::P + (lane & 31);
+  // ring of PD + 1 operand sets: tile index s + PD is read while the MFMAs of s issue (the loop
+  // is fully unrolled, so every ring slot is a compile-time register set)
+  constexpr int PD = XDOT_F32_TRPD;
+  float rr[PD + 1][DB];
+  auto rd = [&](int s, float (&dst)[DB]) {
+    const float* row = img + ((s & 3) + 8 * (s >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
 #pragma unroll
-    for (int db = 0; db < DB; ++db) r0[db] = row[db * 32];
-  }
+    for (int db = 0; db < DB; ++db) dst[db] = row[db * 32];
+  };
+#pragma unroll
+  for (int s = 0; s < PD; ++s) rd(s, rr[s]);
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    float r1[DB];
-    if (s + 1 < 16) {
-      const float* row = img + (((s + 1) & 3) + 8 * ((s + 1) >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
+    if (s + PD < 16) rd(s + PD, rr[(s + PD) % (PD + 1)]);
 #pragma unroll
-      for (int db = 0; db < DB; ++db) r1[db] = row[db * 32];
-    }
-#pragma unroll
-    for (int db = 0; db < DB; ++db) out[db] = mm(r0[db], x[s], out[db]);
+    for (int db = 0; db < DB; ++db) out[db] = mm(rr[s % (PD + 1)][db], x[s], out[db]);
     __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < 16) {
-#pragma unroll
-      for (int db = 0; db < DB; ++db) r0[db] = r1[db];
-    }
   }
 #endif
 }
