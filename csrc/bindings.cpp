@@ -599,7 +599,7 @@ float* sbuf_ptr(const c10::optional<at::Tensor>& sbuf, const FlashGeom& g, int64
   const auto& t = *sbuf;
   TORCH_CHECK(rows.scalar_type() == at::kFloat && (fp32_mode == 0 || fp32_mode == 1), what,
               ": the score buffer is an fp32 (exact or split) feature");
-  const int64_t need = g.B * H * ((g.R + 31) / 32) * ((g.T + 31) / 32) * 1024;
+  const int64_t need = (g.B * H * ((g.R + 31) / 32) * ((g.T + 31) / 32) + 1) * 1024;  // + the dump block
   TORCH_CHECK(t.is_cuda() && t.device() == rows.device() && t.scalar_type() == at::kFloat && t.is_contiguous() &&
                   t.numel() == need && aligned16(t.data_ptr()),
               what, ": score buffer must be a contiguous fp32 device tensor of ", need, " elements");

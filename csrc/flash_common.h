@@ -202,6 +202,11 @@ __device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x1
 #endif
 #endif
 }
+// float offset of the dump block after the last score block: writes of waves that own no block
+// (rows past R, columns past T) go there, so every wave issues the same stores every tile
+__device__ __forceinline__ int64_t sb_dump(int B, int H, int R, int T) {
+  return (int64_t)B * H * ((R + 31) / 32) * ((T + 31) / 32) * 1024;
+}
 __device__ __forceinline__ f32x16 blk_load(const float* blk, int lane) {
   const f32x4* p = reinterpret_cast<const f32x4*>(blk + 16 * lane);
   f32x16 x;
@@ -254,6 +259,33 @@ template <int PF, class F> __device__ __forceinline__ void ring_loop(int beg, in
     if constexpr (PF > 3)
       if (i0 + 3 < end) body(i0 + 3, Ic<3>{});
   }
+}
+
+// Row splits of a column-side launch: W workgroups of `nrt` 32-row tiles each, `slots` of them
+// resident at once.  Fewest splits minimising ceil(W s / slots) / s (the idle share of the last
+// round), each split >= 16 row tiles, 2 % charged per extra split (partials + their sum).
+inline int pick_csplit(int64_t W, int nrt, int slots) {
+  int best = 1;
+  double bc = 1e300;
+  for (int s = 1; s <= 4 && (s == 1 || nrt / s >= 16); ++s) {
+    const double c = (double)((W * s + slots - 1) / slots) / s * (1.0 + 0.02 * (s - 1));
+    if (c < bc * 0.98) {
+      bc = c;
+      best = s;
+    }
+  }
+  return best;
+}
+// resident workgroups per CU of one kernel instantiation (256 threads, `lds` bytes), cached
+template <class K> int wg_per_cu(K kern, int lds) {
+  static int v = 0;
+  if (!v) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kern), 256, lds) != hipSuccess || n < 1)
+      n = 1;
+    v = n;
+  }
+  return v;
 }
 
 // Pin MFMA accumulators to AGPRs (an empty asm with an "a" constraint).  Where accumulators and

@@ -203,7 +203,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < DB; ++i) o[i] = f32x16{};
   // score buffer: this wave's row of 32x32 blocks (r0 < R: waves past R never store)
-  float* sbw = SS ? a.sbuf + ((int64_t)bh * NRB32 + (r0 >> 5)) * NKT32 * 1024 : nullptr;
+  // (waves past R write the dump block after the last one: every wave stores every tile, so the
+  // store count per tile is uniform and the compiler's vmcnt waits stay exact)
+  float* sbw = SS ? a.sbuf + (r0 < a.R ? ((int64_t)bh * NRB32 + (r0 >> 5)) * NKT32 * 1024 : fa::sb_dump(a.B, a.H, a.R, a.T))
+                  : nullptr;
+  const int64_t sbw_step = r0 < a.R ? 1024 : 0;
 
   Stager<D> st;
   if (kt_beg < kt_end) {
@@ -218,9 +222,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     const float* vi = qi + CF::IMG;
     int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
+    f32x16 s{};
+    if (flag != 1) s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
+    // raw S, every tile (skipped tiles store zeros nobody reads)
+    if constexpr (SS) blk_store_lds(sbw + (int64_t)kt * sbw_step, sm + 2 * CF::STAGE + wave * 1024, s, lane);
     if (flag != 1) {
-      f32x16 s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
-      if constexpr (SS) blk_store_lds(sbw + (int64_t)kt * 1024, sm + 2 * CF::STAGE + wave * 1024, s, lane);  // raw S
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
@@ -446,11 +452,16 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   }
   // score buffer column of this wave: block (bh, rt, c0/32) at sbc + rt * NKT32 * 1024
   const bool sown = LS && c0 < a.T;
-  float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
-  float* dsc = LS ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : nullptr;
+  // loads of waves past T read a valid block, their dS stores go to the dump block: every wave
+  // loads and stores every tile (uniform counts keep the compiler's vmcnt waits exact)
+  float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024 : nullptr;
+  float* dsc = LS ? (sown ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024
+                          : (a.dsbuf ? a.dsbuf : a.sbuf) + fa::sb_dump(a.B, a.H, a.R, a.T))
+                  : nullptr;
+  const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
   const int64_t sstep = (int64_t)NKT32 * 1024;
   f32x16 snext{};
-  if (sown && NRT > 0) snext = blk_load(sbc, lane);
+  if (LS && NRT > 0) snext = blk_load(sbc, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
@@ -493,7 +504,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       ax = aux_load(rt + 1);
 #ifndef XDOT_AB_NO_S_LOAD
       if constexpr (LS)
-        if (sown) snext = blk_load(sbc + (rt + 1) * sstep, lane);
+        snext = blk_load(sbc + (rt + 1) * sstep, lane);
 #endif
     }
     const float* ki = sm + (rt & 1) * CF::STAGE;
@@ -501,15 +512,15 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     const float* ls = ki + 2 * CF::IMG;  // lse2[32], δ[32]
     int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
+    f32x16 s{}, dp{};
     if (flag != 1) {
-      f32x16 s;
 #ifdef XDOT_AB_NO_S_LOAD
       if constexpr (LS) s = f32x16{};
 #else
       if constexpr (LS) s = scur;                        // S  (row x col), stored by the forward
 #endif
       else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
-      f32x16 dp = rowprod<D>(di, vf, f32x16{}, lane);  // dP (row x col)
+      dp = rowprod<D>(di, vf, f32x16{}, lane);          // dP (row x col)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = tidx(r, hf);
@@ -523,9 +534,12 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         for (int r = 0; r < 16; ++r)
           if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
+    }
 #ifndef XDOT_AB_NO_DS_STORE
-      if constexpr (LS) blk_store_lds(dsc + rt * sstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);  // dS (over S or apart)
+    // dS (over S or apart), every tile (skipped tiles store zeros nobody reads)
+    if constexpr (LS) blk_store_lds(dsc + rt * dstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);
 #endif
+    if (flag != 1) {
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
       if constexpr (!LS) {
@@ -611,7 +625,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
     st.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (wave_ok && kt_beg + j < kt_end) q[j] = blk_load(sbr + (int64_t)(kt_beg + j) * 1024, lane);
+      if (kt_beg + j < kt_end) q[j] = blk_load(sbr + (int64_t)(kt_beg + j) * 1024, lane);
     st.store(sm, tid);
     __syncthreads();
   }
@@ -620,7 +634,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
     const bool more = kt + 1 < kt_end;
     f32x16 ds = q[j];
     if (more) st.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
-    if (wave_ok && kt + PF < kt_end) q[j] = blk_load(sbr + (int64_t)(kt + PF) * 1024, lane);
+    if (kt + PF < kt_end) q[j] = blk_load(sbr + (int64_t)(kt + PF) * 1024, lane);  // every wave: uniform vmcnt
     const float* qi = sm + ((kt - kt_beg) & 1) * CF::IMG;
     int flag = !wave_ok ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
@@ -670,7 +684,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
-  const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + (sown ? c0 >> 5 : 0)) * 1024;
+  const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024;  // valid for every wave
   const int64_t sstep = (int64_t)NKT32 * 1024;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
@@ -691,7 +705,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     ax = aux_load(0);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (sown && j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
+      if (j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
     st.store(sm, tid);
     if (tid < 32) sm[CF::IMG + tid] = ax;
     __syncthreads();
@@ -704,7 +718,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
       st.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
     }
-    if (sown && rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);
+    if (rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
     const float* di = sm + (rt & 1) * STG;
     const float* ls = di + CF::IMG;
     int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);

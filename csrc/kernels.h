@@ -98,6 +98,15 @@ struct BwdArgs {
   // row kernel (D <= 128 kernels)
   float* dsbuf;
   int sb_passes;           // column launch in score-buffer mode: bit 0 dV pass, bit 1 dQ pass (0: both)
+  // row splits of the fp32 column kernels (0 / 1: none).  A (b, h) x 128-column workgroup sweeps
+  // all R rows, so B*H*T/128 workgroups run in ceil(W / slots) rounds and a last round of a few
+  // workgroups idles the GPU (T = R = 25000, H = 8: 1568 workgroups over 512 slots = 3.06 rounds
+  // in 4).  With splits, workgroup (sp, b, h, cb) sweeps row tiles [sp NRT / s, (sp+1) NRT / s)
+  // and writes fp32 partials (s, B*T, H*D) to cpq (dQ, or both grads of the recompute kernel's
+  // main pass) / cpv (dV); xdot_flash_cols_sum_launch adds them up in order.
+  int csq, csv;
+  float* cpq;
+  float* cpv;
 };
 
 }  // namespace fa
@@ -226,6 +235,13 @@ int xdot_flash_combine_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t
 int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const void* out, float* delta, int D, hipStream_t st);
 int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
+// row splits the fp32 column launch would use (occupancy-aware round model): *sq for the dQ /
+// recompute pass, *sv for the dV pass (score-buffer mode); both 1 for other families
+int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D, int* sq, int* sv);
+int xdot_flash_cols_splits_f32(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
+int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
+// out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c] for r < rows, c < C (C % 4 == 0), fp32
+int xdot_flash_cols_sum_launch(const float* part, float* out, int S, int64_t rows, int C, int64_t ldo, hipStream_t st);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 // wide head dims (csrc/flash_wide.hip): D = 160 / 192 / 256 / 384, 16-bit and exact fp32 (a wide
 // fp32 launch always runs exact); -1 = not a wide (dtype, D), -2 = needs the score buffer (fp32 D > 256)

@@ -135,7 +135,7 @@ def test_flash_f32_score_buffer_checks(gpu):
     rows = torch.randn(1, 64, 128, device=gpu)
     kc = torch.randn(1, 96, 128, device=gpu)
     n = flash.score_buffer_numel(1, 2, 64, 96)
-    assert n == 2 * 2 * 3 * 1024
+    assert n == (2 * 2 * 3 + 1) * 1024  # + the dump block
     for fm in (0, 1):
         with pytest.raises(RuntimeError, match="score buffer"):
             flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=fm, sbuf=torch.empty(n - 1, device=gpu))

@@ -205,8 +205,9 @@ def fp32_code(dtype: torch.dtype, mode: Optional[str] = None) -> int:
 
 
 def score_buffer_numel(B: int, H: int, R: int, T: int) -> int:
-    """Floats of the fp32 score buffer: (B*H, ceil(R/32), ceil(T/32)) blocks of 32x32."""
-    return B * H * ((R + 31) // 32) * ((T + 31) // 32) * 1024
+    """Floats of the fp32 score buffer: (B*H, ceil(R/32), ceil(T/32)) blocks of 32x32, plus one
+    dump block the waves that own no block (rows past R, columns past T) write into."""
+    return (B * H * ((R + 31) // 32) * ((T + 31) // 32) + 1) * 1024
 
 
 def score_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tensor]:
