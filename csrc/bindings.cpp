@@ -739,6 +739,25 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
     TORCH_CHECK(xdot_flash_bwd_delta_launch(&a, out.data_ptr(), have_delta ? nullptr : delta.data_ptr<float>(), dt,
                                             (int)g.D, cur_stream(rows)) == 0,
                 "xdot.flash_bwd_cols: config");
+  // column kernels: row splits against the last-round tail (fp32 partials summed in the launcher;
+  // the exact / split fp32 kernels and the pipelined 16-bit kernel, else 1)
+  at::Tensor cpq, cpv;
+  if (dt != xdot::DT_F32 || (!a.prescaled && !a.dkv16)) {
+    int sq = 1, sv = 1;
+    TORCH_CHECK(xdot_flash_cols_splits(&a, dt, (int)g.D, &sq, &sv) == 0, "xdot.flash_bwd_cols: split config");
+    const bool run_q = !sb || (passes & 2), run_v = !sb || (passes & 1);
+    if (!sb) sv = sq;
+    if (run_q && sq > 1) {
+      cpq = at::empty({sq, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
+      a.cpq = cpq.data_ptr<float>();
+      a.csq = sq;
+    }
+    if (run_v && sv > 1) {
+      cpv = at::empty({sv, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
+      a.cpv = cpv.data_ptr<float>();
+      a.csv = sv;
+    }
+  }
   TORCH_CHECK(xdot_flash_bwd_cols_launch(&a, dt, (int)g.D, cur_stream(rows)) == 0, "xdot.flash_bwd_cols: config");
   check_launch(hipGetLastError(), "flash_bwd_cols");
   return {dkv, delta};

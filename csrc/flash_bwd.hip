@@ -552,6 +552,30 @@ __global__ __launch_bounds__(256) void flash_bwd_rows_sum(BwdArgs a) {
   *reinterpret_cast<u32x2*>(reinterpret_cast<T16*>(a.drows) + idx * 4) = w;
 }
 
+// column-side row-split partials (BwdArgs::csq / csv): out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c],
+// in split order (deterministic), fp32 partials -> output dtype
+template <int DT>
+__global__ __launch_bounds__(256) void cols_sum_kernel(const float* __restrict__ part, void* __restrict__ out_, int S,
+                                                        int64_t rows, int C, int64_t ldo) {
+  const int c4 = C / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * c4) return;
+  const int64_t r = idx / c4;
+  const int c = (int)(idx - r * c4) * 4;
+  const int64_t sl = rows * C;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(part + r * C + c);
+  for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(part + s * sl + r * C + c);
+  if constexpr (DT == DT_F32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out_) + r * ldo + c) = acc;
+  } else {
+    using T16 = typename dt_traits<DT>::T;
+    u32x2 w;
+    w[0] = pack2<DT>(acc[0], acc[1]);
+    w[1] = pack2<DT>(acc[2], acc[3]);
+    *reinterpret_cast<u32x2*>(reinterpret_cast<T16*>(out_) + r * ldo + c) = w;
+  }
+}
+
 template <int DT, int D>
 static void launch_bwd_delta(const BwdArgs& a, const void* out, float* delta, hipStream_t st) {
   const int64_t n0 = (int64_t)a.B * a.R * a.H;
@@ -635,6 +659,32 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
 #define XC(DTV, DV) launch_bwd_cols<DTV, DV>(*a, st)
   XB_DISPATCH(XC)
 #undef XC
+}
+
+extern "C" int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D, int* sq, int* sv) {
+  *sq = *sv = 1;
+  if (D > 128 || a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (dt != xdot::DT_F32) {  // the pipelined 16-bit column kernel (pre-scaled, D <= 96) only
+    if (D > 96 || !a->prescaled) return 0;
+    const int r = xdot_flash_cols_splits_cols2(a, dt, D, sq);
+    *sv = *sq;
+    return r;
+  }
+  return a->fp32_mode ? xdot_flash_cols_splits_x3(a, D, sq, sv) : xdot_flash_cols_splits_f32(a, D, sq, sv);
+}
+
+extern "C" int xdot_flash_cols_sum_launch(const float* part, void* out, int S, int64_t rows, int C, int64_t ldo, int dt,
+                                          hipStream_t st) {
+  using namespace xdot;
+  if (rows == 0 || C == 0) return 0;
+  if (C & 3) return -1;
+  const dim3 grid((unsigned)((rows * (C / 4) + 255) / 256));
+  switch (dt) {
+    case DT_F32: hipLaunchKernelGGL(fa::cols_sum_kernel<DT_F32>, grid, dim3(256), 0, st, part, out, S, rows, C, ldo); return 0;
+    case DT_BF16: hipLaunchKernelGGL(fa::cols_sum_kernel<DT_BF16>, grid, dim3(256), 0, st, part, out, S, rows, C, ldo); return 0;
+    case DT_F16: hipLaunchKernelGGL(fa::cols_sum_kernel<DT_F16>, grid, dim3(256), 0, st, part, out, S, rows, C, ldo); return 0;
+    default: return -1;
+  }
 }
 
 // sum a->nsplit slots of dpart into drows (input dtype)

@@ -3,6 +3,9 @@
 // the prep / sum kernels; flash_bwd.hip's launcher routes pre-scaled D <= 96 launches here.)
 #include "flash_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace xdot {
@@ -56,7 +59,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
   const Lanes L = make_lanes<D>(lane);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csq > 1 ? a.csq : 1;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int NKT = (a.T + 63) / 64;
@@ -87,7 +91,10 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
   }
   const char* vw = vimg + wave * 32 * ROW;  // this wave's 32 V rows (row_frag base, r0 = 0)
 
-  const int NRT = (a.R + 63) / 64;
+  // row split sp of ns (BwdArgs::csq, against the last-round tail): 64-row tiles [rt_beg, rt_end),
+  // rt_beg even (ring stage = tile parity)
+  const int NRT = (a.R + 63) / 64, NRT2 = (NRT + 1) / 2;
+  const int rt_beg = 2 * (int)((int64_t)sp * NRT2 / ns), rt_end = min(NRT, 2 * (int)((int64_t)(sp + 1) * NRT2 / ns));
   ImgDma<D> dma;
   dma.init(wave, lane, C * 2);
   const char* rows_b = reinterpret_cast<const char*>(reinterpret_cast<const T16*>(a.rows) + (int64_t)b * a.R * C + h * D);
@@ -228,12 +235,12 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
     }
   };
 
-  issue(0);
+  if (rt_beg < rt_end) issue(rt_beg);
   wait_vm<0>();
   __syncthreads();  // also publishes the V image (drains its LDS stores)
   auto tile = [&](auto bufc, int rt) {
     constexpr int BUF = decltype(bufc)::value;
-    if (rt + 1 < NRT) issue(rt + 1);
+    if (rt + 1 < rt_end) issue(rt + 1);
     char* ks = smem + BUF * CF::STAGE;
     const char* ds = ks + IMG;
     float* ls = reinterpret_cast<float*>(ks + CB::OFF_L);
@@ -253,12 +260,25 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
     wait_vm<0>();  // tile rt+1 landed (the only DMAs in flight)
     raw_barrier();
   };
-  for (int rt = 0; rt < NRT; rt += 2) {
+  for (int rt = rt_beg; rt < rt_end; rt += 2) {
     tile(std::integral_constant<int, 0>{}, rt);
-    if (rt + 1 < NRT) tile(std::integral_constant<int, 1>{}, rt + 1);
+    if (rt + 1 < rt_end) tile(std::integral_constant<int, 1>{}, rt + 1);
   }
   const float nscale = -LN2;  // dq was accumulated from -dS and K' = K * scale * log2 e
-  if (col_ok && a.dkv16) {
+  if (col_ok && ns > 1) {  // fp32 partials of split sp, (ns, B*T, C) per half
+    const int64_t off = (((int64_t)sp * a.B + b) * a.T + col) * C + h * D;
+    float* pq = a.cpq + off;
+    float* pv = a.cpv + off;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 q4 = {dq[db][4 * g] * nscale, dq[db][4 * g + 1] * nscale, dq[db][4 * g + 2] * nscale, dq[db][4 * g + 3] * nscale};
+        f32x4 v4 = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+        *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) = q4;
+        *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) = v4;
+      }
+  } else if (col_ok && a.dkv16) {
     const int64_t off = col_off(col, b, a.T, a.ldg) + h * D;
     T16* pq = reinterpret_cast<T16*>(a.dkc) + off;
     T16* pv = reinterpret_cast<T16*>(a.dvc) + off;
@@ -297,13 +317,48 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
 extern "C" int xdot_flash_bwd_cols2_launch(const xdot::fa::BwdArgs* a, int dt, int D, hipStream_t st) {
   using namespace xdot;
   using namespace xdot::fa;
-  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+  const int ns = a->csq > 1 ? a->csq : 1;
+  if (ns > 1 && (!a->cpq || !a->cpv || (D & 3))) return -1;
+  const dim3 grid(((a->T + 127) / 128) * a->B * a->H * ns);
+  const int odt = a->dkv16 ? dt : (int)DT_F32;
+  const int64_t rows = (int64_t)a->B * a->T;
 #define XC2(DTV, DV)                                                                                   \
   if (dt == DTV && D == DV) {                                                                          \
     hipLaunchKernelGGL((flash_bwd_cols2_kernel<DTV, DV>), grid, dim3(256), Cols2Cfg<DV>::LDS, st, *a); \
+    if (ns > 1) {                                                                                      \
+      xdot_flash_cols_sum_launch(a->cpq, a->dkc, ns, rows, a->H * D, a->ldg, odt, st);                 \
+      xdot_flash_cols_sum_launch(a->cpv, a->dvc, ns, rows, a->H * D, a->ldg, odt, st);                 \
+    }                                                                                                  \
     return 0;                                                                                          \
   }
   XC2(DT_BF16, 32) XC2(DT_BF16, 64) XC2(DT_BF16, 96) XC2(DT_F16, 32) XC2(DT_F16, 64) XC2(DT_F16, 96)
 #undef XC2
   return -1;
+}
+
+namespace {
+int cols2_csplit_env() {  // XDOT_CSPLIT, as in flash_f32.hip
+  const char* e = std::getenv("XDOT_CSPLIT");
+  return (!e || !*e || !std::strcmp(e, "auto")) ? -1 : std::max(1, std::min(4, std::atoi(e)));
+}
+}  // namespace
+
+// row splits of the pipelined column kernel: XDOT_CSPLIT=n only (opt-in)
+extern "C" int xdot_flash_cols_splits_cols2(const xdot::fa::BwdArgs* a, int dt, int D, int* sq) {
+  using namespace xdot;
+  using namespace xdot::fa;
+  *sq = 1;
+  const int NRT = (a->R + 63) / 64;
+  const int e = cols2_csplit_env();
+  if (e >= 0) {
+    *sq = (NRT + 1) / 2 / e >= 1 ? e : 1;
+    return 0;
+  }
+  // automatic choice: none.  Measured on MI355X (profiles/r5_fp32.md §2b): T = R = 25000, h = 8
+  // 3.68 -> 3.49 ms for the kernel, but the fp32 partials (3 x 154 MB written and read back)
+  // cost more than that in the step (7.84 -> 8.08 ms); at the N=8 rank shape 0.51 -> 0.71 ms.
+  // The tail workgroups of this short kernel run faster alone than the round model assumes.
+  (void)dt;
+  (void)D;
+  return 0;
 }

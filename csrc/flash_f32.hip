@@ -37,6 +37,10 @@
 // 1024 floats; within a block a tile sits in the READER's accumulator order (16 floats per lane,
 // 4 x b128 loads), the writer scatters (blk_store).  Tiles the mask flags skip are neither
 // written nor read.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "flash_common.h"
 
 namespace xdot {
@@ -435,7 +439,8 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csq > 1 ? a.csq : 1;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -443,6 +448,8 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  // row split sp of ns: row tiles [rt_beg, rt_end)
+  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
 
   float qf[LS ? 1 : D / 2], vf[D / 2];
   {
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
   const int64_t sstep = (int64_t)NKT32 * 1024;
   f32x16 snext{};
-  if (LS && NRT > 0) snext = blk_load(sbc, lane);
+  if (LS && rt_beg < rt_end) snext = blk_load(sbc + rt_beg * sstep, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
@@ -488,15 +495,15 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   };
   Stager<D> st;
   float ax = 0.f;
-  if (NRT > 0) {
-    st.load(kb, db_, C, 0, a.R - 1, tid);
-    ax = aux_load(0);
+  if (rt_beg < rt_end) {
+    st.load(kb, db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    ax = aux_load(rt_beg);
     st.store(sm, tid);
     if (tid < 64) sm[2 * CF::IMG + tid] = ax;
     __syncthreads();
   }
-  for (int rt = 0; rt < NRT; ++rt) {
-    const bool more = rt + 1 < NRT;
+  for (int rt = rt_beg; rt < rt_end; ++rt) {
+    const bool more = rt + 1 < rt_end;
     f32x16 scur;
     if constexpr (LS) scur = snext;
     if (more) {
@@ -507,7 +514,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         snext = blk_load(sbc + (rt + 1) * sstep, lane);
 #endif
     }
-    const float* ki = sm + (rt & 1) * CF::STAGE;
+    const float* ki = sm + ((rt - rt_beg) & 1) * CF::STAGE;
     const float* di = ki + CF::IMG;
     const float* ls = ki + 2 * CF::IMG;  // lse2[32], δ[32]
     int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
@@ -548,15 +555,16 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       }
     }
     if (more) {
-      float* nx = sm + ((rt + 1) & 1) * CF::STAGE;
+      float* nx = sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE;
       st.store(nx, tid);
       if (tid < 64) nx[2 * CF::IMG + tid] = ax;
     }
     __syncthreads();
   }
   if (!col_ok) return;
-  float* pq = reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
-  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  const int64_t prow = ((int64_t)sp * a.B + b) * a.T + col;  // row of the split partials
+  float* pq = ns > 1 ? a.cpq + prow * C + h * D : reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = ns > 1 ? a.cpv + prow * C + h * D : reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
   const float sc = a.scale;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
@@ -676,7 +684,8 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csv > 1 ? a.csv : 1;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -684,6 +693,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
   const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024;  // valid for every wave
   const int64_t sstep = (int64_t)NKT32 * 1024;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
@@ -700,26 +710,26 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   Stager1<D> st;
   f32x16 q[PF];
   float ax = 0.f;
-  if (NRT > 0) {
-    st.load(db_, C, 0, a.R - 1, tid);
-    ax = aux_load(0);
+  if (rt_beg < rt_end) {
+    st.load(db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    ax = aux_load(rt_beg);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
+      if (rt_beg + j < rt_end) q[j] = blk_load(sbc + (rt_beg + j) * sstep, lane);
     st.store(sm, tid);
     if (tid < 32) sm[CF::IMG + tid] = ax;
     __syncthreads();
   }
-  fa::ring_loop<PF>(0, NRT, [&](int rt, auto J) {
+  fa::ring_loop<PF>(rt_beg, rt_end, [&](int rt, auto J) {
     constexpr int j = decltype(J)::value;
-    const bool more = rt + 1 < NRT;
+    const bool more = rt + 1 < rt_end;
     f32x16 s = q[j];
     if (more) {
       st.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
     }
-    if (rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
-    const float* di = sm + (rt & 1) * STG;
+    if (rt + PF < rt_end) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
+    const float* di = sm + ((rt - rt_beg) & 1) * STG;
     const float* ls = di + CF::IMG;
     int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
@@ -735,14 +745,15 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
       trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
     }
     if (more) {
-      float* nx = sm + ((rt + 1) & 1) * STG;
+      float* nx = sm + ((rt + 1 - rt_beg) & 1) * STG;
       st.store(nx, tid);
       if (tid < 32) nx[CF::IMG + tid] = ax;
     }
     __syncthreads();
   });
   if (!col_ok) return;
-  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = ns > 1 ? a.cpv + (((int64_t)sp * a.B + b) * a.T + col) * C + h * D
+                     : reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -828,24 +839,83 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   using namespace xdot::fa32;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
-  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+  const int W = ((a->T + 127) / 128) * a->B * a->H, sq = a->csq > 1 ? a->csq : 1, sv = a->csv > 1 ? a->csv : 1;
+  if ((sq > 1 && (!a->cpq || (!a->sbuf && !a->cpv))) || (sv > 1 && !a->cpv) || (D & 3)) return -1;
+  const int64_t rows = (int64_t)a->B * a->T;
+  const int C = a->H * D;
+  // the split partials of one pass, summed into its grad half (fp32, ldg-strided)
+  auto sum_q = [&] {
+    if (sq > 1) xdot_flash_cols_sum_launch(a->cpq, a->dkc, sq, rows, C, a->ldg, xdot::DT_F32, st);
+  };
+  auto sum_v = [&](int s) {
+    if (s > 1) xdot_flash_cols_sum_launch(a->cpv, a->dvc, s, rows, C, a->ldg, xdot::DT_F32, st);
+  };
   if (a->sbuf) {  // in place: dV from S first, then dQ (S -> dS); with a dS buffer dQ first
     const int ps = a->sb_passes ? a->sb_passes : 3;
     const bool dv_first = !a->dsbuf;
-#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a)
-#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
+#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, dim3(W * sv), dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a)
+#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), dim3(W * sq), dim3(256), lds_bytes_sb<DV>(), st, *a)
 #define L(DV)                            \
-  if ((ps & 1) && dv_first) LDV(DV);     \
-  if (ps & 2) LDQ(DV);                   \
-  if ((ps & 1) && !dv_first) LDV(DV)
+  if ((ps & 1) && dv_first) {            \
+    LDV(DV);                             \
+    sum_v(sv);                           \
+  }                                      \
+  if (ps & 2) {                          \
+    LDQ(DV);                             \
+    sum_q();                             \
+  }                                      \
+  if ((ps & 1) && !dv_first) {           \
+    LDV(DV);                             \
+    sum_v(sv);                           \
+  }
     XF32_DISPATCH(L)
 #undef L
 #undef LDQ
 #undef LDV
   }
-#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+#define L(DV)                                                                                                \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), dim3(W * sq), dim3(256), lds_bytes<DV>(), st, *a); \
+  sum_q();                                                                                                   \
+  sum_v(sq)
   XF32_DISPATCH(L)
 #undef L
+}
+
+namespace {
+// XDOT_CSPLIT: unset / "auto" = occupancy round model, "0" / "1" = no split, n = n splits (<= 4)
+int csplit_env() {
+  const char* e = std::getenv("XDOT_CSPLIT");  // read per call (tests switch it)
+  return (!e || !*e || !std::strcmp(e, "auto")) ? -1 : std::max(1, std::min(4, std::atoi(e)));
+}
+template <int D> void f32_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
+  using namespace xdot::fa32;
+  const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H;
+  const int NRT = (a->R + 31) / 32, cus = xdot_num_cus();
+  if (a->sbuf) {
+    *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_sb<D>()));
+    *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, 2 * (Cfg<D>::IMG + 32) * 4));
+  } else {
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false>, lds_bytes<D>()));
+  }
+}
+}  // namespace
+
+extern "C" int xdot_flash_cols_splits_f32(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv) {
+  *sq = *sv = 1;
+  const int e = csplit_env();
+  if (e >= 0) {
+    const int NRT = (a->R + 31) / 32;
+    *sq = *sv = NRT / e >= 1 ? e : 1;
+    return 0;
+  }
+  switch (D) {
+    case 32: f32_splits<32>(a, sq, sv); break;
+    case 64: f32_splits<64>(a, sq, sv); break;
+    case 96: f32_splits<96>(a, sq, sv); break;
+    case 128: f32_splits<128>(a, sq, sv); break;
+    default: return -1;
+  }
+  return 0;
 }
 
 extern "C" int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {

@@ -22,6 +22,10 @@
 //     slots permuted so that lane half h of K step j reads tile rows tidx(8j + t, h), t = 0..7,
 //     i.e. the accumulator registers 8j..8j+7 of the previous product (B operand straight from
 //     the accumulator, split in registers).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "flash_common.h"
 
 namespace xdot {
@@ -448,7 +452,8 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csq > 1 ? a.csq : 1;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -456,6 +461,8 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32;
+  // row split sp of ns (BwdArgs::csq): row tiles [rt_beg, rt_end)
+  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
 
   constexpr int QS = LS ? 1 : CF::KS;
   u32x4 qh[QS], ql[QS], vh[CF::KS], vl[CF::KS];
@@ -474,7 +481,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
   const int64_t sstep = (int64_t)NKT32 * 1024;
   f32x16 snext{};
-  if (LS && NRT > 0) snext = blk_load(sbc, lane);
+  if (LS && rt_beg < rt_end) snext = blk_load(sbc + rt_beg * sstep, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
@@ -504,15 +511,15 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   };
   Tile<D> tk, td;
   float ax = 0.f;
-  if (NRT > 0) {
-    tk.load(kb, C, 0, a.R - 1, tid);
-    td.load(db_, C, 0, a.R - 1, tid);
-    ax = aux_load(0);
+  if (rt_beg < rt_end) {
+    tk.load(kb, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    td.load(db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    ax = aux_load(rt_beg);
     put(smem, tk, td, ax);
     __syncthreads();
   }
-  for (int rt = 0; rt < NRT; ++rt) {
-    const bool more = rt + 1 < NRT;
+  for (int rt = rt_beg; rt < rt_end; ++rt) {
+    const bool more = rt + 1 < rt_end;
     f32x16 scur;
     if constexpr (LS) scur = snext;
     if (more) {
@@ -522,7 +529,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       if constexpr (LS)
         snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
-    const char* ki = smem + (rt & 1) * KL::STAGE;
+    const char* ki = smem + ((rt - rt_beg) & 1) * KL::STAGE;
     const char* di = ki + KL::K::BYTES;
     const float* ls = reinterpret_cast<const float*>(di + KL::DO::BYTES);  // lse2[32], δ[32]
     int flag = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
@@ -558,12 +565,13 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         fa::pin_agpr(dv);
       }
     }
-    if (more) put(smem + ((rt + 1) & 1) * KL::STAGE, tk, td, ax);
+    if (more) put(smem + ((rt + 1 - rt_beg) & 1) * KL::STAGE, tk, td, ax);
     __syncthreads();
   }
   if (!col_ok) return;
-  float* pq = reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
-  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  const int64_t prow = ((int64_t)sp * a.B + b) * a.T + col;  // row of the split partials
+  float* pq = ns > 1 ? a.cpq + prow * C + h * D : reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = ns > 1 ? a.cpv + prow * C + h * D : reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
   const float sc = a.scale;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
@@ -597,7 +605,8 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csv > 1 ? a.csv : 1;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -605,6 +614,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
   const float* sbc = a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024;  // valid for every wave
   const int64_t sstep = (int64_t)NKT32 * 1024;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
@@ -621,26 +631,26 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
   Tile<D> td;
   f32x16 q[PF];
   float ax = 0.f;
-  if (NRT > 0) {
-    td.load(db_, C, 0, a.R - 1, tid);
-    ax = aux_load(0);
+  if (rt_beg < rt_end) {
+    td.load(db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    ax = aux_load(rt_beg);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-      if (j < NRT) q[j] = blk_load(sbc + j * sstep, lane);
+      if (rt_beg + j < rt_end) q[j] = blk_load(sbc + (rt_beg + j) * sstep, lane);
     td.template store<false, true>(smem, tid);
     if (tid < 32) reinterpret_cast<float*>(smem + VL::DO::BYTES)[tid] = ax;
     __syncthreads();
   }
-  fa::ring_loop<PF>(0, NRT, [&](int rt, auto J) {
+  fa::ring_loop<PF>(rt_beg, rt_end, [&](int rt, auto J) {
     constexpr int j = decltype(J)::value;
-    const bool more = rt + 1 < NRT;
+    const bool more = rt + 1 < rt_end;
     f32x16 s = q[j];
     if (more) {
       td.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
     }
-    if (rt + PF < NRT) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
-    const char* di = smem + (rt & 1) * VL::STAGE;
+    if (rt + PF < rt_end) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
+    const char* di = smem + ((rt - rt_beg) & 1) * VL::STAGE;
     const float* ls = reinterpret_cast<const float*>(di + VL::DO::BYTES);
     int flag = !sown ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, rt, c0 >> 6) : 0);
     flag = __builtin_amdgcn_readfirstlane(flag);
@@ -656,14 +666,15 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
       trprod<D, false, true>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
     }
     if (more) {
-      char* nx = smem + ((rt + 1) & 1) * VL::STAGE;
+      char* nx = smem + ((rt + 1 - rt_beg) & 1) * VL::STAGE;
       td.template store<false, true>(nx, tid);
       if (tid < 32) reinterpret_cast<float*>(nx + VL::DO::BYTES)[tid] = ax;
     }
     __syncthreads();
   });
   if (!col_ok) return;
-  float* pv = reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* pv = ns > 1 ? a.cpv + (((int64_t)sp * a.B + b) * a.T + col) * C + h * D
+                     : reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -796,22 +807,78 @@ extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   using namespace xdot::fa3;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled || a->dkv16) return -1;
-  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+  const int W = ((a->T + 127) / 128) * a->B * a->H, sq = a->csq > 1 ? a->csq : 1, sv = a->csv > 1 ? a->csv : 1;
+  if ((sq > 1 && (!a->cpq || (!a->sbuf && !a->cpv))) || (sv > 1 && !a->cpv) || (D & 3)) return -1;
+  const int64_t rows = (int64_t)a->B * a->T;
+  const int C = a->H * D;
+  auto sum_q = [&] {  // split partials of a pass summed into its grad half (BwdArgs::csq / csv)
+    if (sq > 1) xdot_flash_cols_sum_launch(a->cpq, a->dkc, sq, rows, C, a->ldg, xdot::DT_F32, st);
+  };
+  auto sum_v = [&](int s) {
+    if (s > 1) xdot_flash_cols_sum_launch(a->cpv, a->dvc, s, rows, C, a->ldg, xdot::DT_F32, st);
+  };
   if (a->sbuf) {  // in place: dV from S first, then dQ (S -> dS); with a dS buffer dQ first
     const int ps = a->sb_passes ? a->sb_passes : 3;
     const bool dv_first = !a->dsbuf;
-#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, grid, dim3(256), DvL<DV>::LDS, st, *a)
-#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), grid, dim3(256), (ColsL<DV, true>::LDS), st, *a)
+#define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, dim3(W * sv), dim3(256), DvL<DV>::LDS, st, *a)
+#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), dim3(W * sq), dim3(256), (ColsL<DV, true>::LDS), st, *a)
 #define L(DV)                            \
-  if ((ps & 1) && dv_first) LDV(DV);     \
-  if (ps & 2) LDQ(DV);                   \
-  if ((ps & 1) && !dv_first) LDV(DV)
+  if ((ps & 1) && dv_first) {            \
+    LDV(DV);                             \
+    sum_v(sv);                           \
+  }                                      \
+  if (ps & 2) {                          \
+    LDQ(DV);                             \
+    sum_q();                             \
+  }                                      \
+  if ((ps & 1) && !dv_first) {           \
+    LDV(DV);                             \
+    sum_v(sv);                           \
+  }
     X3_DISPATCH(L)
 #undef L
 #undef LDQ
 #undef LDV
   }
-#define L(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), grid, dim3(256), (ColsL<DV, false>::LDS), st, *a)
+#define L(DV)                                                                                                          \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), dim3(W * sq), dim3(256), (ColsL<DV, false>::LDS), st, *a); \
+  sum_q();                                                                                                             \
+  sum_v(sq)
   X3_DISPATCH(L)
 #undef L
+}
+
+namespace {
+int x3_csplit_env() {  // XDOT_CSPLIT, as in flash_f32.hip
+  const char* e = std::getenv("XDOT_CSPLIT");  // read per call (tests switch it)
+  return (!e || !*e || !std::strcmp(e, "auto")) ? -1 : std::max(1, std::min(4, std::atoi(e)));
+}
+template <int D> void x3_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
+  using namespace xdot::fa3;
+  const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H;
+  const int NRT = (a->R + 31) / 32, cus = xdot_num_cus();
+  if (a->sbuf) {
+    *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, ColsL<D, true>::LDS));
+    *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, DvL<D>::LDS));
+  } else {
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false>, ColsL<D, false>::LDS));
+  }
+}
+}  // namespace
+
+extern "C" int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv) {
+  *sq = *sv = 1;
+  const int e = x3_csplit_env();
+  if (e >= 0) {
+    *sq = *sv = (a->R + 31) / 32 / e >= 1 ? e : 1;
+    return 0;
+  }
+  switch (D) {
+    case 32: x3_splits<32>(a, sq, sv); break;
+    case 64: x3_splits<64>(a, sq, sv); break;
+    case 96: x3_splits<96>(a, sq, sv); break;
+    case 128: x3_splits<128>(a, sq, sv); break;
+    default: return -1;
+  }
+  return 0;
 }

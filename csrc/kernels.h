@@ -240,8 +240,11 @@ int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_
 int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D, int* sq, int* sv);
 int xdot_flash_cols_splits_f32(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
 int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
-// out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c] for r < rows, c < C (C % 4 == 0), fp32
-int xdot_flash_cols_sum_launch(const float* part, float* out, int S, int64_t rows, int C, int64_t ldo, hipStream_t st);
+// out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c] for r < rows, c < C (C % 4 == 0): fp32
+// partials, output in dtype `dt` (DT_F32 / DT_BF16 / DT_F16)
+int xdot_flash_cols_sum_launch(const float* part, void* out, int S, int64_t rows, int C, int64_t ldo, int dt,
+                               hipStream_t st);
+int xdot_flash_cols_splits_cols2(const xdot::fa::BwdArgs* a, int dt, int D, int* sq);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 // wide head dims (csrc/flash_wide.hip): D = 160 / 192 / 256 / 384, 16-bit and exact fp32 (a wide
 // fp32 launch always runs exact); -1 = not a wide (dtype, D), -2 = needs the score buffer (fp32 D > 256)

@@ -365,3 +365,51 @@ def test_flash_split_column_split_and_exact_module(gpu):
         FLAGS.fp32_mode = old
     assert _rel(out, ro) <= 3e-5
     assert _rel(x.grad, xd.grad) <= 1e-4
+
+
+# ---- column-side row splits (BwdArgs::csq / csv, XDOT_CSPLIT): the fp32 column kernels cut the
+# R rows into s ranges against the last-round tail; fp32 partials are summed in order ------------
+@pytest.mark.parametrize("fm", [0, 1])
+@pytest.mark.parametrize("mode", ["recompute", "inplace", "dsbuf"])
+def test_flash_f32_column_row_splits(gpu, monkeypatch, fm, mode):
+    """Row splits 2 / 3 / 4 and the automatic choice match the unsplit column grads (another
+    summation order: <= 1e-6 exact, <= 2e-5 split family) and the fp64 reference; the dQ-first
+    + separate-dS schedule runs each pass with its own split count."""
+    from xdot.ops import flash
+
+    case = (1, 2100, 1, 1500, 2, 96)  # 66 row tiles: up to 4 splits of >= 16
+    B, R, N, Rc, H, D = case
+    T, C = N * Rc, H * D
+    rows, kc, vc, do, mask = _inputs(case, "blocks", gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    tol = 1e-6 if fm == 0 else 2e-5
+
+    def cols():
+        if mode == "recompute":
+            o, l = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=fm)
+            return flash.bwd_cols(do, rows, kb, vb, o, l, mk, H, scale, fp32_mode=fm)[0]
+        sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)
+        o, l = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=fm, sbuf=sb)
+        if mode == "inplace":
+            return flash.bwd_cols(do, rows, kb, vb, o, l, mk, H, scale, fp32_mode=fm, sbuf=sb)[0]
+        ds = torch.full_like(sb, float("nan"))
+        dkv, dl = flash.bwd_cols(do, rows, kb, vb, o, l, mk, H, scale, fp32_mode=fm, sbuf=sb, dsbuf=ds, passes=2)
+        flash.bwd_cols(do, rows, kb, vb, o, l, mk, H, scale, delta=dl, fp32_mode=fm, sbuf=sb, dsbuf=ds,
+                       passes=1, out_dkv=dkv)
+        return dkv
+
+    monkeypatch.setenv("XDOT_CSPLIT", "1")
+    base = cols()
+    k, q, v, ref_o, _ = _ref64(rows, kc, vc, mask, H, scale)
+    ref_o.backward(do.double())
+    refq, refv = _to_gathered(q.grad, N, B, Rc, C), _to_gathered(v.grad, N, B, Rc, C)
+    for s in ("2", "3", "4", "auto"):
+        monkeypatch.setenv("XDOT_CSPLIT", s)
+        got = cols()
+        assert torch.isfinite(got).all(), s
+        assert _rel(got, base) <= tol, f"splits {s}: {_rel(got, base):.2e}"
+        for what, g_, r_ in (("q", got[..., :C], refq), ("v", got[..., C:], refv)):
+            err = _rel(flash.btc_to_rank_major(g_.contiguous(), N), r_)
+            assert err <= (2e-6 if fm == 0 else 2e-5), f"splits {s} d cols ({what}): {err:.2e}"

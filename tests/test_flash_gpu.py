@@ -344,3 +344,53 @@ def test_flash_head_heavy_grid(gpu, prescaled):
     # whole blocks are bitwise the uniform launch's; tail rows agree to bf16 rounding
     assert torch.equal(out[:, : 64 * 128], o1[:, : 64 * 128])
     assert (out[:, keep].float() - o1[:, keep].float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mask_kind", ["none", "blocks"])
+def test_flash_cols_row_splits(gpu, monkeypatch, dt, mask_kind):
+    """Row splits of the pipelined 16-bit column kernel (pre-scaled, D <= 96; BwdArgs::csq,
+    XDOT_CSPLIT): fp32 partials of 2 / 3 / 4 row ranges and the automatic choice match the
+    unsplit grads (fp32 output: <= 1e-5, another summation order of the same products; 16-bit
+    output: one rounding) and the torch fp32 reference."""
+    from xdot.ops import flash
+
+    B, R, N, Rc, H, D = 1, 2600, 1, 1500, 2, 96  # 41 row tiles of 64
+    C, T = H * D, N * Rc
+    g = torch.Generator(device="cpu").manual_seed(7)
+    rows = torch.randn(B, R, C, generator=g).to(gpu, dt)
+    kc = torch.randn(N, B, Rc, C, generator=g).to(gpu, dt)
+    vc = torch.randn(N, B, Rc, C, generator=g).to(gpu, dt)
+    do = torch.randn(B, R, C, generator=g).to(gpu, dt)
+    mask = None
+    if mask_kind == "blocks":
+        mask = torch.zeros(B, R, T, dtype=torch.bool)
+        mask[:, :, :128] = True
+        mask[:, 40:900, 128:] = torch.rand(B, 860, T - 128, generator=g) < 0.5
+        mask[..., T - 1] = False
+        mask = mask.to(gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    rk = flash.prescale(rows, scale)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    out, lse = flash.fwd(rk, kb, vb, mk, H, scale, prescaled=True)
+
+    def cols(fp32_out):
+        return flash.bwd_cols(do, rk, kb, vb, out, lse, mk, H, scale, fp32_out=fp32_out, prescaled=True)[0]
+
+    monkeypatch.setenv("XDOT_CSPLIT", "1")
+    base32, base16 = cols(True), cols(False)
+    k, q, v, ref_o, _ = _ref(rows, kc, vc, mask, H, scale)
+    ref_o.backward(do.float())
+    refq, refv = _to_gathered(q.grad, N, B, Rc, C), _to_gathered(v.grad, N, B, Rc, C)
+    gfro = 1.5e-2 if dt == torch.bfloat16 else 4e-3
+    for s in ("2", "3", "4", "auto"):
+        monkeypatch.setenv("XDOT_CSPLIT", s)
+        g32, g16 = cols(True), cols(False)
+        assert g16.dtype == dt and g32.dtype == torch.float32
+        r32 = ((g32 - base32).norm() / base32.norm()).item()
+        r16 = ((g16.float() - base16.float()).norm() / base16.float().norm()).item()
+        assert r32 <= 1e-5, f"splits {s}: fp32 out {r32:.2e}"
+        assert r16 <= (8e-3 if dt == torch.bfloat16 else 1e-3), f"splits {s}: 16-bit out {r16:.2e}"
+        _close(f"splits {s} d cols (q)", flash.btc_to_rank_major(g16[..., :C].contiguous(), N), refq, gfro)
+        _close(f"splits {s} d cols (v)", flash.btc_to_rank_major(g16[..., C:].contiguous(), N), refv, gfro)

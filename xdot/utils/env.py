@@ -81,6 +81,10 @@ variable                    default   effect
                                       default, kept for A/B), 1 = 16-bit ones too
 ``XDOT_GEMM3`` (C++)        1         16-bit products with M, N >= 256 and beta = 0 run the 8-phase
                                       16x16x32 kernel (``csrc/gemm3.hip``; 0: the 256x256 v2 kernel)
+``XDOT_CSPLIT`` (C++)        auto      row splits of the fp32 column kernels against the last-round
+                                      tail (fp32 partials, ordered sum; auto: occupancy round
+                                      model; n: n splits <= 4, also for the 16-bit pipelined kernel,
+                                      whose auto is 1)
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
 ==========================  ========  ===========================================================
 
