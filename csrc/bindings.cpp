@@ -619,7 +619,11 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   const int64_t NB = ((g.R + rpw - 1) / rpw) * g.B * H;
   int hw = 0, hr = 0, hs = 0;
   const bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && g.D <= 128 && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
-  const int ns = heavy ? hs : pick_split(NB, g.T, 512, nsplit);
+  int ns = heavy ? hs : pick_split(NB, g.T, 512, nsplit);
+  if (nsplit == 0 && rows.scalar_type() == at::kFloat) {  // fp32 kernels: their own occupancy / tile model
+    const int f = xdot_flash_f32_row_splits(0, (int)fp32_mode, (int)g.D, sb != nullptr, NB, g.T);
+    if (f > 0) ns = f;
+  }
   at::Tensor opart, lpart;
   if (heavy) {  // compact partials of the split tail blocks only
     opart = at::empty({(int64_t)hs * 8 * hr * 128 * g.D}, rows.options().dtype(at::kFloat));
@@ -1084,7 +1088,12 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
               "xdot.flash_bwd_rows: delta");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   auto drows = at::empty_like(rows);
-  const int ns = nsplit > 0 ? pick_split(1, g.T, 1, nsplit) : rows_split(g.B, g.R, g.T, H);
+  int ns = nsplit > 0 ? pick_split(1, g.T, 1, nsplit) : rows_split(g.B, g.R, g.T, H);
+  if (nsplit == 0 && rows.scalar_type() == at::kFloat) {
+    const int f = xdot_flash_f32_row_splits(1, (int)fp32_mode, (int)g.D, sb != nullptr,
+                                            ((g.R + 127) / 128) * g.B * H, g.T);
+    if (f > 0) ns = f;
+  }
   at::Tensor dpart;
   if (ns > 1) dpart = at::empty({ns, g.B, g.R, g.C}, rows.options().dtype(at::kFloat));
   a.delta = delta.data_ptr<float>(); a.drows = drows.data_ptr();

@@ -24,6 +24,10 @@
 // packed registers; the one operand that must be transposed is read with ds_read_b64_tr_b16.
 #include "flash_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include <type_traits>
 
 namespace xdot {
@@ -675,6 +679,25 @@ extern "C" int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D,
     return r;
   }
   return a->fp32_mode ? xdot_flash_cols_splits_x3(a, D, sq, sv) : xdot_flash_cols_splits_f32(a, D, sq, sv);
+}
+
+// XDOT_F32_SPLIT: unset / "auto" = the occupancy round model for the fp32 forward and row-side
+// backward (measured r5s20: step 55.99 -> 55.23 ms, forward 16.61 -> 16.05, rows 8.63 -> 8.46);
+// "fwd" = the model for the forward only; "old" = the 16-bit model (pick_split / rows_split) for
+// both; n = n splits for both.  Returns 0 when the caller should use its own model.
+extern "C" int xdot_flash_f32_row_splits(int kernel, int fp32_mode, int D, bool sbuf, int64_t W, int64_t T) {
+  if (D > 128 || W <= 0 || T <= 0) return 0;
+  const char* e = std::getenv("XDOT_F32_SPLIT");
+  const bool dflt = !e || !*e || !std::strcmp(e, "auto");
+  if (!dflt && !std::strcmp(e, "old")) return 0;
+  if (!dflt && !std::strcmp(e, "fwd")) {
+    if (kernel == 1) return 0;
+  } else if (!dflt) {
+    const int n = std::atoi(e);
+    return n > 0 ? std::min<int64_t>(n, (T + 31) / 32) : 0;
+  }
+  return fp32_mode ? xdot_flash_f32_row_splits_x3(kernel, D, sbuf, W, T)
+                   : xdot_flash_f32_row_splits_exact(kernel, D, sbuf, W, T);
 }
 
 extern "C" int xdot_flash_cols_sum_launch(const float* part, void* out, int S, int64_t rows, int C, int64_t ldo, int dt,

@@ -264,11 +264,13 @@ template <int PF, class F> __device__ __forceinline__ void ring_loop(int beg, in
 // Row splits of a column-side launch: W workgroups of `nrt` 32-row tiles each, `slots` of them
 // resident at once.  Fewest splits minimising ceil(W s / slots) / s (the idle share of the last
 // round), each split >= 16 row tiles, 2 % charged per extra split (partials + their sum).
-inline int pick_csplit(int64_t W, int nrt, int slots) {
+// (The fp32 forward / row kernels use it with up to 8 splits at 0.4 % each: their partials are
+// ~1 % of an exact-fp32 kernel's time.)
+inline int pick_csplit(int64_t W, int nrt, int slots, int maxs = 4, double per = 0.02) {
   int best = 1;
   double bc = 1e300;
-  for (int s = 1; s <= 4 && (s == 1 || nrt / s >= 16); ++s) {
-    const double c = (double)((W * s + slots - 1) / slots) / s * (1.0 + 0.02 * (s - 1));
+  for (int s = 1; s <= maxs && (s == 1 || nrt / s >= 16); ++s) {
+    const double c = (double)((W * s + slots - 1) / slots) / s * (1.0 + per * (s - 1));
     if (c < bc * 0.98) {
       bc = c;
       best = s;

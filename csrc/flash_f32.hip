@@ -924,3 +924,19 @@ extern "C" int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D,
   hipLaunchKernelGGL(xdot::fa32::rows_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, *a, D);
   return 0;
 }
+
+// column splits of the exact-fp32 forward (kernel 0) / row-side backward (1), see kernels.h
+extern "C" int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int64_t W, int64_t T) {
+  using namespace xdot::fa32;
+  int occ = 0;
+#define OC(DV)                                                                                                   \
+  if (D == DV)                                                                                                   \
+    occ = kernel == 0 ? (sbuf ? xdot::fa::wg_per_cu(fwd_kernel<DV, true>, lds_bytes_sb<DV>())                  \
+                              : xdot::fa::wg_per_cu(fwd_kernel<DV, false>, lds_bytes<DV>()))                   \
+                      : (sbuf ? xdot::fa::wg_per_cu(bwd_rows_ds_kernel<DV>, 2 * Cfg<DV>::IMG * 4)              \
+                              : xdot::fa::wg_per_cu(bwd_rows_kernel<DV>, lds_bytes<DV>()));
+  OC(32) OC(64) OC(96) OC(128)
+#undef OC
+  if (!occ) return 0;
+  return xdot::fa::pick_csplit(W, (int)((T + 31) / 32), occ * xdot_num_cus(), 8, 0.004);
+}

@@ -882,3 +882,19 @@ extern "C" int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int*
   }
   return 0;
 }
+
+// column splits of the split-bf16 forward (kernel 0) / row-side backward (1), see kernels.h
+extern "C" int xdot_flash_f32_row_splits_x3(int kernel, int D, bool sbuf, int64_t W, int64_t T) {
+  using namespace xdot::fa3;
+  int occ = 0;
+#define OC(DV)                                                                                                   \
+  if (D == DV)                                                                                                   \
+    occ = kernel == 0 ? (sbuf ? xdot::fa::wg_per_cu(fwd_kernel<DV, true>, FwdL<DV>::LDS_SB)                    \
+                              : xdot::fa::wg_per_cu(fwd_kernel<DV, false>, FwdL<DV>::LDS))                     \
+                      : (sbuf ? xdot::fa::wg_per_cu(bwd_rows_ds_kernel<DV>, RowsDsL<DV>::LDS)                  \
+                              : xdot::fa::wg_per_cu(bwd_rows_kernel<DV>, RowsL<DV>::LDS));
+  OC(32) OC(64) OC(96) OC(128)
+#undef OC
+  if (!occ) return 0;
+  return xdot::fa::pick_csplit(W, (int)((T + 31) / 32), occ * xdot_num_cus(), 8, 0.004);
+}

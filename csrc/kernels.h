@@ -245,6 +245,12 @@ int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int* sq, int* s
 int xdot_flash_cols_sum_launch(const float* part, void* out, int S, int64_t rows, int C, int64_t ldo, int dt,
                                hipStream_t st);
 int xdot_flash_cols_splits_cols2(const xdot::fa::BwdArgs* a, int dt, int D, int* sq);
+// column splits of the fp32 row-block kernels (kernel 0: forward, 1: row-side backward) for W
+// unsplit workgroups over T columns: occupancy of the instantiation x CUs, round model
+// (XDOT_F32_SPLIT: unset / auto = model, "old" = the 16-bit model, n = forced); 0: not handled
+int xdot_flash_f32_row_splits(int kernel, int fp32_mode, int D, bool sbuf, int64_t W, int64_t T);
+int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int64_t W, int64_t T);
+int xdot_flash_f32_row_splits_x3(int kernel, int D, bool sbuf, int64_t W, int64_t T);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 // wide head dims (csrc/flash_wide.hip): D = 160 / 192 / 256 / 384, 16-bit and exact fp32 (a wide
 // fp32 launch always runs exact); -1 = not a wide (dtype, D), -2 = needs the score buffer (fp32 D > 256)

@@ -85,6 +85,9 @@ variable                    default   effect
                                       tail (fp32 partials, ordered sum; auto: occupancy round
                                       model; n: n splits <= 4, also for the 16-bit pipelined kernel,
                                       whose auto is 1)
+``XDOT_F32_SPLIT`` (C++)     auto      column splits of the fp32 forward / row-side kernels: auto =
+                                      occupancy round model of the fp32 instantiation (up to 8);
+                                      fwd = forward only; old = the 16-bit model; n = forced
 ``XDOT_HIPCC_FLAGS`` (build)          extra hipcc flags for ``python -m xdot.build``
 ==========================  ========  ===========================================================
 
