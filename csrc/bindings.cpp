@@ -693,7 +693,8 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags, /*colmajor=*/true);
   float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols");
   float* dsb = sbuf_ptr(dsbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols (dS buffer)");
-  TORCH_CHECK(!dsb || sb, "xdot.flash_bwd_cols: a dS buffer needs the score buffer");
+  // a dS buffer alone: dS-only mode (the recomputing column kernel stores dS, D <= 128)
+  TORCH_CHECK(!dsb || sb || g.D <= 128, "xdot.flash_bwd_cols: a dS buffer without the score buffer needs D <= 128");
   TORCH_CHECK(passes >= 1 && passes <= 3 && (passes == 3 || (sb && dsb)),
               "xdot.flash_bwd_cols: single passes (1 = dV, 2 = dQ) need the score and dS buffers");
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
@@ -1083,14 +1084,14 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   const FlashGeom g = flash_check(rows, kc, vc, H, bits, flags);
   float* sb = sbuf_ptr(sbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_rows");
   float* dsb = sbuf_ptr(dsbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_rows (dS buffer)");
-  TORCH_CHECK(!dsb || sb, "xdot.flash_bwd_rows: a dS buffer needs the score buffer");
+  TORCH_CHECK(!dsb || sb || g.D <= 128, "xdot.flash_bwd_rows: a dS buffer without the score buffer needs D <= 128");
   TORCH_CHECK(delta.is_contiguous() && delta.scalar_type() == at::kFloat && delta.numel() == g.B * H * g.R,
               "xdot.flash_bwd_rows: delta");
   auto a = bwd_args(g, dout, rows, kc, vc, lse, bits, flags, H, scale);
   auto drows = at::empty_like(rows);
   int ns = nsplit > 0 ? pick_split(1, g.T, 1, nsplit) : rows_split(g.B, g.R, g.T, H);
   if (nsplit == 0 && rows.scalar_type() == at::kFloat) {
-    const int f = xdot_flash_f32_row_splits(1, (int)fp32_mode, (int)g.D, sb != nullptr,
+    const int f = xdot_flash_f32_row_splits(1, (int)fp32_mode, (int)g.D, sb != nullptr || dsb != nullptr,
                                             ((g.R + 127) / 128) * g.B * H, g.T);
     if (f > 0) ns = f;
   }

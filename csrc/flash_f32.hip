@@ -430,7 +430,10 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
 // K·Qᵀ product, each block is overwritten with dS / scale for the row kernel, and dV is left to
 // bwd_cols_dv_kernel (run first): without the dV accumulators this dQ pass fits two waves per
 // SIMD at D <= 96 (one wave per SIMD exposed every LDS / barrier stall: MFMA 54 % busy with both).
-template <int D, bool LS>
+// DS (dS-only buffer mode, recompute kernel): S recomputed as without a buffer, dS stored into
+// a.dsbuf for the row kernel (the split family's memory-bound mode: 40 GB of score traffic per
+// step instead of 100)
+template <int D, bool LS, bool DS = LS>
 __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
@@ -458,11 +461,11 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     load_frag<D>(vf, reinterpret_cast<const float*>(a.vc) + off, col_ok);
   }
   // score buffer column of this wave: block (bh, rt, c0/32) at sbc + rt * NKT32 * 1024
-  const bool sown = LS && c0 < a.T;
+  const bool sown = DS && c0 < a.T;
   // loads of waves past T read a valid block, their dS stores go to the dump block: every wave
   // loads and stores every tile (uniform counts keep the compiler's vmcnt waits exact)
   float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024 : nullptr;
-  float* dsc = LS ? (sown ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024
+  float* dsc = DS ? (sown ? (a.dsbuf ? a.dsbuf : a.sbuf) + ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024
                           : (a.dsbuf ? a.dsbuf : a.sbuf) + fa::sb_dump(a.B, a.H, a.R, a.T))
                   : nullptr;
   const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     }
 #ifndef XDOT_AB_NO_DS_STORE
     // dS (over S or apart), every tile (skipped tiles store zeros nobody reads)
-    if constexpr (LS) blk_store_lds(dsc + rt * dstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);
+    if constexpr (DS) blk_store_lds(dsc + rt * dstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);
 #endif
     if (flag != 1) {
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
@@ -825,7 +828,7 @@ extern "C" int xdot_flash_bwd_rows_f32_launch(const xdot::fa::BwdArgs* a, int D,
   if (a->prescaled) return -1;
   const int nrb = (a->R + 127) / 128;
   const dim3 grid(nrb * a->B * a->H * a->nsplit);
-  if (a->sbuf) {  // score-buffer mode: dS from the column kernel, Q image only
+  if (a->sbuf || a->dsbuf) {  // score-buffer modes: dS from the column kernel, Q image only
 #define L(DV) hipLaunchKernelGGL(bwd_rows_ds_kernel<DV>, grid, dim3(256), 2 * Cfg<DV>::IMG * 4, st, *a)
     XF32_DISPATCH(L)
 #undef L
@@ -873,6 +876,14 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
 #undef LDQ
 #undef LDV
   }
+  if (a->dsbuf) {  // dS-only buffer: recompute S, store dS for the row kernel
+#define L(DV)                                                                                                     \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, false, true>), dim3(W * sq), dim3(256), lds_bytes_sb<DV>(), st, *a); \
+  sum_q();                                                                                                        \
+  sum_v(sq)
+    XF32_DISPATCH(L)
+#undef L
+  }
 #define L(DV)                                                                                                \
   hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), dim3(W * sq), dim3(256), lds_bytes<DV>(), st, *a); \
   sum_q();                                                                                                   \
@@ -894,6 +905,8 @@ template <int D> void f32_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
   if (a->sbuf) {
     *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_sb<D>()));
     *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, 2 * (Cfg<D>::IMG + 32) * 4));
+  } else if (a->dsbuf) {
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false, true>, lds_bytes_sb<D>()));
   } else {
     *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false>, lds_bytes<D>()));
   }

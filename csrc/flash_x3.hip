@@ -434,18 +434,21 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void bwd_rows_kernel(BwdArgs 
 // LS (score-buffer mode): S comes from a.sbuf (prefetched one tile ahead) instead of the K·Qᵀ
 // product, each block is overwritten with dS / scale for bwd_rows_ds_kernel, and dV is left to
 // bwd_cols_dv_kernel (run first).  K then needs only its transposed image, dO its row-major one.
-template <int D, bool LS> struct ColsL {
+// DS (dS-only buffer mode, recompute kernel): S recomputed as without a buffer, dS stored into
+// a.dsbuf for bwd_rows_ds_kernel (40 GB of score traffic per step instead of the 100 GB of the
+// S + dS mode, which bounds this family's kernels)
+template <int D, bool LS, bool DS = LS> struct ColsL {
   using K = Img<D, !LS, true>;
   using DO = Img<D, true, !LS>;
   static constexpr int AUX = 256;  // lse2[32], δ[32] (fp32)
   static constexpr int STAGE = K::BYTES + DO::BYTES + AUX;
-  static constexpr int LDS = 2 * STAGE + (LS ? 4 * 4096 : 0);
+  static constexpr int LDS = 2 * STAGE + (DS ? 4 * 4096 : 0);
 };
 
-template <int D, bool LS>
+template <int D, bool LS, bool DS = LS>
 __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
-  using KL = ColsL<D, LS>;
+  using KL = ColsL<D, LS, DS>;
   constexpr int DB = CF::DB;
   using fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
@@ -472,10 +475,10 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     load_frag<D>(vh, vl, reinterpret_cast<const float*>(a.vc) + off, col_ok);
   }
   const int NKT32 = (a.T + 31) / 32;
-  const bool sown = LS && c0 < a.T;
+  const bool sown = DS && c0 < a.T;
   // every wave loads and stores every tile (waves past T: a valid block / the dump block)
   float* sbc = LS ? a.sbuf + ((int64_t)bh * NRB32 * NKT32 + min(c0 >> 5, NKT32 - 1)) * 1024 : nullptr;
-  float* dsc = LS ? (a.dsbuf ? a.dsbuf : a.sbuf) +
+  float* dsc = DS ? (a.dsbuf ? a.dsbuf : a.sbuf) +
                         (sown ? ((int64_t)bh * NRB32 * NKT32 + (c0 >> 5)) * 1024 : fa::sb_dump(a.B, a.H, a.R, a.T))
                   : nullptr;
   const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       }
     }
     // dS, every tile: uniform store counts keep the compiler's vmcnt waits exact
-    if constexpr (LS) blk_store_lds(dsc + rt * dstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
+    if constexpr (DS) blk_store_lds(dsc + rt * dstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
     if (flag != 1) {
       if constexpr (LS) {
         trprod<D, false, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
@@ -793,7 +796,7 @@ extern "C" int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
   if (a->prescaled) return -1;
   const dim3 grid(((a->R + 127) / 128) * a->B * a->H * a->nsplit);
-  if (a->sbuf) {  // score-buffer mode: dS from the column kernel, Q image only
+  if (a->sbuf || a->dsbuf) {  // score-buffer modes: dS from the column kernel, Q image only
 #define L(DV) hipLaunchKernelGGL(bwd_rows_ds_kernel<DV>, grid, dim3(256), RowsDsL<DV>::LDS, st, *a)
     X3_DISPATCH(L)
 #undef L
@@ -802,6 +805,21 @@ extern "C" int xdot_flash_bwd_rows_x3_launch(const xdot::fa::BwdArgs* a, int D, 
   X3_DISPATCH(L)
 #undef L
 }
+
+namespace {
+// dS-only column launch: the recompute kernel's two-image stages plus the transpose tiles exceed
+// the 160 KiB of LDS at D = 128 (refused: -1)
+template <int D> int launch_cols_ds(const xdot::fa::BwdArgs& a, dim3 grid, hipStream_t st) {
+  using namespace xdot::fa3;
+  if constexpr (ColsL<D, false, true>::LDS > 160 * 1024) {
+    (void)a; (void)grid; (void)st;
+    return -1;
+  } else {
+    hipLaunchKernelGGL((bwd_cols_kernel<D, false, true>), grid, dim3(256), (ColsL<D, false, true>::LDS), st, a);
+    return 0;
+  }
+}
+}  // namespace
 
 extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st) {
   using namespace xdot::fa3;
@@ -840,6 +858,20 @@ extern "C" int xdot_flash_bwd_cols_x3_launch(const xdot::fa::BwdArgs* a, int D, 
 #undef LDQ
 #undef LDV
   }
+  if (a->dsbuf) {  // dS-only buffer: recompute S, store dS for the row kernel (D <= 96: LDS)
+    int rc = -1;
+    switch (D) {
+      case 32: rc = launch_cols_ds<32>(*a, dim3(W * sq), st); break;
+      case 64: rc = launch_cols_ds<64>(*a, dim3(W * sq), st); break;
+      case 96: rc = launch_cols_ds<96>(*a, dim3(W * sq), st); break;
+      case 128: rc = launch_cols_ds<128>(*a, dim3(W * sq), st); break;
+      default: break;
+    }
+    if (rc) return rc;
+    sum_q();
+    sum_v(sq);
+    return 0;
+  }
 #define L(DV)                                                                                                          \
   hipLaunchKernelGGL((bwd_cols_kernel<DV, false>), dim3(W * sq), dim3(256), (ColsL<DV, false>::LDS), st, *a); \
   sum_q();                                                                                                             \
@@ -860,6 +892,9 @@ template <int D> void x3_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
   if (a->sbuf) {
     *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, ColsL<D, true>::LDS));
     *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, DvL<D>::LDS));
+  } else if (a->dsbuf) {
+    *sq = *sv =
+        xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false, true>, ColsL<D, false, true>::LDS));
   } else {
     *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false>, ColsL<D, false>::LDS));
   }

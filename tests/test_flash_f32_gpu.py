@@ -413,3 +413,80 @@ def test_flash_f32_column_row_splits(gpu, monkeypatch, fm, mode):
         for what, g_, r_ in (("q", got[..., :C], refq), ("v", got[..., C:], refv)):
             err = _rel(flash.btc_to_rank_major(g_.contiguous(), N), r_)
             assert err <= (2e-6 if fm == 0 else 2e-5), f"splits {s} d cols ({what}): {err:.2e}"
+
+
+# ---- dS-only buffer mode (XDOT_FP32_DS_ONLY): the forward stores nothing, the single-pass column
+# kernel recomputes S and stores dS, the row kernel reads it --------------------------------------
+@pytest.mark.parametrize("fm", [0, 1])
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mask_kind", ["none", "blocks"])
+def test_flash_f32_ds_only_buffer(gpu, fm, case, mask_kind):
+    """Column grads are bitwise those of the recompute path (same kernel, plus a store); the row
+    grad from the stored dS is bitwise that of the S + dS buffer mode in the exact family (same
+    dS chain), and within each family's fp64 bound either way."""
+    from xdot.ops import flash
+
+    B, R, N, Rc, H, D = case
+    T = N * Rc
+    rows, kc, vc, do, mask = _inputs(case, mask_kind, gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    out, lse = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=fm)
+    if fm == 1 and D > 96:  # the split family's recompute stages + transpose tiles exceed LDS
+        with pytest.raises(RuntimeError, match="config"):
+            flash.bwd_cols(do, rows, kb, vb, out, lse, mk, H, scale, fp32_mode=fm,
+                           dsbuf=torch.empty(flash.score_buffer_numel(B, H, R, T), device=gpu))
+        assert not flash.ds_only_wanted(1, D)
+        return
+    dkv1, dl1 = flash.bwd_cols(do, rows, kb, vb, out, lse, mk, H, scale, fp32_mode=fm)
+    ds = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)
+    dkv2, dl2 = flash.bwd_cols(do, rows, kb, vb, out, lse, mk, H, scale, fp32_mode=fm, dsbuf=ds)
+    assert torch.equal(dkv1, dkv2) and torch.equal(dl1, dl2)
+    drows = flash.bwd_rows(do, rows, kb, vb, lse, dl2, mk, H, scale, fp32_mode=fm, dsbuf=ds)
+    k, q, v, ref_o, _ = _ref64(rows, kc, vc, mask, H, scale)
+    ref_o.backward(do.double())
+    ref = k.grad.transpose(1, 2).reshape(B, R, H * D)
+    assert torch.isfinite(drows).all()
+    assert _rel(drows, ref) <= (2e-6 if fm == 0 else SPLIT_TOL), f"d rows {_rel(drows, ref):.2e}"
+    if fm == 0:
+        sb = torch.full_like(ds, float("nan"))
+        o3, l3 = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=0, sbuf=sb)
+        _, dl3 = flash.bwd_cols(do, rows, kb, vb, o3, l3, mk, H, scale, fp32_mode=0, sbuf=sb)
+        d3 = flash.bwd_rows(do, rows, kb, vb, l3, dl3, mk, H, scale, fp32_mode=0, sbuf=sb)
+        assert torch.equal(d3, drows)
+
+
+@pytest.mark.parametrize("mode", ["all", "none"])
+def test_module_fp32_ds_only_mode(gpu, monkeypatch, mode):
+    """The module's fp32 paths under XDOT_FP32_DS_ONLY=all / none against fp64 torch."""
+    import xdot
+    from xdot.utils.comm import LocalComm, use_comm
+    from xdot.utils.env import FLAGS
+
+    torch.manual_seed(0)
+    Dm, H, T = 384, 4, 700
+    old = (FLAGS.fp32_ds_only, FLAGS.fp32_mode)
+    try:
+        with use_comm(LocalComm()):
+            m = xdot.DistributedDotProductAttn(Dm, num_heads=H, add_bias=True).to(gpu)
+            ref = xdot.DistributedDotProductAttn(Dm, num_heads=H, add_bias=True, distributed=False,
+                                                 impl="materialized", backend="torch").to(gpu, torch.float64)
+            ref.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+            xd = torch.randn(1, T, Dm, device=gpu, dtype=torch.float64)
+            mask = torch.rand(1, T, T, device=gpu) < 0.2
+            mask[..., 0] = False
+            xr = xd.clone().requires_grad_(True)
+            ro = ref(xr, xr, xr, mask)
+            ro.square().sum().backward()
+            FLAGS.fp32_ds_only = mode
+            for fmode, tol in (("exact", 1e-5), ("split", 3e-5)):  # as the module tests above
+                FLAGS.fp32_mode = fmode
+                x = xd.float().requires_grad_(True)
+                out = m(x, x, x, mask)
+                out.square().sum().backward()
+                assert _rel(out, ro) <= tol, (fmode, _rel(out, ro))
+                assert _rel(x.grad, xr.grad) <= 1e-4, (fmode, _rel(x.grad, xr.grad))
+                m.zero_grad()
+    finally:
+        FLAGS.fp32_ds_only, FLAGS.fp32_mode = old

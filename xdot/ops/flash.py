@@ -251,6 +251,24 @@ def score_buffers(B: int, H: int, R: int, T: int, device):
     return None
 
 
+def ds_only_wanted(fp32_mode: int, D: int) -> bool:
+    """Whether fp32 family ``fp32_mode`` (0 exact, 1 split) at head dim ``D`` keeps only a dS
+    buffer (``XDOT_FP32_DS_ONLY``): the forward stores nothing, the single-pass column kernel
+    recomputes S and stores dS, the row kernel reads dS.  The split family's kernels are bound by
+    the score traffic (S written, read twice, dS written and read: 100 GB per step at T = R =
+    25000, H = 8); this mode moves 40 GB for one recomputed product on the column side."""
+    if D > (96 if fp32_mode == 1 else 128):  # split family at D = 128: the stages + transpose tiles exceed LDS
+        return False
+    m = FLAGS.fp32_ds_only
+    return m == "all" or (m == "split" and fp32_mode == 1)
+
+
+def ds_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tensor]:
+    """The dS buffer of the dS-only mode (:func:`ds_only_wanted`), same size rule as
+    :func:`score_buffer`, or None."""
+    return score_buffer(B, H, R, T, device)
+
+
 def fwd(rows: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, mk: Optional[PackedMask], H: int,
         scale: float, nsplit: int = 0, prescaled: bool = False,
         fp32_mode: Optional[int] = None, sbuf: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -503,10 +503,15 @@ class SeqParallelAttention(torch.autograd.Function):
             # fp32 (exact or split): score buffer (flash.score_buffer) when it fits: the backward
             # then reads S / dS instead of recomputing them.  One kernel over the whole gathered
             # side (in fp32 the own-block-first segmentation hides < 5 % of a rank's forward)
-            sbs = flash.score_buffers(B, H, R, n * qv.shape[1], k.device)
-            if sbs is not None:
-                sbuf, dsbuf = sbs
-                segmented = False
+            if flash.ds_only_wanted(fm, D):  # dS-only: nothing stored by the forward
+                dsbuf = flash.ds_buffer(B, H, R, n * qv.shape[1], k.device)
+                if dsbuf is not None:
+                    segmented = False
+            else:
+                sbs = flash.score_buffers(B, H, R, n * qv.shape[1], k.device)
+                if sbs is not None:
+                    sbuf, dsbuf = sbs
+                    segmented = False
         if use_hip and k.dtype == torch.float32 and D > WIDE_F32_NEEDS_SCORES and sbuf is None:
             # no kernel recomputes an fp32 head this wide (three D-wide register sets): the torch path
             import warnings
@@ -603,7 +608,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     g = bufs[0]
                     cargs = dict(fp32_out=FLAGS.grad_fp32, prescaled=ctx.prescaled, lse2=lse2,
                                  fp32_mode=ctx.fp32_mode, sbuf=sbuf)
-                    if dsbuf is not None:
+                    if dsbuf is not None and sbuf is not None:
                         # dQ pass (S -> dS), then the row kernel (reads dS) on `cur` concurrently
                         # with the dV pass (reads S) here
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
@@ -614,8 +619,8 @@ class SeqParallelAttention(torch.autograd.Function):
                                        dsbuf=dsbuf, passes=1, out_dkv=dkv, **cargs)
                     else:
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                                **cargs)
-                        if sbuf is not None:  # the row kernel reads the dS this kernel wrote
+                                                dsbuf=dsbuf, **cargs)
+                        if sbuf is not None or dsbuf is not None:  # the row kernel reads the dS this kernel wrote
                             ev_cols = torch.cuda.Event()
                             ev_cols.record(hi)
                     off = 0

@@ -50,6 +50,11 @@ variable                    default   effect
 ``XDOT_FP32_SCORES_FRAC``   0.5       ... only when that fits this fraction of the free device memory
 ``XDOT_FP32_SCORES_DS``     1         ... and a second buffer for dS when both fit: the column side's
                                       dV pass then runs concurrently with the row kernel
+``XDOT_FP32_DS_ONLY``       split     fp32 families that keep only the dS buffer (the forward stores
+                                      nothing, the single-pass column kernel recomputes S and stores
+                                      dS, the row kernel reads it: 40 GB of score traffic per step
+                                      instead of 100): ``split`` (the memory-bound split-bf16
+                                      family), ``all``, ``none``
 ``XDOT_FUSED_MODULE``       1         the module's flash path as ONE autograd node (projections +
                                       attention + output projection, xdot/models/fused.py; 0: one
                                       node per op)
@@ -146,6 +151,7 @@ class _Flags:
         self.fp32_scores = _flag("XDOT_FP32_SCORES", default="1")
         self.fp32_scores_frac = _num("XDOT_FP32_SCORES_FRAC", 0.5)
         self.fp32_scores_dsbuf = _flag("XDOT_FP32_SCORES_DS", default="1")
+        self.fp32_ds_only = _str("XDOT_FP32_DS_ONLY", "split")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
         self.proj_kernel = _num("XDOT_PROJ", 1, int)
