@@ -167,31 +167,21 @@ __device__ __forceinline__ void blk_store(float* blk, const f32x16& x, int lane)
 }
 // The same through a wave-private 4-KiB LDS tile: the scatter goes to LDS (16 ds_write_b32, the
 // 2-way bank conflicts of which cost nothing), then the block leaves as 4 coalesced 16-byte global
-// stores per lane (64 lanes x 64 B contiguous) instead of 16 dword stores in 64-byte pieces.
-// XDOT_SB_DIRECT: the direct scatter (A/B).
-__device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x16& x, int lane) {
-#ifdef XDOT_SB_DIRECT
-  blk_store(blk, x, lane);
-#else
-#ifdef XDOT_SB_NOSWZ
-  const int a = lane & 31, hf = lane >> 5;
-  float* p = wl + 512 * ((a >> 2) & 1) + (a & 3) + 4 * (a >> 3);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) p[16 * tidx(r, hf)] = x[r];
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
-  const f32x4* q = reinterpret_cast<const f32x4*>(wl + 16 * lane);
-  f32x4* d = reinterpret_cast<f32x4*>(blk + 16 * lane);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) d[i] = q[i];
-#else
-  // The tile position q of logical float q is q ^ 16 ((q >> 6) & 1) ^ 32 ((q >> 9) & 1): the 16
-  // scatter writes then cover all 64 banks (unswizzled: 16 banks, 4-way conflicts), and each
-  // reader lane's 16 floats stay one contiguous 64-byte slot (slot l ^ ((l >> 2) & 1) ^
-  // 2 ((l >> 5) & 1)), read chunk-rotated so every 16-lane b128 phase hits 16 bank quads.
+// stores per lane (64 lanes x 64 B contiguous) instead of 16 dword stores in 64-byte pieces
+// (the direct scatter measured 2.5 % slower, the unswizzled tile the same: profiles/r5_fp32.md).
+// Two halves, so the caller can put the tile's LDS writes before its next MFMA block and flush
+// after it (the writes' latency then hides under the MFMAs instead of a wait in front of them).
+// The tile position q of logical float q is q ^ 16 ((q >> 6) & 1) ^ 32 ((q >> 9) & 1): the 16
+// scatter writes then cover all 64 banks (unswizzled: 16 banks, 4-way conflicts), and each
+// reader lane's 16 floats stay one contiguous 64-byte slot (slot l ^ ((l >> 2) & 1) ^
+// 2 ((l >> 5) & 1)), read chunk-rotated so every 16-lane b128 phase hits 16 bank quads.
+__device__ __forceinline__ void blk_put_lds(float* wl, const f32x16& x, int lane) {
   const int a = lane & 31, hf = lane >> 5, sa = (a >> 2) & 1, k = hf + 2 * sa;
   float* p = wl + 512 * sa + (a & 3) + 4 * (a >> 3) + 64 * hf;
 #pragma unroll
   for (int r = 0; r < 16; ++r) p[128 * (r >> 2) + 16 * ((r & 3) ^ k)] = x[r];
+}
+__device__ __forceinline__ void blk_flush_lds(float* blk, const float* wl, int lane) {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
   const int slot = lane ^ ((lane >> 2) & 1) ^ (2 * ((lane >> 5) & 1));
 #pragma unroll
@@ -199,8 +189,10 @@ __device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x1
     const int c = (i + (lane >> 2)) & 3;
     *reinterpret_cast<f32x4*>(blk + 16 * lane + 4 * c) = *reinterpret_cast<const f32x4*>(wl + 16 * slot + 4 * c);
   }
-#endif
-#endif
+}
+__device__ __forceinline__ void blk_store_lds(float* blk, float* wl, const f32x16& x, int lane) {
+  blk_put_lds(wl, x, lane);
+  blk_flush_lds(blk, wl, lane);
 }
 // float offset of the dump block after the last score block: writes of waves that own no block
 // (rows past R, columns past T) go there, so every wave issues the same stores every tile

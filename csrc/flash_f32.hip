@@ -228,8 +228,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     f32x16 s{};
     if (flag != 1) s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
-    // raw S, every tile (skipped tiles store zeros nobody reads)
-    if constexpr (SS) blk_store_lds(sbw + (int64_t)kt * sbw_step, sm + 2 * CF::STAGE + wave * 1024, s, lane);
+    // raw S, every tile (skipped tiles store zeros nobody reads): LDS writes here, the transposed
+    // global stores after the PV product
+    float* swl = sm + 2 * CF::STAGE + wave * 1024;
+    if constexpr (SS) fa::blk_put_lds(swl, s, lane);
     if (flag != 1) {
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
@@ -263,6 +265,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
       l_run += ls;
       trprod<D>(vi, s, o, lane);  // Oᵀ += Vᵀ · Pᵀ
     }
+    if constexpr (SS) fa::blk_flush_lds(sbw + (int64_t)kt * sbw_step, swl, lane);
     if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
     __syncthreads();
   }
@@ -512,10 +515,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     if (more) {
       st.load(kb, db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
       ax = aux_load(rt + 1);
-#ifndef XDOT_AB_NO_S_LOAD
-      if constexpr (LS)
-        snext = blk_load(sbc + (rt + 1) * sstep, lane);
-#endif
+      if constexpr (LS) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
     const float* ki = sm + ((rt - rt_beg) & 1) * CF::STAGE;
     const float* di = ki + CF::IMG;
@@ -524,11 +524,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     flag = __builtin_amdgcn_readfirstlane(flag);
     f32x16 s{}, dp{};
     if (flag != 1) {
-#ifdef XDOT_AB_NO_S_LOAD
-      if constexpr (LS) s = f32x16{};
-#else
       if constexpr (LS) s = scur;                        // S  (row x col), stored by the forward
-#endif
       else s = rowprod<D>(ki, qf, f32x16{}, lane);      // S  (row x col)
       dp = rowprod<D>(di, vf, f32x16{}, lane);          // dP (row x col)
 #pragma unroll
@@ -545,10 +541,10 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
           if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
     }
-#ifndef XDOT_AB_NO_DS_STORE
-    // dS (over S or apart), every tile (skipped tiles store zeros nobody reads)
-    if constexpr (DS) blk_store_lds(dsc + rt * dstep, sm + 2 * CF::STAGE + wave * 1024, dp, lane);
-#endif
+    // dS (over S or apart), every tile (skipped tiles store zeros nobody reads): LDS writes
+    // before the dQ product, the transposed global stores after it
+    float* dwl = sm + 2 * CF::STAGE + wave * 1024;
+    if constexpr (DS) fa::blk_put_lds(dwl, dp, lane);
     if (flag != 1) {
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
@@ -557,6 +553,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         fa::pin_agpr(dv);
       }
     }
+    if constexpr (DS) fa::blk_flush_lds(dsc + rt * dstep, dwl, lane);
     if (more) {
       float* nx = sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE;
       st.store(nx, tid);

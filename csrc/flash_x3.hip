@@ -262,8 +262,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     f32x16 s{};
     if (flag != 1) s = rowprod<D, true, false>(qi, kh, kl, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
-    // raw S, every tile (skipped tiles store zeros nobody reads)
-    if constexpr (SS) blk_store_lds(sbw + kt * sbw_step, reinterpret_cast<float*>(smem + FL::LDS) + wave * 1024, s, lane);
+    // raw S, every tile (skipped tiles store zeros nobody reads): LDS writes here, the transposed
+    // global stores after the PV product
+    float* swl = reinterpret_cast<float*>(smem + FL::LDS) + wave * 1024;
+    if constexpr (SS) fa::blk_put_lds(swl, s, lane);
     if (flag != 1) {
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
       l_run += ls;
       trprod<D, false, true>(vi, s, o, lane);  // Oᵀ += Vᵀ · Pᵀ
     }
+    if constexpr (SS) fa::blk_flush_lds(sbw + kt * sbw_step, swl, lane);
     if (more) {
       char* nx = smem + ((kt + 1 - kt_beg) & 1) * FL::STAGE;
       tq.template store<true, false>(nx, tid);
@@ -556,8 +559,10 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
           if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
       }
     }
-    // dS, every tile: uniform store counts keep the compiler's vmcnt waits exact
-    if constexpr (DS) blk_store_lds(dsc + rt * dstep, reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024, dp, lane);
+    // dS, every tile: uniform store counts keep the compiler's vmcnt waits exact (LDS writes
+    // before the products, the transposed global stores after them)
+    float* dwl = reinterpret_cast<float*>(smem + 2 * KL::STAGE) + wave * 1024;
+    if constexpr (DS) fa::blk_put_lds(dwl, dp, lane);
     if (flag != 1) {
       if constexpr (LS) {
         trprod<D, false, true>(ki, dp, dq, lane);  // dQᵀ += Kᵀ · dS
@@ -568,6 +573,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         fa::pin_agpr(dv);
       }
     }
+    if constexpr (DS) fa::blk_flush_lds(dsc + rt * dstep, dwl, lane);
     if (more) put(smem + ((rt + 1 - rt_beg) & 1) * KL::STAGE, tk, td, ax);
     __syncthreads();
   }
