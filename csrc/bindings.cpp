@@ -624,6 +624,10 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
     const int f = xdot_flash_f32_row_splits(0, (int)fp32_mode, (int)g.D, sb != nullptr, NB, g.T);
     if (f > 0) ns = f;
   }
+  if (nsplit == 0 && g.D > 128) {  // wide kernels (one workgroup per CU): their own occupancy
+    const int f = xdot_flash_wide_splits(0, dt_code(rows.scalar_type()), (int)g.D, sb != nullptr, NB, (g.T + 31) / 32);
+    if (f > 0) ns = f;
+  }
   at::Tensor opart, lpart;
   if (heavy) {  // compact partials of the split tail blocks only
     opart = at::empty({(int64_t)hs * 8 * hr * 128 * g.D}, rows.options().dtype(at::kFloat));
@@ -747,11 +751,10 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   // column kernels: row splits against the last-round tail (fp32 partials summed in the launcher;
   // the exact / split fp32 kernels and the pipelined 16-bit kernel, else 1)
   at::Tensor cpq, cpv;
-  if (dt != xdot::DT_F32 || (!a.prescaled && !a.dkv16)) {
-    int sq = 1, sv = 1;
+  if (dt != xdot::DT_F32 || g.D > 128 || (!a.prescaled && !a.dkv16)) {
+    int sq = 1, sv = 1;  // (the single-pass recompute kernels use sq for both halves: sv == sq there)
     TORCH_CHECK(xdot_flash_cols_splits(&a, dt, (int)g.D, &sq, &sv) == 0, "xdot.flash_bwd_cols: split config");
     const bool run_q = !sb || (passes & 2), run_v = !sb || (passes & 1);
-    if (!sb) sv = sq;
     if (run_q && sq > 1) {
       cpq = at::empty({sq, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
       a.cpq = cpq.data_ptr<float>();
@@ -1093,6 +1096,11 @@ at::Tensor flash_bwd_rows(const at::Tensor& dout, const at::Tensor& rows, const 
   if (nsplit == 0 && rows.scalar_type() == at::kFloat) {
     const int f = xdot_flash_f32_row_splits(1, (int)fp32_mode, (int)g.D, sb != nullptr || dsb != nullptr,
                                             ((g.R + 127) / 128) * g.B * H, g.T);
+    if (f > 0) ns = f;
+  }
+  if (nsplit == 0 && g.D > 128) {
+    const int f = xdot_flash_wide_splits(1, dt_code(rows.scalar_type()), (int)g.D, sb != nullptr,
+                                         ((g.R + 127) / 128) * g.B * H, (g.T + 31) / 32);
     if (f > 0) ns = f;
   }
   at::Tensor dpart;

@@ -671,7 +671,13 @@ extern "C" int xdot_flash_bwd_cols_launch(const xdot::fa::BwdArgs* a, int dt, in
 
 extern "C" int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D, int* sq, int* sv) {
   *sq = *sv = 1;
-  if (D > 128 || a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (a->R == 0 || a->B == 0 || a->H == 0 || a->T == 0) return 0;
+  if (D > 128) {  // the wide family's two passes, each from its own occupancy
+    const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H, nrt = (a->R + 31) / 32;
+    *sq = std::max(1, xdot_flash_wide_splits(2, dt, D, a->sbuf != nullptr, W, nrt));
+    *sv = std::max(1, xdot_flash_wide_splits(3, dt, D, a->sbuf != nullptr, W, nrt));
+    return 0;
+  }
   if (dt != xdot::DT_F32) {  // the pipelined 16-bit column kernel (pre-scaled, D <= 96) only
     if (D > 96 || !a->prescaled) return 0;
     const int r = xdot_flash_cols_splits_cols2(a, dt, D, sq);

@@ -23,6 +23,11 @@
 //   * the backward splits the gathered side into a dV pass and a dQ pass (the three D-wide
 //     register sets a single pass needs do not fit); exact fp32 D = 384 takes S from the score
 //     buffer (flash_f32.hip "score-buffer mode") in both passes and dS in the row kernel.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+
 #include "flash_common.h"
 
 namespace xdot {
@@ -512,7 +517,10 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const auto L = Pl::lanes(lane);
   const int ncb = (a.T + 127) / 128;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bh = lin / ncb;
+  const int cb = lin % ncb, bhs = lin / ncb;
+  // row split sp of ns (BwdArgs::csq for the dQ pass, csv for the dV pass): row tiles [rt_beg, rt_end)
+  const int ns = DQ ? (a.csq > 1 ? a.csq : 1) : (a.csv > 1 ? a.csv : 1);
+  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -520,6 +528,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
   const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
   const int NRT = (a.R + 31) / 32, NKT32 = (a.T + 31) / 32;
+  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
 
   typename Pl::Frag qf[LS ? 1 : Pl::NF], vf[DQ ? Pl::NF : 1];
   {
@@ -567,15 +576,15 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   };
   auto issue_k = [&](int t) { dm.issue(kb + (int64_t)t * 32 * ldb, ldb, a.R - 1 - t * 32, kimg(t), wave); };
   f32x16 snext{};
-  if (NRT > 0) {
-    issue_a(0);
-    if (NEED_K && !DBL) issue_k(0);
-    if (sown) snext = blk_load(sbc, lane);
+  if (rt_beg < rt_end) {
+    issue_a(rt_beg);
+    if (NEED_K && !DBL) issue_k(rt_beg);
+    if (sown) snext = blk_load(sbc + rt_beg * sstep, lane);
     wait_vm<0>();
     raw_barrier();
   }
-  for (int rt = 0; rt < NRT; ++rt) {
-    const bool more = rt + 1 < NRT;
+  for (int rt = rt_beg; rt < rt_end; ++rt) {
+    const bool more = rt + 1 < rt_end;
     f32x16 s = snext;
     if (more) {
       issue_a(rt + 1);
@@ -628,12 +637,14 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   const float sc = DQ ? (a.prescaled ? LN2 : a.scale) : 1.f;
   char* base = reinterpret_cast<char*>(DQ ? a.dkc : a.dvc);
   const int64_t eo = ((int64_t)b * a.T + col) * a.ldg + h * D;
+  float* const part = ns > 1 ? (DQ ? a.cpq : a.cpv) + (((int64_t)sp * a.B + b) * a.T + col) * C + h * D : nullptr;
 #pragma unroll
   for (int d = 0; d < DB; ++d)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const float x0 = acc[d][4 * g] * sc, x1 = acc[d][4 * g + 1] * sc, x2 = acc[d][4 * g + 2] * sc, x3 = acc[d][4 * g + 3] * sc;
-      if (a.dkv16) Pl::store4(reinterpret_cast<T*>(base) + eo + d * 32 + 8 * g + 4 * hf, x0, x1, x2, x3);
+      if (part) *reinterpret_cast<f32x4*>(part + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};  // fp32 split partial
+      else if (a.dkv16) Pl::store4(reinterpret_cast<T*>(base) + eo + d * 32 + 8 * g + 4 * hf, x0, x1, x2, x3);
       else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + eo + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};
     }
 }
@@ -708,26 +719,66 @@ template <int DT, int D>
 int wide_cols(const xdot::fa::BwdArgs* a, hipStream_t st) {
   using namespace xdot::faw;
   using Pl = Pol<DT, D>;
-  const dim3 grid(((a->T + 127) / 128) * a->B * a->H);
+  const int W = ((a->T + 127) / 128) * a->B * a->H, sq = a->csq > 1 ? a->csq : 1, sv = a->csv > 1 ? a->csv : 1;
+  if ((sq > 1 && !a->cpq) || (sv > 1 && !a->cpv)) return -1;
+  const int odt = a->dkv16 ? DT : (int)xdot::DT_F32;
+  const int64_t rows = (int64_t)a->B * a->T;
+  // split partials of a pass summed into its grad half (output dtype)
+  auto fin = [&](bool dq) {
+    const int s = dq ? sq : sv;
+    if (s > 1) xdot_flash_cols_sum_launch(dq ? a->cpq : a->cpv, dq ? a->dkc : a->dvc, s, rows, a->H * D, a->ldg, odt, st);
+  };
+  auto dvp = [&](auto LSC) {
+    constexpr bool LSV = decltype(LSC)::value;
+    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, LSV>), dim3(W * sv), dim3(256), (cols_lds<Pl, false, LSV>()), st, *a);
+    fin(false);
+  };
+  auto dqp = [&](auto LSC) {
+    constexpr bool LSV = decltype(LSC)::value;
+    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, LSV>), dim3(W * sq), dim3(256), (cols_lds<Pl, true, LSV>()), st, *a);
+    fin(true);
+  };
   if constexpr (DT == xdot::DT_F32) {
     if (a->sbuf) {  // in place: dV first (the dQ pass overwrites S with dS); with a dS buffer dQ first
       const int ps = a->sb_passes ? a->sb_passes : 3;
       const bool dv_first = !a->dsbuf;
-      if ((ps & 1) && dv_first)
-        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, true>), grid, dim3(256), (cols_lds<Pl, false, true>()), st, *a);
-      if (ps & 2)
-        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, true>), grid, dim3(256), (cols_lds<Pl, true, true>()), st, *a);
-      if ((ps & 1) && !dv_first)
-        hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, true>), grid, dim3(256), (cols_lds<Pl, false, true>()), st, *a);
+      if ((ps & 1) && dv_first) dvp(std::true_type{});
+      if (ps & 2) dqp(std::true_type{});
+      if ((ps & 1) && !dv_first) dvp(std::true_type{});
       return 0;
     }
   }
   if constexpr (recompute_ok<DT, D>()) {
-    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, false>), grid, dim3(256), (cols_lds<Pl, false, false>()), st, *a);
-    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, false>), grid, dim3(256), (cols_lds<Pl, true, false>()), st, *a);
+    dvp(std::false_type{});
+    dqp(std::false_type{});
     return 0;
   }
   return -2;
+}
+
+// occupancy (workgroups per CU) of a wide instantiation: kernel 0 forward, 1 row side, 2 / 3
+// the column side's dQ / dV pass
+template <int DT, int D>
+int wide_occ(int kernel, bool sbuf) {
+  using namespace xdot::faw;
+  using xdot::fa::wg_per_cu;
+  using Pl = Pol<DT, D>;
+  const bool sb = DT == xdot::DT_F32 && sbuf;
+  if constexpr (DT == xdot::DT_F32) {
+    if (sb) {
+      if (kernel == 0) return wg_per_cu(fwd_kernel<DT, D, true>, fwd_lds<Pl>());
+      if (kernel == 1) return wg_per_cu(bwd_rows_kernel<DT, D, true>, rows_lds<Pl, true>());
+      if (kernel == 2) return wg_per_cu(bwd_cols_kernel<DT, D, true, true>, cols_lds<Pl, true, true>());
+      return wg_per_cu(bwd_cols_kernel<DT, D, false, true>, cols_lds<Pl, false, true>());
+    }
+  }
+  if constexpr (recompute_ok<DT, D>()) {
+    if (kernel == 0) return wg_per_cu(fwd_kernel<DT, D, false>, fwd_lds<Pl>());
+    if (kernel == 1) return wg_per_cu(bwd_rows_kernel<DT, D, false>, rows_lds<Pl, false>());
+    if (kernel == 2) return wg_per_cu(bwd_cols_kernel<DT, D, true, false>, cols_lds<Pl, true, false>());
+    return wg_per_cu(bwd_cols_kernel<DT, D, false, false>, cols_lds<Pl, false, false>());
+  }
+  return 0;
 }
 }  // namespace
 
@@ -750,5 +801,46 @@ extern "C" int xdot_flash_wide_cols_launch(const xdot::fa::BwdArgs* a, int dt, i
 #define L(DTV, DV) return wide_cols<DTV, DV>(a, st)
   XW_DISPATCH(L)
 #undef L
+}
+
+namespace {
+int wide_split_env() {  // XDOT_WIDE_SPLIT: unset / auto = the round model, 0 = the caller's old model, n = forced
+  const char* e = std::getenv("XDOT_WIDE_SPLIT");
+  if (!e || !*e || !std::strcmp(e, "auto")) return -1;
+  return std::max(0, std::atoi(e));
+}
+}  // namespace
+
+// Split counts of the wide kernels from their own occupancy (one workgroup per CU at these
+// widths): kernel 0 / 1 column splits of the forward / row side (0: the caller's model), kernel
+// 2 / 3 row splits of the column side's dQ / dV pass.  W = unsplit workgroups, n = tiles (32 wide)
+// of the split dimension.
+extern "C" int xdot_flash_wide_splits(int kernel, int dt, int D, bool sbuf, int64_t W, int64_t n) {
+  const int e = wide_split_env();
+  if (e == 0) return kernel >= 2 ? 1 : 0;
+  if (e > 0) return (int)std::min<int64_t>(e, n);
+  int occ = 0;
+#define L(DTV, DV) occ = wide_occ<DTV, DV>(kernel, sbuf); break
+  switch (dt * 1000 + D) {
+    case xdot::DT_BF16 * 1000 + 160: L(xdot::DT_BF16, 160);
+    case xdot::DT_BF16 * 1000 + 192: L(xdot::DT_BF16, 192);
+    case xdot::DT_BF16 * 1000 + 256: L(xdot::DT_BF16, 256);
+    case xdot::DT_BF16 * 1000 + 384: L(xdot::DT_BF16, 384);
+    case xdot::DT_F16 * 1000 + 160: L(xdot::DT_F16, 160);
+    case xdot::DT_F16 * 1000 + 192: L(xdot::DT_F16, 192);
+    case xdot::DT_F16 * 1000 + 256: L(xdot::DT_F16, 256);
+    case xdot::DT_F16 * 1000 + 384: L(xdot::DT_F16, 384);
+    case xdot::DT_F32 * 1000 + 160: L(xdot::DT_F32, 160);
+    case xdot::DT_F32 * 1000 + 192: L(xdot::DT_F32, 192);
+    case xdot::DT_F32 * 1000 + 256: L(xdot::DT_F32, 256);
+    case xdot::DT_F32 * 1000 + 384: L(xdot::DT_F32, 384);
+    default: break;
+  }
+#undef L
+  if (occ <= 0) return kernel >= 2 ? 1 : 0;
+  // forward / row side: partials of a wide 16-bit kernel cost ~1 % per split; the column side's
+  // row splits are capped at 4 (fp32 partials of the whole D-wide gradient per split)
+  return kernel >= 2 ? xdot::fa::pick_csplit(W, (int)n, occ * xdot_num_cus(), 4, 0.02)
+                     : xdot::fa::pick_csplit(W, (int)n, occ * xdot_num_cus(), 8, 0.01);
 }
 

@@ -251,6 +251,10 @@ int xdot_flash_cols_splits_cols2(const xdot::fa::BwdArgs* a, int dt, int D, int*
 int xdot_flash_f32_row_splits(int kernel, int fp32_mode, int D, bool sbuf, int64_t W, int64_t T);
 int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int64_t W, int64_t T);
 int xdot_flash_f32_row_splits_x3(int kernel, int D, bool sbuf, int64_t W, int64_t T);
+// split counts of the wide (D > 128) kernels from their own occupancy: kernel 0 / 1 = column
+// splits of the forward / row side (0: use the caller's model), 2 / 3 = row splits of the
+// column side's dQ / dV pass (XDOT_WIDE_SPLIT: auto, 0 = off, n = forced)
+int xdot_flash_wide_splits(int kernel, int dt, int D, bool sbuf, int64_t W, int64_t n);
 int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_t st);
 // wide head dims (csrc/flash_wide.hip): D = 160 / 192 / 256 / 384, 16-bit and exact fp32 (a wide
 // fp32 launch always runs exact); -1 = not a wide (dtype, D), -2 = needs the score buffer (fp32 D > 256)

@@ -237,3 +237,21 @@ def test_module_padded_heads_flash(gpu, dtype, cfg):
     assert _rel(xk.grad, xkd.grad) <= 10 * tol and _rel(xv.grad, xvd.grad) <= 10 * tol
     for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
         assert _rel(p.grad, q.grad) <= 10 * tol, n
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_flash_wide_row_splits(gpu, monkeypatch, dtype):
+    """Split counts of the wide kernels from their own occupancy (XDOT_WIDE_SPLIT): row splits of
+    both column passes (fp32 partials, ordered sum into the output dtype) and column splits of the
+    forward / row side; forced 2 / 3 and the automatic choice against the unsplit run and fp64."""
+    case = (1, 2100, 1, 1500, 2, 256)  # 66 row tiles, 47 column tiles
+    monkeypatch.setenv("XDOT_WIDE_SPLIT", "0")
+    inputs, base = _run(case, "blocks", gpu, dtype, scores=dtype == torch.float32, nsplit=0)
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    for sp in ("2", "3", "auto"):
+        monkeypatch.setenv("XDOT_WIDE_SPLIT", sp)
+        _, got = _run(case, "blocks", gpu, dtype, scores=dtype == torch.float32, nsplit=0)
+        for a, b in zip(base, got):
+            assert torch.isfinite(b).all()
+            assert _rel(b, a) <= tol, f"splits {sp}: {_rel(b, a):.2e}"
+        _check(case, inputs, got, 2e-6 if dtype == torch.float32 else 2e-2)
