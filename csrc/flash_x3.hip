@@ -75,26 +75,22 @@ __device__ __forceinline__ void split8(const float* x, u32x4& hi, u32x4& lo) {
 }
 
 template <int D> struct Cfg {
-  static constexpr int PR = D + 8;          // row-major image stride (bf16)
-  static constexpr int RM = 32 * PR * 2;    // bytes of one row-major image (hi or lo)
-  static constexpr int PT = 40;             // transposed image stride (bf16): 32 slots + pad
-  static constexpr int TR = D * PT * 2;     // bytes of one transposed image
-  static constexpr int KS = D / 16;         // 16-deep K steps over the head dim
-  static constexpr int DB = D / 32;         // 32-wide output blocks
-  static constexpr int NC = D / 32;         // f32x4 per thread per 32-row fp32 tile (256 threads)
+  static constexpr int ROW = fa::Img<D>::ROW;  // image row stride (bytes): the bf16 kernels' layout
+  static constexpr int KS = D / 16;            // 16-deep K steps over the head dim
+  static constexpr int DB = D / 32;            // 32-wide output blocks
+  static constexpr int NC = D / 32;            // f32x4 per thread per 32-row fp32 tile (256 threads)
 };
 
-// one staged image: row-major hi/lo (RMF) and/or transposed hi/lo (TRF)
+// One staged 32-row tile: a hi and a lo bf16 image, row-major in the bf16 kernels' swizzled
+// layout (fa::Img / fa::img_off: rows of ROW bytes, 16-byte chunks XOR (row >> 2) & 3).  Products
+// over the head dim read it with ds_read_b128 (fa::row_frag), products over the tile index with
+// the hardware transpose ds_read_b64_tr_b16 (fa::tr_frag), whose key order (k0 + 8 (j >> 2) + 4h
+// + (j & 3)) is the accumulator-register order the B operands come in: one image serves both
+// (the flags say which reads a kernel makes; the layout is the same).
 template <int D, bool RMF, bool TRF> struct Img {
-  using CF = Cfg<D>;
-  static constexpr int RMH = 0, RML = CF::RM;
-  static constexpr int TRH = RMF ? 2 * CF::RM : 0, TRL = TRH + CF::TR;
-  static constexpr int BYTES = (RMF ? 2 * CF::RM : 0) + (TRF ? 2 * CF::TR : 0);
+  static constexpr int H = 0, L = 32 * Cfg<D>::ROW;
+  static constexpr int BYTES = (RMF || TRF) ? 64 * Cfg<D>::ROW : 0;
 };
-
-// tile row c (0..31) -> slot of the transposed image (inverse of K step j, half h, t = 0..7
-// <-> row tidx(8j + t, h) = (t & 3) + 16j + 8(t >> 2) + 4h)
-__device__ __forceinline__ int slot_of(int c) { return 16 * (c >> 4) + 8 * ((c >> 2) & 1) + (c & 3) + 4 * ((c >> 3) & 1); }
 
 // one 32-row fp32 tile global -> registers (rows row0.., clamped to row0 + rmax) -> split images
 template <int D> struct Tile {
@@ -116,21 +112,9 @@ template <int D> struct Tile {
       uint32_t h0, l0, h1, l1;
       split2(r[i][0], r[i][1], h0, l0);
       split2(r[i][2], r[i][3], h1, l1);
-      if constexpr (RMF) {
-        const int o = (row * CF::PR + 4 * c) * 2;
-        *reinterpret_cast<u32x2*>(img + IL::RMH + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(img + IL::RML + o) = u32x2{l0, l1};
-      }
-      if constexpr (TRF) {
-        const int o = ((4 * c) * CF::PT + slot_of(row)) * 2;
-        const uint32_t hs[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
-        const uint32_t ls[4] = {l0 & 0xffffu, l0 >> 16, l1 & 0xffffu, l1 >> 16};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          *reinterpret_cast<uint16_t*>(img + IL::TRH + o + e * CF::PT * 2) = (uint16_t)hs[e];
-          *reinterpret_cast<uint16_t*>(img + IL::TRL + o + e * CF::PT * 2) = (uint16_t)ls[e];
-        }
-      }
+      const int o = fa::img_off<D>(row, c >> 1) + 8 * (c & 1);  // 4 bf16 = half a 16-byte chunk
+      *reinterpret_cast<u32x2*>(img + IL::H + o) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(img + IL::L + o) = u32x2{l0, l1};
     }
   }
 };
@@ -158,11 +142,11 @@ template <int D, bool RMF, bool TRF>
 __device__ __forceinline__ f32x16 rowprod(const char* img, const u32x4 (&fh)[D / 16], const u32x4 (&fl)[D / 16],
                                           f32x16 acc, int lane) {
   using IL = Img<D, RMF, TRF>;
-  const char* p = img + ((lane & 31) * Cfg<D>::PR + 8 * (lane >> 5)) * 2;
+  const fa::Lanes Ln = fa::make_lanes<D>(lane);
 #pragma unroll
   for (int m = 0; m < D / 16; ++m) {
-    const u32x4 ah = *reinterpret_cast<const u32x4*>(p + IL::RMH + 32 * m);
-    const u32x4 al = *reinterpret_cast<const u32x4*>(p + IL::RML + 32 * m);
+    const u32x4 ah = fa::row_frag<D>(img + IL::H, 0, m, Ln);
+    const u32x4 al = fa::row_frag<D>(img + IL::L, 0, m, Ln);
     acc = mm3(ah, al, fh[m], fl[m], acc);
   }
   return acc;
@@ -181,14 +165,13 @@ __device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 
     for (int t = 0; t < 8; ++t) v[t] = x[8 * j + t];
     split8(v, bh[j], bl[j]);
   }
-  const char* p = img + ((lane & 31) * CF::PT + 8 * (lane >> 5)) * 2;
+  const fa::Lanes Ln = fa::make_lanes<D>(lane);
 #pragma unroll
   for (int db = 0; db < D / 32; ++db)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int o = db * 32 * CF::PT * 2 + 32 * j;
-      const u32x4 ah = *reinterpret_cast<const u32x4*>(p + IL::TRH + o);
-      const u32x4 al = *reinterpret_cast<const u32x4*>(p + IL::TRL + o);
+      const u32x4 ah = fa::tr_frag<D>(img + IL::H, 16 * j, 32 * db, Ln);
+      const u32x4 al = fa::tr_frag<D>(img + IL::L, 16 * j, 32 * db, Ln);
       out[db] = mm3(ah, al, bh[j], bl[j], out[db]);
     }
 }

@@ -257,7 +257,7 @@ def ds_only_wanted(fp32_mode: int, D: int) -> bool:
     recomputes S and stores dS, the row kernel reads dS.  The split family's kernels are bound by
     the score traffic (S written, read twice, dS written and read: 100 GB per step at T = R =
     25000, H = 8); this mode moves 40 GB for one recomputed product on the column side."""
-    if D > (96 if fp32_mode == 1 else 128):  # split family at D = 128: the stages + transpose tiles exceed LDS
+    if D > 128:
         return False
     m = FLAGS.fp32_ds_only
     return m == "all" or (m == "split" and fp32_mode == 1)
