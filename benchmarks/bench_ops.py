@@ -135,8 +135,13 @@ def main(argv=None):
     # fp32 products: which fp32 family ran (exact fp32 MFMA / library fp32 GEMM by default, the
     # reference's precision; "split" = hi/lo bf16 halves, opt-in via XDOT_FP32_MODE=split)
     fp32_mode = _F.fp32_mode if a.dtype == "fp32" else None
+    # which GEMMs ran the products: the xdot kernels unless XDOT_GEMM_LIB routes them to the
+    # library (csrc/bindings.cpp gemm_lib: unset / 0 = none, "fp32" = exact-fp32 ones, 1 = all)
+    lib = (os.environ.get("XDOT_GEMM_LIB") or "0").strip().lower()
+    on_lib = lib.startswith("1") or (lib.startswith("f") and a.dtype == "fp32")
     rec = {"mode": a.mode, "schedule": a.schedule or "gather", "world_size": n, "emulated": bool(a.emulate), "T": T, "D": D, "offset": a.offset, "dtype": a.dtype,
-           "fp32_mode": fp32_mode, "link_gbps": a.link_gbps, "p2p_gbps": a.p2p_gbps}
+           "fp32_mode": fp32_mode, "link_gbps": a.link_gbps, "p2p_gbps": a.p2p_gbps,
+           "gemm": "library" if on_lib else "xdot"}
 
     local_trials = []
     fb = a.mode.endswith("_fb")
@@ -213,7 +218,7 @@ def main(argv=None):
         print(json.dumps(rec), flush=True)
         recs = [rec]
         for i in range(a.trials - 1):  # one record per synchronised call, in call order
-            r = {k: rec[k] for k in ("mode", "schedule", "world_size", "emulated", "T", "D", "offset", "dtype", "fp32_mode",
+            r = {k: rec[k] for k in ("mode", "schedule", "world_size", "emulated", "T", "D", "offset", "dtype", "fp32_mode", "gemm",
                                      "input_memory", "peak_memory", "output_memory", "distributed_input_memory",
                                      "distributed_peak_memory", "distributed_output_memory") if k in rec}
             r["trial"] = i + 1

@@ -332,6 +332,24 @@ template <> struct GldsRun<1> {
                  : "=&s"(keep) : "v"(o[0]), "s"(lds), "s"(base) : "memory");
   }
 };
+template <> struct GldsRun<2> {
+  static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %4\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %4\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "s"(lds), "s"(base) : "memory", "scc");
+  }
+};
+template <> struct GldsRun<4> {
+  static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %6\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %6\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %6\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %6\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(lds), "s"(base) : "memory", "scc");
+  }
+};
 template <> struct GldsRun<3> {
   static __device__ __forceinline__ void run(const void* base, const uint32_t* o, uint32_t lds) {
     uint32_t keep;

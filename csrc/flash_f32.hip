@@ -65,7 +65,8 @@ __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x)
 
 template <int D> struct Cfg {
   static constexpr int P = D + 4;       // image row stride (floats)
-  static constexpr int IMG = 32 * P;    // one 32-row image
+  static constexpr int NPC = (32 * P * 4 + 1023) / 1024;  // 1-KiB LDS-DMA pieces of one image
+  static constexpr int IMG = NPC * 256; // one 32-row image region (floats; >= 32 P, DMA slack at the end)
   static constexpr int KG = D / 8;      // b128 groups over the head dim (4 MFMAs each)
   static constexpr int DB = D / 32;     // 32-wide output blocks
   static constexpr int NC = D / 32;     // f32x4 chunks per thread per image (256 threads)
@@ -73,25 +74,51 @@ template <int D> struct Cfg {
   static constexpr int STAGE = 2 * IMG + AUX;
 };
 
-// two 32-row images (rows row0.., clamped to row0 + rmax) global -> registers -> LDS
-template <int D> struct Stager {
+// LDS-DMA staging of NI 32-row fp32 images with the same global row stride (HBM -> LDS with no
+// VGPR round trip, no per-element LDS writes).  The padded image (rows of P floats) is filled
+// linearly by 1-KiB pieces, wave w taking a contiguous run of them; each lane's 16 bytes map to
+// (row, 16-byte chunk) of the image, the pad chunks and the slack past the last row load a valid
+// dummy.  The kernels wait for the pieces (vmcnt(0)) before the tile's barrier.
+template <int D, int NI> struct DmaStager {
   using CF = Cfg<D>;
-  f32x4 r[2][CF::NC];
-  __device__ __forceinline__ void load(const float* b0, const float* b1, int64_t ld, int64_t row0, int rmax, int tid) {
+  static constexpr int RB = CF::P * 4, NPC = CF::NPC, Q4 = NPC / 4, R4 = NPC % 4;
+  static constexpr int MAXP = Q4 + (R4 ? 1 : 0);
+  int off[MAXP], row[MAXP];
+  int start, cnt;  // wave-uniform
+  __device__ __forceinline__ void init(int wave, int lane, int ld_bytes) {
+    cnt = Q4 + (wave < R4 ? 1 : 0);
+    start = wave * Q4 + min(wave, R4);
 #pragma unroll
-    for (int i = 0; i < CF::NC; ++i) {
-      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
-      const int64_t off = (row0 + min(row, rmax)) * ld + 4 * c;
-      r[0][i] = *reinterpret_cast<const f32x4*>(b0 + off);
-      r[1][i] = *reinterpret_cast<const f32x4*>(b1 + off);
+    for (int i = 0; i < MAXP; ++i) {
+      const int p = (start + i) * 1024 + lane * 16;
+      int r = p / RB, c = (p % RB) >> 4;
+      if (r >= 32 || c >= D / 4) r = c = 0;
+      row[i] = r;
+      off[i] = r * ld_bytes + c * 16;
     }
   }
-  __device__ __forceinline__ void store(float* img, int tid) const {
+  // images k = 0..NI-1 of tile rows row0.. (rows past rmax re-read row rmax) from b[k] into
+  // img + k * img_stride (floats)
+  __device__ __forceinline__ void issue(const float* const* b, int64_t ld, int64_t row0, int rmax, float* img,
+                                        int img_stride) const {
+    uint32_t o[MAXP];
 #pragma unroll
-    for (int i = 0; i < CF::NC; ++i) {
-      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
-      *reinterpret_cast<f32x4*>(img + row * CF::P + 4 * c) = r[0][i];
-      *reinterpret_cast<f32x4*>(img + CF::IMG + row * CF::P + 4 * c) = r[1][i];
+    for (int i = 0; i < MAXP; ++i) o[i] = (uint32_t)off[i];
+    if (rmax < 31) {
+#pragma unroll
+      for (int i = 0; i < MAXP; ++i) o[i] = (uint32_t)(off[i] - (row[i] - min(row[i], rmax)) * (int)(ld * 4));
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const char* base = reinterpret_cast<const char*>(b[k] + row0 * ld);
+      const uint32_t lds =
+          __builtin_amdgcn_readfirstlane(fa::lds_addr(reinterpret_cast<char*>(img + k * img_stride) + start * 1024));
+      if constexpr (R4 == 0) {
+        fa::GldsRun<Q4>::run(base, o, lds);
+      } else {
+        if (cnt == MAXP) fa::GldsRun<MAXP>::run(base, o, lds);
+        else fa::GldsRun<MAXP - 1>::run(base, o, lds);
+      }
     }
   }
 };
@@ -213,15 +240,25 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
                   : nullptr;
   const int64_t sbw_step = r0 < a.R ? 1024 : 0;
 
-  Stager<D> st;
+  DmaStager<D, 2> dm;
+  dm.init(wave, lane, (int)(a.ldkv * 4));
+  const float* const qvb[2] = {qb, vb};
   if (kt_beg < kt_end) {
-    st.load(qb, vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
-    st.store(sm, tid);
+    dm.issue(qvb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, sm, CF::IMG);
+    fa::wait_vm<0>();
     __syncthreads();
   }
+  float* const swl = sm + 2 * CF::STAGE + wave * 1024;  // S transpose tile (score buffer)
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const bool more = kt + 1 < kt_end;
-    if (more) st.load(qb, vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    // the previous tile's S leaves first: its global stores then complete under this tile's
+    // products instead of in the wait before its barrier (vmcnt counts stores too)
+    if constexpr (SS) {
+      if (kt > kt_beg) fa::blk_flush_lds(sbw + (int64_t)(kt - 1) * sbw_step, swl, lane);
+    }
+    if (more)  // into the stage the previous tile used (all reads of it ended at its barrier)
+      dm.issue(qvb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE,
+               CF::IMG);
     const float* qi = sm + ((kt - kt_beg) & 1) * CF::STAGE;
     const float* vi = qi + CF::IMG;
     int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
@@ -229,8 +266,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     f32x16 s{};
     if (flag != 1) s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
     // raw S, every tile (skipped tiles store zeros nobody reads): LDS writes here, the transposed
-    // global stores after the PV product
-    float* swl = sm + 2 * CF::STAGE + wave * 1024;
+    // global stores at the start of the next tile
     if constexpr (SS) fa::blk_put_lds(swl, s, lane);
     if (flag != 1) {
       const int valid = a.T - kt * 32;
@@ -265,9 +301,11 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
       l_run += ls;
       trprod<D>(vi, s, o, lane);  // Oᵀ += Vᵀ · Pᵀ
     }
-    if constexpr (SS) fa::blk_flush_lds(sbw + (int64_t)kt * sbw_step, swl, lane);
-    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
+    fa::wait_vm<0>();  // the next tile's pieces landed
     __syncthreads();
+  }
+  if constexpr (SS) {
+    if (kt_end > kt_beg) fa::blk_flush_lds(sbw + (int64_t)(kt_end - 1) * sbw_step, swl, lane);
   }
 
   const float l_tot = pair_sum(l_run);
@@ -379,15 +417,19 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
   if constexpr (D >= 128) fa::pin_agpr(dk);  // one wave per SIMD: accumulators in AGPRs
 
-  Stager<D> st;
+  DmaStager<D, 2> dm;
+  dm.init(wave, lane, (int)(a.ldkv * 4));
+  const float* const qvb[2] = {qb, vb};
   if (kt_beg < kt_end) {
-    st.load(qb, vb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
-    st.store(sm, tid);
+    dm.issue(qvb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, sm, CF::IMG);
+    fa::wait_vm<0>();
     __syncthreads();
   }
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const bool more = kt + 1 < kt_end;
-    if (more) st.load(qb, vb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    if (more)  // into the stage the previous tile used (all reads of it ended at its barrier)
+      dm.issue(qvb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE,
+               CF::IMG);
     const float* qi = sm + ((kt - kt_beg) & 1) * CF::STAGE;
     const float* vi = qi + CF::IMG;
     int flag = r0 >= a.R ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
@@ -411,7 +453,7 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
       trprod<D>(qi, s, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
       if constexpr (D >= 128) fa::pin_agpr(dk);
     }
-    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::STAGE, tid);
+    fa::wait_vm<0>();  // the next tile's pieces landed
     __syncthreads();
   }
   if (!row_ok) return;
@@ -499,21 +541,28 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     if (tid < 64) return rr < a.R ? dlt[rr] : 0.f;
     return 0.f;
   };
-  Stager<D> st;
+  DmaStager<D, 2> dm;
+  dm.init(wave, lane, C * 4);
+  const float* const kdb[2] = {kb, db_};
   float ax = 0.f;
   if (rt_beg < rt_end) {
-    st.load(kb, db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    dm.issue(kdb, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, sm, CF::IMG);
     ax = aux_load(rt_beg);
-    st.store(sm, tid);
     if (tid < 64) sm[2 * CF::IMG + tid] = ax;
+    fa::wait_vm<0>();
     __syncthreads();
   }
+  float* const dwl = sm + 2 * CF::STAGE + wave * 1024;  // dS transpose tile
   for (int rt = rt_beg; rt < rt_end; ++rt) {
     const bool more = rt + 1 < rt_end;
     f32x16 scur;
     if constexpr (LS) scur = snext;
+    // the previous tile's dS leaves first (its stores complete under this tile's products)
+    if constexpr (DS) {
+      if (rt > rt_beg) fa::blk_flush_lds(dsc + (rt - 1) * dstep, dwl, lane);
+    }
     if (more) {
-      st.load(kb, db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      dm.issue(kdb, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE, CF::IMG);
       ax = aux_load(rt + 1);
       if constexpr (LS) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
@@ -542,8 +591,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       }
     }
     // dS (over S or apart), every tile (skipped tiles store zeros nobody reads): LDS writes
-    // before the dQ product, the transposed global stores after it
-    float* dwl = sm + 2 * CF::STAGE + wave * 1024;
+    // before the dQ product, the transposed global stores at the start of the next tile
     if constexpr (DS) fa::blk_put_lds(dwl, dp, lane);
     if (flag != 1) {
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
@@ -553,13 +601,15 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         fa::pin_agpr(dv);
       }
     }
-    if constexpr (DS) fa::blk_flush_lds(dsc + rt * dstep, dwl, lane);
     if (more) {
       float* nx = sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE;
-      st.store(nx, tid);
       if (tid < 64) nx[2 * CF::IMG + tid] = ax;
     }
+    fa::wait_vm<0>();  // the next tile's pieces (and S) landed
     __syncthreads();
+  }
+  if constexpr (DS) {
+    if (rt_end > rt_beg) fa::blk_flush_lds(dsc + (rt_end - 1) * dstep, dwl, lane);
   }
   if (!col_ok) return;
   const int64_t prow = ((int64_t)sp * a.B + b) * a.T + col;  // row of the split partials
@@ -582,24 +632,6 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
 // backward, row side in score-buffer mode: dK = scale · Σ_cols dS · Q_cols with dS read from the
 // buffer the column kernel wrote (one product per tile: no S, no dP, no V / dO traffic).  Same
 // grid, column split and partial protocol as bwd_rows_kernel; the only LDS image is Q.
-template <int D> struct Stager1 {  // one 32-row image (Q) global -> registers -> LDS
-  using CF = Cfg<D>;
-  f32x4 r[CF::NC];  // 32 rows x D floats = 256 threads x NC f32x4
-  __device__ __forceinline__ void load(const float* b0, int64_t ld, int64_t row0, int rmax, int tid) {
-#pragma unroll
-    for (int i = 0; i < CF::NC; ++i) {
-      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
-      r[i] = *reinterpret_cast<const f32x4*>(b0 + (row0 + min(row, rmax)) * ld + 4 * c);
-    }
-  }
-  __device__ __forceinline__ void store(float* img, int tid) const {
-#pragma unroll
-    for (int i = 0; i < CF::NC; ++i) {
-      const int q = tid + 256 * i, row = q / (D / 4), c = q % (D / 4);
-      *reinterpret_cast<f32x4*>(img + row * CF::P + 4 * c) = r[i];
-    }
-  }
-};
 
 template <int D>
 __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
@@ -627,21 +659,22 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
 
   constexpr int PF = XDOT_SB_PF;
-  Stager1<D> st;
+  DmaStager<D, 1> dm;
+  dm.init(wave, lane, (int)(a.ldkv * 4));
   f32x16 q[PF];
   if (kt_beg < kt_end) {
-    st.load(qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, tid);
+    dm.issue(&qb, a.ldkv, (int64_t)kt_beg * 32, a.T - 1 - kt_beg * 32, sm, CF::IMG);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
       if (kt_beg + j < kt_end) q[j] = blk_load(sbr + (int64_t)(kt_beg + j) * 1024, lane);
-    st.store(sm, tid);
+    fa::wait_vm<0>();
     __syncthreads();
   }
   fa::ring_loop<PF>(kt_beg, kt_end, [&](int kt, auto J) {
     constexpr int j = decltype(J)::value;
     const bool more = kt + 1 < kt_end;
     f32x16 ds = q[j];
-    if (more) st.load(qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, tid);
+    if (more) dm.issue(&qb, a.ldkv, (int64_t)(kt + 1) * 32, a.T - 1 - (kt + 1) * 32, sm + ((kt + 1 - kt_beg) & 1) * CF::IMG, 0);
     if (kt + PF < kt_end) q[j] = blk_load(sbr + (int64_t)(kt + PF) * 1024, lane);  // every wave: uniform vmcnt
     const float* qi = sm + ((kt - kt_beg) & 1) * CF::IMG;
     int flag = !wave_ok ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, r0 >> 5, kt >> 1) : 0);
@@ -655,7 +688,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
       }
       trprod<D>(qi, ds, dk, lane);  // dKᵀ += Q_colsᵀ · dSᵀ
     }
-    if (more) st.store(sm + ((kt + 1 - kt_beg) & 1) * CF::IMG, tid);
+    fa::wait_vm<0>();  // the next tile's pieces landed
     __syncthreads();
   });
   if (!row_ok) return;
@@ -707,17 +740,18 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
   };
   constexpr int PF = XDOT_SB_PF;
-  Stager1<D> st;
+  DmaStager<D, 1> dm;
+  dm.init(wave, lane, C * 4);
   f32x16 q[PF];
   float ax = 0.f;
   if (rt_beg < rt_end) {
-    st.load(db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, tid);
+    dm.issue(&db_, C, (int64_t)rt_beg * 32, a.R - 1 - rt_beg * 32, sm, 0);
     ax = aux_load(rt_beg);
 #pragma unroll
     for (int j = 0; j < PF; ++j)
       if (rt_beg + j < rt_end) q[j] = blk_load(sbc + (rt_beg + j) * sstep, lane);
-    st.store(sm, tid);
     if (tid < 32) sm[CF::IMG + tid] = ax;
+    fa::wait_vm<0>();
     __syncthreads();
   }
   fa::ring_loop<PF>(rt_beg, rt_end, [&](int rt, auto J) {
@@ -725,7 +759,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     const bool more = rt + 1 < rt_end;
     f32x16 s = q[j];
     if (more) {
-      st.load(db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, tid);
+      dm.issue(&db_, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, sm + ((rt + 1 - rt_beg) & 1) * STG, 0);
       ax = aux_load(rt + 1);
     }
     if (rt + PF < rt_end) q[j] = blk_load(sbc + (rt + PF) * sstep, lane);  // every wave: uniform vmcnt
@@ -746,9 +780,9 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     }
     if (more) {
       float* nx = sm + ((rt + 1 - rt_beg) & 1) * STG;
-      st.store(nx, tid);
       if (tid < 32) nx[CF::IMG + tid] = ax;
     }
+    fa::wait_vm<0>();  // the next tile's pieces landed
     __syncthreads();
   });
   if (!col_ok) return;
