@@ -150,3 +150,25 @@ def test_measure_debug_output(capsys, monkeypatch):
         monkeypatch.delenv("XDOT_DEBUG")
         FLAGS.reload()
     assert "distributed_matmul_nt" in capsys.readouterr().out
+
+
+def test_fp32_buffer_mode_flags(monkeypatch):
+    """XDOT_FP32_DS_ONLY picks which fp32 families keep only a dS buffer (flash.ds_only_wanted):
+    the split family by default, both or none on request, never the wide heads."""
+    from xdot.ops import flash
+    from xdot.utils.env import FLAGS
+
+    old = FLAGS.fp32_ds_only
+    try:
+        for mode, exact, split in (("split", False, True), ("all", True, True), ("none", False, False)):
+            monkeypatch.setenv("XDOT_FP32_DS_ONLY", mode)
+            FLAGS.reload()
+            assert FLAGS.fp32_ds_only == mode
+            assert flash.ds_only_wanted(0, 96) is exact and flash.ds_only_wanted(1, 96) is split
+            assert flash.ds_only_wanted(1, 128) is split
+            assert not flash.ds_only_wanted(0, 256) and not flash.ds_only_wanted(1, 384)
+        monkeypatch.delenv("XDOT_FP32_DS_ONLY")
+        FLAGS.reload()
+        assert FLAGS.fp32_ds_only == "split"
+    finally:
+        FLAGS.fp32_ds_only = old
