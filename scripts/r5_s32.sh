@@ -2,7 +2,7 @@
 # Round 5 pass 32: closing health -- full GPU suite, smoke, default bench, masked ratio
 # (interleaved), long context T = 200000 at the reference example's heads (h = 2) and h = 8
 set -o pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/r5s32; mkdir -p $OUT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r5s32}; mkdir -p $OUT
 export XDOT_EXT_PATH=$GRAFT_REPO_ROOT/xdot/_C.so
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log
