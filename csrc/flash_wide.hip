@@ -12,7 +12,7 @@
 // tensors, packed masks from mask_pack.hip), re-balanced for a wide head:
 //   * one wave per SIMD (launch_bounds(256, 1)): a wave's 32-row fragment of the stationary side
 //     (D/4 VGPRs in 16-bit, D/2 in fp32) and its output accumulators (D/2) need up to ~430 of the
-//     512 unified VGPR+AGPR registers;
+//     512 unified VGPR+AGPR registers (the 16-bit forward at D <= 256 fits two: fwd_occ);
 //   * 32-row tiles of the streamed side arrive by LDS-DMA (global_load_lds_dwordx4: no staging
 //     registers), double-buffered, one barrier per tile; where two fp32 D = 384 images per stage
 //     would not fit LDS twice, the image used second is single-buffered and refilled mid-tile;
@@ -98,10 +98,19 @@ template <int DT, int D> struct Pol {  // 16-bit
   // acc += image rows (lane & 31) . fragᵀ over the head dim.  Operand reads run two MFMAs ahead
   // and sched_barrier keeps them there: unfenced, the compiler hoists all D/16 reads (4 VGPRs
   // each) to the top and a wide head spills.
+  // (LA = 1: one read ahead, for a kernel whose registers are two workgroups' share)
+  template <int LA = 2>
   static __device__ __forceinline__ f32x16 rowprod(const char* img, const Frag (&f)[NF], f32x16 acc, const Lanes& L) {
-    u32x4 a0 = fa::row_frag<D>(img, 0, 0, L.L), a1 = fa::row_frag<D>(img, 0, 1, L.L);
+    u32x4 a0 = fa::row_frag<D>(img, 0, 0, L.L), a1 = LA > 1 ? fa::row_frag<D>(img, 0, 1, L.L) : a0;
 #pragma unroll
     for (int s = 0; s < NF; ++s) {
+      if (LA == 1) {
+        const u32x4 cur = a0;
+        if (s + 1 < NF) a0 = fa::row_frag<D>(img, 0, s + 1, L.L);
+        acc = fa::mfma32<DT>::run(cur, f[s], acc);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       u32x4 a2 = a1;
       if (s + 2 < NF) a2 = fa::row_frag<D>(img, 0, s + 2, L.L);
       acc = fa::mfma32<DT>::run(a0, f[s], acc);
@@ -112,12 +121,21 @@ template <int DT, int D> struct Pol {  // 16-bit
     return acc;
   }
   // out[db] += imageᵀ (d x tile row) . x (tile row x lane), x an accumulator tile
+  template <int LA = 2>
   static __device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 (&out)[D / 32], const Lanes& L) {
     constexpr int DB = D / 32, N = 2 * DB;
     const u32x4 pf[2] = {fa::acc_to_frag<DT>(x, 0), fa::acc_to_frag<DT>(x, 1)};
     u32x4 v0 = fa::tr_frag<D>(img, 0, 0, L.L), v1 = fa::tr_frag<D>(img, 16 * (1 / DB), 32 * (1 % DB), L.L);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
+      if (LA == 1) {
+        const u32x4 cur = v0;
+        v0 = v1;
+        if (i + 2 < N) v1 = fa::tr_frag<D>(img, 16 * ((i + 2) / DB), 32 * ((i + 2) % DB), L.L);
+        out[i % DB] = fa::mfma32<DT>::run(cur, pf[i / DB], out[i % DB]);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
       u32x4 v2 = v1;
       if (i + 2 < N) v2 = fa::tr_frag<D>(img, 16 * ((i + 2) / DB), 32 * ((i + 2) % DB), L.L);
       out[i % DB] = fa::mfma32<DT>::run(v0, pf[i / DB], out[i % DB]);
@@ -158,7 +176,8 @@ template <int D> struct Pol<DT_F32, D> {
       for (int t = 0; t < 4; ++t) f[4 * g + t] = v[t];
     }
   }
-  // (operand reads one group ahead, fenced as in the 16-bit policy)
+  // (operand reads one group ahead, fenced as in the 16-bit policy; LA unused)
+  template <int LA = 2>
   static __device__ __forceinline__ f32x16 rowprod(const char* img, const Frag (&f)[NF], f32x16 acc, const Lanes& L) {
     const float* p = reinterpret_cast<const float*>(img + (L.lane & 31) * ROW) + 4 * (L.lane >> 5);
     f32x4 a0 = *reinterpret_cast<const f32x4*>(p);
@@ -173,6 +192,7 @@ template <int D> struct Pol<DT_F32, D> {
     }
     return acc;
   }
+  template <int LA = 2>
   static __device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 (&out)[D / 32], const Lanes& L) {
     constexpr int DB = D / 32;
     const int hf = L.lane >> 5;
@@ -236,13 +256,23 @@ template <class Pl> constexpr bool dbl2() { return 4 * Dma32<Pl>::SLOT + 1024 <=
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split.
 // Stage: [Q image][V image]; SS: store the raw scores into a.sbuf (exact fp32).
+// 16-bit D <= 256: 128 accumulator AGPRs + the K fragment fit 256 registers, so two workgroups
+// share a CU and one wave's softmax VALU runs beside the other's MFMAs (LDS: 2 x 80 KB at D = 256)
+template <int DT, int D> constexpr int fwd_occ() {
+#ifdef XDOT_WIDE_OCC1
+  return 1;
+#else
+  return (DT != DT_F32 && D <= 256) ? 2 : 1;
+#endif
+}
 template <int DT, int D, bool SS>
-__global__ __launch_bounds__(256, 1) void fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a) {
   using Pl = Pol<DT, D>;
   using T = typename Pl::T;
   using DM = Dma32<Pl>;
   constexpr int DB = D / 32, SLOT = DM::SLOT;
   constexpr bool DBL = dbl2<Pl>();
+  constexpr int LA = (fwd_occ<DT, D>() == 2 && D >= 256) ? 1 : 2;  // operand reads ahead
   char* const sm = fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -298,18 +328,14 @@ __global__ __launch_bounds__(256, 1) void fwd_kernel(FwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     f32x16 s;
     if (flag != 1) {
-      s = Pl::rowprod(qimg(kt), kf, f32x16{}, L);  // Sᵀ: col (register) x row (lane)
+      s = Pl::template rowprod<LA>(qimg(kt), kf, f32x16{}, L);  // Sᵀ: col (register) x row (lane)
       pin_first<KFA>(kf);
       if constexpr (SS) blk_store(sbw + (int64_t)kt * 1024, s, lane);
       const int valid = a.T - kt * 32;
-      if (flag == 2 || valid < 32) {
+      if (flag == 2 || valid < 32) {  // bit tidx(r, hf) of the word (or column >= valid) -> -inf
         uint32_t w = 0;
         if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = tidx(r, hf);
-          if (((w >> c) & 1u) || c >= valid) s[r] = NEG_INF;
-        }
+        fa::sel_bits16(s, (uint32_t)fa::tile_bits(w, valid, hf), fa::NINF_BITS);
       }
       float mx = NEG_INF;
 #pragma unroll
@@ -335,7 +361,7 @@ __global__ __launch_bounds__(256, 1) void fwd_kernel(FwdArgs a) {
       wait_vm<0>();
       raw_barrier();
     }
-    if (flag != 1) Pl::trprod(vimg(kt), s, o, L);  // Oᵀ += Vᵀ · Pᵀ
+    if (flag != 1) Pl::template trprod<LA>(vimg(kt), s, o, L);  // Oᵀ += Vᵀ · Pᵀ
     pin_agpr(o);
     if (!DBL && more) {
       raw_barrier();  // every wave is done with the single V image
