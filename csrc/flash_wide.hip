@@ -256,6 +256,17 @@ template <class Pl> constexpr bool dbl2() { return 4 * Dma32<Pl>::SLOT + 1024 <=
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split.
 // Stage: [Q image][V image]; SS: store the raw scores into a.sbuf (exact fp32).
+// backward softmax: the mask select in a wave-uniform branch taken by partial tiles only, softmax
+// logits in place (a per-score test on every tile cost the 16-bit D = 160-256 column side 1.3x,
+// profiles/r5_wide_long.md).  K: 0 row side, 1 dV pass, 2 dQ pass.  The instantiations whose
+// registers this would spill (two D-wide sets and D = 384 / fp32 D = 256) keep the per-score form.
+template <int DT, int D, int K> constexpr bool SELB() {
+#ifdef XDOT_WIDE_NOSELB
+  return false;
+#else
+  return K == 1 || !(D == 384 || (DT == DT_F32 && D == 256));
+#endif
+}
 // 16-bit D <= 256: 128 accumulator AGPRs + the K fragment fit 256 registers, so two workgroups
 // share a CU and one wave's softmax VALU runs beside the other's MFMAs (LDS: 2 x 80 KB at D = 256)
 template <int DT, int D> constexpr int fwd_occ() {
@@ -479,17 +490,29 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
       } else {
         f32x16 s = Pl::rowprod(qi, kf, f32x16{}, L);          // Sᵀ  (col x row)
         f32x16 dp = Pl::rowprod(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
-        uint32_t w = 0;
-        const bool chk = flag == 2 || valid < 32;
-        if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
+        if constexpr (SELB<DT, D, 0>()) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = __builtin_fmaf(s[r], c2, -lse2);
-          if (chk) {
-            const int c = tidx(r, hf);
-            if (((w >> c) & 1u) || c >= valid) x = NEG_INF;
+          for (int r = 0; r < 16; ++r) s[r] = __builtin_fmaf(s[r], c2, -lse2);  // in place
+          if (flag == 2 || valid < 32) {  // partial tiles only: masked bits / columns past T -> -inf
+            uint32_t w = 0;
+            if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
+            fa::sel_bits16(s, (uint32_t)fa::tile_bits(w, valid, hf), fa::NINF_BITS);
           }
-          ds[r] = __builtin_amdgcn_exp2f(x) * (dp[r] - dlt);  // dSᵀ / scale
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(s[r]) * (dp[r] - dlt);  // dSᵀ / scale
+        } else {
+          uint32_t w = 0;
+          const bool chk = flag == 2 || valid < 32;
+          if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = __builtin_fmaf(s[r], c2, -lse2);
+            if (chk) {
+              const int c = tidx(r, hf);
+              if (((w >> c) & 1u) || c >= valid) x = NEG_INF;
+            }
+            ds[r] = __builtin_amdgcn_exp2f(x) * (dp[r] - dlt);  // dSᵀ / scale
+          }
         }
       }
       Pl::trprod(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
@@ -624,17 +647,35 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
       if constexpr (!LS) s = Pl::rowprod(kimg(rt), qf, f32x16{}, L);  // S (row x col)
       if constexpr (DQ) dp = Pl::rowprod(doimg(rt), vf, f32x16{}, L);  // dP (row x col)
       pin_frags();
-      uint32_t w = 0;
-      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
-      const int vr = a.R - rt * 32;  // valid rows of this tile
+      if constexpr (SELB<DT, D, DQ ? 2 : 1>()) {
+        const int vr = a.R - rt * 32;  // valid rows of this tile
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = tidx(r, hf);
-        float x = __builtin_fmaf(s[r], c2, -ls[i]);
-        if ((flag == 2 && ((w >> i) & 1u)) || i >= vr) x = NEG_INF;
-        const float p = __builtin_amdgcn_exp2f(x);
-        if constexpr (DQ) dp[r] = p * (dp[r] - ls[64 + i]);  // dS / scale
-        else s[r] = p;
+        for (int r = 0; r < 16; ++r) s[r] = __builtin_fmaf(s[r], c2, -ls[tidx(r, hf)]);  // in place
+        // partial tiles only (wave-uniform branch): masked bits / rows past R -> -inf
+        if (flag == 2 || vr < 32) {
+          uint32_t w = 0;
+          if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
+          fa::sel_bits16(s, (uint32_t)fa::tile_bits(w, vr, hf), fa::NINF_BITS);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[r]);
+          if constexpr (DQ) dp[r] = p * (dp[r] - ls[64 + tidx(r, hf)]);  // dS / scale
+          else s[r] = p;
+        }
+      } else {
+        uint32_t w = 0;
+        if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1))));
+        const int vr = a.R - rt * 32;  // valid rows of this tile
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = tidx(r, hf);
+          float x = __builtin_fmaf(s[r], c2, -ls[i]);
+          if ((flag == 2 && ((w >> i) & 1u)) || i >= vr) x = NEG_INF;
+          const float p = __builtin_amdgcn_exp2f(x);
+          if constexpr (DQ) dp[r] = p * (dp[r] - ls[64 + i]);  // dS / scale
+          else s[r] = p;
+        }
       }
       if constexpr (DQ && LS) blk_store(dsc + rt * sstep, dp, lane);  // dS over S or apart (row-kernel order)
       if constexpr (!DQ) Pl::trprod(doimg(rt), s, acc, L);  // dVᵀ += dOᵀ · P
