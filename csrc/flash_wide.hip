@@ -233,11 +233,17 @@ template <class Pl> struct Dma32 {
   static constexpr int NPC = (BYTES + 4095) / 4096 * 4;
   static constexpr int PPW = NPC / 4;
   static constexpr int SLOT = NPC * 1024;
+  static_assert(Pl::ROW <= 2048, "16 x the 16-byte chunk index must fit 11 bits");
   int wave, lane;
-  __device__ __forceinline__ void init(int w, int l, int) { wave = w; lane = l; }
-  // tile rows past rmax (past T / R) re-read row rmax: callers mask them.  The per-piece source
-  // offsets are recomputed at every issue (a few integer ops) rather than held in 2 x PPW VGPRs.
-  __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int) const {
+  // per piece of this lane: image row r (5 bits) | 16 x chunk (11 bits) << 5, two pieces per
+  // register, computed once: an issue then costs 4 VALU per piece (2 bfe, min, mad) instead of the
+  // ~16 of the division / swizzle / clamp arithmetic
+  uint32_t pk[(PPW + 1) / 2];
+  __device__ __forceinline__ void init(int w, int l, int) {
+    wave = w;
+    lane = l;
+#pragma unroll
+    for (int i = 0; i < (PPW + 1) / 2; ++i) pk[i] = 0;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int p = (wave * PPW + i) * 1024 + lane * 16;
@@ -245,7 +251,32 @@ template <class Pl> struct Dma32 {
       int c = (p % Pl::ROW) >> 4;
       if (Pl::SWZ) c ^= (r >> 2) & 3;
       if (c >= Pl::VALID || p >= BYTES) c = 0;
-      fa::glds16(base, (uint32_t)(min(r, rmax) * stride_bytes + c * 16), img + (wave * PPW + i) * 1024);
+      pk[i / 2] |= (uint32_t)(r | ((16 * c) << 5)) << (16 * (i & 1));
+    }
+  }
+  // tile rows past rmax (past T / R) re-read row rmax: callers mask them; padding chunks and the
+  // slack rows past 32 load a valid dummy address.
+  // SKIP: pieces wholly past the image are not loaded (their LDS stays free for other data; the
+  // waves then issue different counts, so only callers that drain with vmcnt(0) may use it)
+  template <bool SKIP = false>
+  __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int) const {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      // (SKIP: the piece index through readfirstlane keeps the LDS address an SGPR operand)
+      const int pc = SKIP ? __builtin_amdgcn_readfirstlane(wave * PPW + i) : wave * PPW + i;
+      if (SKIP && pc * 1024 >= BYTES) continue;  // wave-uniform
+#ifdef XDOT_WIDE_NOPK  // A/B: recompute the piece's row / chunk at every issue
+      const int p = pc * 1024 + lane * 16;
+      const int r = min(p / Pl::ROW, 31);
+      int c = (p % Pl::ROW) >> 4;
+      if (Pl::SWZ) c ^= (r >> 2) & 3;
+      if (c >= Pl::VALID || p >= BYTES) c = 0;
+      fa::glds16(base, (uint32_t)(min(r, rmax) * stride_bytes + c * 16), img + pc * 1024);
+#else
+      const uint32_t r = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1), 5);
+      const uint32_t c16 = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1) + 5, 11);
+      fa::glds16(base, (uint32_t)min((int)r, rmax) * (uint32_t)stride_bytes + c16, img + pc * 1024);
+#endif
     }
   }
 };
@@ -267,6 +298,17 @@ template <int DT, int D, int K> constexpr bool SELB() {
   return K == 1 || !(D == 384 || (DT == DT_F32 && D == 256));
 #endif
 }
+// The 16-bit D = 256 dV pass at two workgroups per CU: 128 accumulator AGPRs + the Q fragment
+// in 128 VGPRs (operand reads one ahead), and its four 20-KiB images fill 80 KiB exactly, so the
+// lse2 / δ rows move into the dO slots' 2 KiB of slack (aux_in_slack)
+template <int DT, int D, bool DQ, bool LS> constexpr int cols_occ() {
+#ifdef XDOT_WIDE_COLS_OCC1
+  return 1;
+#else
+  return (DT != DT_F32 && D == 256 && !DQ && !LS) ? 2 : 1;
+#endif
+}
+template <int DT, int D, bool DQ, bool LS> constexpr bool aux_in_slack() { return cols_occ<DT, D, DQ, LS>() == 2; }
 // 16-bit D <= 256: 128 accumulator AGPRs + the K fragment fit 256 registers, so two workgroups
 // share a CU and one wave's softmax VALU runs beside the other's MFMAs (LDS: 2 x 80 KB at D = 256)
 template <int DT, int D> constexpr int fwd_occ() {
@@ -551,7 +593,7 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
 // kernel); else S = K · Q_colsᵀ from register-resident Q fragments and the K image.
 // Stage: [dO image][K image][lse2 | δ, 256 B]; images a pass does not read are not loaded.
 template <int DT, int D, bool DQ, bool LS>
-__global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_kernel(BwdArgs a) {
   using Pl = Pol<DT, D>;
   using T = typename Pl::T;
   using DM = Dma32<Pl>;
@@ -560,6 +602,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   // the image used second in the tile (K for dQ) is single-buffered when two per stage do not fit
   constexpr bool DBL = !(NEED_K && NEED_DO) || dbl2<Pl>();
   constexpr int AUX = 1024;  // lse2[32], δ[32] at the start of a 1-KiB slot
+  constexpr int CLA = cols_occ<DT, D, DQ, LS>() == 2 ? 1 : 2;  // operand reads ahead
   char* const sm = fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -600,9 +643,13 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   DM dm;
   dm.init(wave, lane, ldb);
   // LDS: [dO 0][dO 1][aux 0][aux 1][K 0][K 1 (DBL)]
+  // AUXS (two workgroups per CU): lse2 / δ in the dO slots' slack past the image, so the
+  // four images alone fill the workgroup's 80 KiB
+  constexpr bool AUXS = aux_in_slack<DT, D, DQ, LS>();
+  static_assert(!AUXS || (DM::BYTES % 1024 == 0 && DM::SLOT - DM::BYTES >= 512), "lse2 / δ need 512 B of whole-piece slack");
   auto doimg = [&](int t) { return sm + (t & 1) * SLOT; };
-  auto aux = [&](int t) { return sm + 2 * SLOT + (t & 1) * AUX; };
-  auto kimg = [&](int t) { return sm + 2 * SLOT + 2 * AUX + (DBL ? (t & 1) * SLOT : 0); };
+  auto aux = [&](int t) { return AUXS ? doimg(t) + DM::BYTES : sm + 2 * SLOT + (t & 1) * AUX; };
+  auto kimg = [&](int t) { return sm + 2 * SLOT + (AUXS ? 0 : 2 * AUX) + (DBL ? (t & 1) * SLOT : 0); };
   const float c2 = a.prescaled ? 1.f : a.scale * LOG2E, NEG_INF = -__builtin_inff();
   f32x16 acc[DB];
 #pragma unroll
@@ -617,7 +664,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
   // the tile's rows at aux floats [0, 32), δ at [64, 96) (two 256-byte DMAs, lanes >= 32 load
   // duplicates into the unused halves)
   auto issue_a = [&](int t) {
-    dm.issue(db_ + (int64_t)t * 32 * ldb, ldb, a.R - 1 - t * 32, doimg(t), wave);
+    dm.template issue<AUXS>(db_ + (int64_t)t * 32 * ldb, ldb, a.R - 1 - t * 32, doimg(t), wave);
     const uint32_t rr = (uint32_t)min(t * 32 + (lane & 31), a.R - 1) * 4;
     fa::glds4(lse2, rr, aux(t));
     fa::glds4(dlt, rr, aux(t) + 256);
@@ -644,7 +691,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
     flag = __builtin_amdgcn_readfirstlane(flag);
     f32x16 dp;
     if (flag != 1) {
-      if constexpr (!LS) s = Pl::rowprod(kimg(rt), qf, f32x16{}, L);  // S (row x col)
+      if constexpr (!LS) s = Pl::template rowprod<CLA>(kimg(rt), qf, f32x16{}, L);  // S (row x col)
       if constexpr (DQ) dp = Pl::rowprod(doimg(rt), vf, f32x16{}, L);  // dP (row x col)
       pin_frags();
       if constexpr (SELB<DT, D, DQ ? 2 : 1>()) {
@@ -678,7 +725,7 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
         }
       }
       if constexpr (DQ && LS) blk_store(dsc + rt * sstep, dp, lane);  // dS over S or apart (row-kernel order)
-      if constexpr (!DQ) Pl::trprod(doimg(rt), s, acc, L);  // dVᵀ += dOᵀ · P
+      if constexpr (!DQ) Pl::template trprod<CLA>(doimg(rt), s, acc, L);  // dVᵀ += dOᵀ · P
     }
     if constexpr (DQ) {
       if (!DBL) {  // K(rt) was DMA'd after the previous tile's dQ: complete and visible first
@@ -718,10 +765,10 @@ __global__ __launch_bounds__(256, 1) void bwd_cols_kernel(BwdArgs a) {
 
 template <class Pl> constexpr int fwd_lds() { return (2 + (dbl2<Pl>() ? 2 : 1)) * Dma32<Pl>::SLOT; }
 template <class Pl, bool LD> constexpr int rows_lds() { return 2 * (LD ? 1 : 2) * Dma32<Pl>::SLOT; }
-template <class Pl, bool DQ, bool LS> constexpr int cols_lds() {
+template <class Pl, bool DQ, bool LS, bool AUXS = false> constexpr int cols_lds() {
   constexpr bool NEED_K = DQ || !LS;
   constexpr bool DBL = !NEED_K || dbl2<Pl>();
-  return 2 * Dma32<Pl>::SLOT + 2 * 1024 + (NEED_K ? (DBL ? 2 : 1) * Dma32<Pl>::SLOT : 0);
+  return 2 * Dma32<Pl>::SLOT + (AUXS ? 0 : 2 * 1024) + (NEED_K ? (DBL ? 2 : 1) * Dma32<Pl>::SLOT : 0);
 }
 
 }  // namespace faw
@@ -797,7 +844,7 @@ int wide_cols(const xdot::fa::BwdArgs* a, hipStream_t st) {
   };
   auto dvp = [&](auto LSC) {
     constexpr bool LSV = decltype(LSC)::value;
-    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, LSV>), dim3(W * sv), dim3(256), (cols_lds<Pl, false, LSV>()), st, *a);
+    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, false, LSV>), dim3(W * sv), dim3(256), (cols_lds<Pl, false, LSV, aux_in_slack<DT, D, false, LSV>()>()), st, *a);
     fin(false);
   };
   auto dqp = [&](auto LSC) {
@@ -843,7 +890,7 @@ int wide_occ(int kernel, bool sbuf) {
     if (kernel == 0) return wg_per_cu(fwd_kernel<DT, D, false>, fwd_lds<Pl>());
     if (kernel == 1) return wg_per_cu(bwd_rows_kernel<DT, D, false>, rows_lds<Pl, false>());
     if (kernel == 2) return wg_per_cu(bwd_cols_kernel<DT, D, true, false>, cols_lds<Pl, true, false>());
-    return wg_per_cu(bwd_cols_kernel<DT, D, false, false>, cols_lds<Pl, false, false>());
+    return wg_per_cu(bwd_cols_kernel<DT, D, false, false>, cols_lds<Pl, false, false, aux_in_slack<DT, D, false, false>()>());
   }
   return 0;
 }
