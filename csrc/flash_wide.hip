@@ -79,6 +79,12 @@ __device__ __forceinline__ void scale_pinned(f32x16 (&x)[N], float s) {
 }
 
 // ---- operand policies ------------------------------------------------------------------------
+// operand reads ahead of the MFMAs in the one-workgroup-per-CU kernels (16-bit)
+#ifndef XDOT_WIDE_LA
+#define XDOT_WIDE_LA 2
+#endif
+constexpr int WIDE_LA = XDOT_WIDE_LA;
+
 template <int DT, int D> struct Pol {  // 16-bit
   using T = typename dt_traits<DT>::T;
   using Frag = u32x4;
@@ -98,50 +104,36 @@ template <int DT, int D> struct Pol {  // 16-bit
   // acc += image rows (lane & 31) . fragᵀ over the head dim.  Operand reads run two MFMAs ahead
   // and sched_barrier keeps them there: unfenced, the compiler hoists all D/16 reads (4 VGPRs
   // each) to the top and a wide head spills.
-  // (LA = 1: one read ahead, for a kernel whose registers are two workgroups' share)
+  // LA: operand reads in flight ahead of the MFMA that consumes them (a ring of LA + 1 fragments,
+  // compile-time indices): 1 for a kernel whose registers are two workgroups' share, more where
+  // one wave per SIMD leaves LDS latency in front of every MFMA
   template <int LA = 2>
   static __device__ __forceinline__ f32x16 rowprod(const char* img, const Frag (&f)[NF], f32x16 acc, const Lanes& L) {
-    u32x4 a0 = fa::row_frag<D>(img, 0, 0, L.L), a1 = LA > 1 ? fa::row_frag<D>(img, 0, 1, L.L) : a0;
+    constexpr int RL = LA + 1;
+    u32x4 buf[RL];
+#pragma unroll
+    for (int s = 0; s < LA && s < NF; ++s) buf[s] = fa::row_frag<D>(img, 0, s, L.L);
 #pragma unroll
     for (int s = 0; s < NF; ++s) {
-      if (LA == 1) {
-        const u32x4 cur = a0;
-        if (s + 1 < NF) a0 = fa::row_frag<D>(img, 0, s + 1, L.L);
-        acc = fa::mfma32<DT>::run(cur, f[s], acc);
-        __builtin_amdgcn_sched_barrier(0);
-        continue;
-      }
-      u32x4 a2 = a1;
-      if (s + 2 < NF) a2 = fa::row_frag<D>(img, 0, s + 2, L.L);
-      acc = fa::mfma32<DT>::run(a0, f[s], acc);
+      if (s + LA < NF) buf[(s + LA) % RL] = fa::row_frag<D>(img, 0, s + LA, L.L);
+      acc = fa::mfma32<DT>::run(buf[s % RL], f[s], acc);
       __builtin_amdgcn_sched_barrier(0);
-      a0 = a1;
-      a1 = a2;
     }
     return acc;
   }
   // out[db] += imageᵀ (d x tile row) . x (tile row x lane), x an accumulator tile
   template <int LA = 2>
   static __device__ __forceinline__ void trprod(const char* img, const f32x16& x, f32x16 (&out)[D / 32], const Lanes& L) {
-    constexpr int DB = D / 32, N = 2 * DB;
+    constexpr int DB = D / 32, N = 2 * DB, RL = LA + 1;
     const u32x4 pf[2] = {fa::acc_to_frag<DT>(x, 0), fa::acc_to_frag<DT>(x, 1)};
-    u32x4 v0 = fa::tr_frag<D>(img, 0, 0, L.L), v1 = fa::tr_frag<D>(img, 16 * (1 / DB), 32 * (1 % DB), L.L);
+    u32x4 buf[RL];
+#pragma unroll
+    for (int i = 0; i < LA && i < N; ++i) buf[i] = fa::tr_frag<D>(img, 16 * (i / DB), 32 * (i % DB), L.L);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      if (LA == 1) {
-        const u32x4 cur = v0;
-        v0 = v1;
-        if (i + 2 < N) v1 = fa::tr_frag<D>(img, 16 * ((i + 2) / DB), 32 * ((i + 2) % DB), L.L);
-        out[i % DB] = fa::mfma32<DT>::run(cur, pf[i / DB], out[i % DB]);
-        __builtin_amdgcn_sched_barrier(0);
-        continue;
-      }
-      u32x4 v2 = v1;
-      if (i + 2 < N) v2 = fa::tr_frag<D>(img, 16 * ((i + 2) / DB), 32 * ((i + 2) % DB), L.L);
-      out[i % DB] = fa::mfma32<DT>::run(v0, pf[i / DB], out[i % DB]);
+      if (i + LA < N) buf[(i + LA) % RL] = fa::tr_frag<D>(img, 16 * ((i + LA) / DB), 32 * ((i + LA) % DB), L.L);
+      out[i % DB] = fa::mfma32<DT>::run(buf[i % RL], pf[i / DB], out[i % DB]);
       __builtin_amdgcn_sched_barrier(0);
-      v0 = v1;
-      v1 = v2;
     }
   }
   // 4 consecutive outputs of one row, o[4g..4g+3] * k, to global memory
@@ -325,7 +317,7 @@ __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a)
   using DM = Dma32<Pl>;
   constexpr int DB = D / 32, SLOT = DM::SLOT;
   constexpr bool DBL = dbl2<Pl>();
-  constexpr int LA = (fwd_occ<DT, D>() == 2 && D >= 256) ? 1 : 2;  // operand reads ahead
+  constexpr int LA = fwd_occ<DT, D>() == 2 ? (D >= 256 ? 1 : 2) : WIDE_LA;  // operand reads ahead
   char* const sm = fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -421,7 +413,9 @@ __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a)
       dm.issue(vb + nx, ldb, a.T - 1 - (kt + 1) * 32, vimg(kt + 1), wave);
       wait_vm<DM::PPW>();  // Q(kt+1) landed (V(kt+1) may still fly: waited above next tile)
     } else {
+#ifndef XDOT_AB_NOWAIT  // timing-only variant (results are wrong): no wait for the next tile's DMA
       wait_vm<0>();
+#endif
     }
     raw_barrier();
   }
@@ -530,8 +524,8 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
             if (tidx(r, hf) >= valid) ds[r] = 0.f;
         }
       } else {
-        f32x16 s = Pl::rowprod(qi, kf, f32x16{}, L);          // Sᵀ  (col x row)
-        f32x16 dp = Pl::rowprod(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
+        f32x16 s = Pl::template rowprod<WIDE_LA>(qi, kf, f32x16{}, L);          // Sᵀ  (col x row)
+        f32x16 dp = Pl::template rowprod<WIDE_LA>(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
         if constexpr (SELB<DT, D, 0>()) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[r] = __builtin_fmaf(s[r], c2, -lse2);  // in place
@@ -557,10 +551,12 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
           }
         }
       }
-      Pl::trprod(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
+      Pl::template trprod<WIDE_LA>(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
     }
     pin_agpr(dk);
+#ifndef XDOT_AB_NOWAIT
     wait_vm<0>();
+#endif
     raw_barrier();
   }
   if (!row_ok) return;
@@ -602,7 +598,7 @@ __global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_ker
   // the image used second in the tile (K for dQ) is single-buffered when two per stage do not fit
   constexpr bool DBL = !(NEED_K && NEED_DO) || dbl2<Pl>();
   constexpr int AUX = 1024;  // lse2[32], δ[32] at the start of a 1-KiB slot
-  constexpr int CLA = cols_occ<DT, D, DQ, LS>() == 2 ? 1 : 2;  // operand reads ahead
+  constexpr int CLA = cols_occ<DT, D, DQ, LS>() == 2 ? 1 : WIDE_LA;  // operand reads ahead
   char* const sm = fa::smem;
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -692,7 +688,7 @@ __global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_ker
     f32x16 dp;
     if (flag != 1) {
       if constexpr (!LS) s = Pl::template rowprod<CLA>(kimg(rt), qf, f32x16{}, L);  // S (row x col)
-      if constexpr (DQ) dp = Pl::rowprod(doimg(rt), vf, f32x16{}, L);  // dP (row x col)
+      if constexpr (DQ) dp = Pl::template rowprod<CLA>(doimg(rt), vf, f32x16{}, L);  // dP (row x col)
       pin_frags();
       if constexpr (SELB<DT, D, DQ ? 2 : 1>()) {
         const int vr = a.R - rt * 32;  // valid rows of this tile
@@ -732,16 +728,20 @@ __global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_ker
         wait_vm<0>();
         raw_barrier();
       }
-      if (flag != 1) Pl::trprod(kimg(rt), dp, acc, L);  // dQᵀ += Kᵀ · dS
+      if (flag != 1) Pl::template trprod<CLA>(kimg(rt), dp, acc, L);  // dQᵀ += Kᵀ · dS
       if (!DBL && more) {
         raw_barrier();
         issue_k(rt + 1);
         wait_vm<DM::PPW>();
       } else {
+#ifndef XDOT_AB_NOWAIT
         wait_vm<0>();
+#endif
       }
     } else {
+#ifndef XDOT_AB_NOWAIT
       wait_vm<0>();
+#endif
     }
     pin_agpr(acc);
     raw_barrier();
