@@ -23,7 +23,7 @@ def hip_dtype_ok(*ts: torch.Tensor) -> bool:
 
 def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0, sA2=0,
                  sB1=0, sB2=0, sC1=0, sC2=0, sAseg=0, sBseg=0, a_mc=False, b_mc=False,
-                 alpha=1.0, beta=0.0, path=0) -> None:
+                 alpha=1.0, beta=0.0, path=0, split_ok=True) -> None:
     """C[z1, z2](m, n) = alpha * sum_s sum_k opA(m, k) * opB(k, n) + beta * C[z1, z2](m, n)
     (csrc/gemm.hip; 16-bit operands with large outputs run the 256x256 csrc/gemm2.hip).
 
@@ -32,8 +32,9 @@ def strided_gemm(A, B, C, *, M, N, K, nseg=1, nb1=1, nb2=1, lda, ldb, ldc, sA1=0
     where it takes the call, else the 256x256 one -- whenever the layout rules hold; 6 = automatic
     with the split-fp32 route allowed (what path 0 becomes for fp32 operands under
     ``XDOT_FP32_MODE=split``; the default ``exact`` keeps fp32 products on the exact fp32 MFMA kernel).
-    ``FLAGS.fp32_mode`` is read here on every call: the one source of truth for the GEMMs too."""
-    if path == 0 and A.dtype == torch.float32 and FLAGS.fp32_mode == "split":
+    ``FLAGS.fp32_mode`` is read here on every call: the one source of truth for the GEMMs too.
+    ``split_ok=False`` keeps an fp32 call on the exact kernels under either mode."""
+    if path == 0 and split_ok and A.dtype == torch.float32 and FLAGS.fp32_mode == "split":
         path = 6
     _ext.ops().gemm(A, B, C, int(M), int(N), int(K), int(nseg), int(nb1), int(nb2), int(lda),
                     int(ldb), int(ldc), int(sA1), int(sA2), int(sB1), int(sB2), int(sC1), int(sC2),

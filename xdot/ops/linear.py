@@ -55,10 +55,13 @@ def _proj_ok(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
 
 
 def _f32_ok(*ts) -> bool:
-    """Exact-fp32 products of a projection on csrc/gemm_f32.hip (through xdot.gemm): fp32 GPU
-    tensors, ``XDOT_FP32_MODE=exact``, ``XDOT_F32_PROJ`` on (the library's fp32 GEMM otherwise)."""
+    """Exact-fp32 products of a projection on the exact-fp32 GEMM kernels (through xdot.gemm with
+    split_ok off): fp32 GPU tensors, ``XDOT_F32_PROJ`` on (the library's fp32 GEMM otherwise).
+    Under ``XDOT_FP32_MODE=split`` too: only the attention products take the split-bf16 route there
+    (the library's fp32 projections cost the split step 4.3 ms against 2.6 on these kernels,
+    profiles/r5_fp32.md), the projections stay exact."""
     return (FLAGS.f32_proj and all(t is None or (t.dtype == torch.float32 and t.is_cuda) for t in ts)
-            and FLAGS.fp32_mode == "exact" and _ext.use_hip(*[t for t in ts if t is not None]))
+            and FLAGS.fp32_mode in ("exact", "split") and _ext.use_hip(*[t for t in ts if t is not None]))
 
 
 def _force() -> int:
@@ -85,7 +88,7 @@ def proj(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = N
         if bias is not None:
             y.copy_(bias.expand(M, N))  # C = alpha * x Wᵀ + alpha * bias
         strided_gemm(x2, w, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=y.stride(0), alpha=alpha,
-                     beta=alpha if bias is not None else 0.0)
+                     beta=alpha if bias is not None else 0.0, split_ok=False)
         return y if out is not None else y.view(*x.shape[:-1], N)
     if out is None:
         y = F.linear(x, weight, bias)
@@ -105,7 +108,7 @@ def proj_dx(dy: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
         dy, w = dy.contiguous(), weight.contiguous()
         M, K, N = dy.shape[0], dy.shape[1], w.shape[1]
         out = torch.empty(M, N, dtype=dy.dtype, device=dy.device)
-        strided_gemm(dy, w, out, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, b_mc=True)
+        strided_gemm(dy, w, out, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, b_mc=True, split_ok=False)
         return out
     return dy @ weight
 
@@ -131,7 +134,7 @@ def weight_grad(dy: torch.Tensor, x: torch.Tensor, out_dtype: Optional[torch.dty
         # exact fp32 on csrc/gemm_f32.hip; the long K (= rows) runs as K slabs + one ordered sum
         dy, x = dy.contiguous(), x.contiguous()
         out = torch.empty(M, N, dtype=torch.float32, device=dy.device)
-        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True)
+        strided_gemm(dy, x, out, M=M, N=N, K=K, lda=M, ldb=N, ldc=N, a_mc=True, b_mc=True, split_ok=False)
         return out
     if not native_wgrad(dy, x):
         ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else torch.promote_types(dy.dtype, x.dtype)

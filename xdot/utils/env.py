@@ -69,7 +69,7 @@ variable                    default   effect
 ``XDOT_WGRAD_PAIR``         1         the fused backward's dWk and dW[q|v] in one launch (A/B knob)
 ``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
                                       launcher's occupancy model; A/B knob)
-``XDOT_F32_PROJ``           1         exact-fp32 projections / weight gradients on csrc/gemm_f32.hip
+``XDOT_F32_PROJ``           1         exact-fp32 projections / weight gradients on the exact-fp32 GEMM kernels (both fp32 modes)
                                       (0: the library's fp32 GEMM)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
                                       (1: where it beats the library, i.e. below 16384 rows;
