@@ -246,12 +246,33 @@ template <class Pl> struct Dma32 {
       pk[i / 2] |= (uint32_t)(r | ((16 * c) << 5)) << (16 * (i & 1));
     }
   }
+  template <int F>
+  static __device__ __forceinline__ void runs(const char* base, const uint32_t (&o)[PPW], uint32_t lds) {
+    constexpr int N = PPW - F < 5 ? PPW - F : 5;
+    if constexpr (N > 0) {
+      fa::GldsRun<N>::run(base, o + F, lds + F * 1024);
+      runs<F + N>(base, o, lds);
+    }
+  }
   // tile rows past rmax (past T / R) re-read row rmax: callers mask them; padding chunks and the
   // slack rows past 32 load a valid dummy address.
   // SKIP: pieces wholly past the image are not loaded (their LDS stays free for other data; the
   // waves then issue different counts, so only callers that drain with vmcnt(0) may use it)
   template <bool SKIP = false>
   __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int) const {
+#ifdef XDOT_WIDE_RUN  // opt-in: runs measured 1-2 % slower here (r5s55), unlike the narrow kernels
+    if constexpr (!SKIP) {  // the wave's PPW consecutive pieces as runs of <= 5 DMAs (one M0 setup each)
+      uint32_t o[PPW];
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const uint32_t r = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1), 5);
+        const uint32_t c16 = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1) + 5, 11);
+        o[i] = (uint32_t)min((int)r, rmax) * (uint32_t)stride_bytes + c16;
+      }
+      runs<0>(base, o, fa::lds_addr(img + wave * PPW * 1024));
+      return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       // (SKIP: the piece index through readfirstlane keeps the LDS address an SGPR operand)
