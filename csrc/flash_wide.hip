@@ -470,8 +470,18 @@ __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a)
 // backward, row side: dK = scale · Σ_cols dS · Q_cols.  4 waves x 32 rows, column split.
 // LD: dS from the score buffer (one product per tile, Q image only); else S and dP are
 // recomputed from register-resident K / dO fragments (stage [Q image][V image]).
+// 16-bit D = 160 row side (recomputed S): K / dO fragments + dK accumulators fit two waves'
+// share of the registers (operand reads one ahead); its four images fit LDS twice.  D = 160 h = 4
+// row side 2.63 -> 2.29 ms (r5s56)
+template <int DT, int D, bool LD> constexpr int rows_occ() {
+#ifdef XDOT_WIDE_ROWS_OCC1
+  return 1;
+#else
+  return (DT != DT_F32 && D <= 160 && !LD) ? 2 : 1;  // D = 192 would spill 84 registers
+#endif
+}
 template <int DT, int D, bool LD>
-__global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, (rows_occ<DT, D, LD>())) void bwd_rows_kernel(BwdArgs a) {
   using Pl = Pol<DT, D>;
   using T = typename Pl::T;
   using DM = Dma32<Pl>;
@@ -545,8 +555,9 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
             if (tidx(r, hf) >= valid) ds[r] = 0.f;
         }
       } else {
-        f32x16 s = Pl::template rowprod<WIDE_LA>(qi, kf, f32x16{}, L);          // Sᵀ  (col x row)
-        f32x16 dp = Pl::template rowprod<WIDE_LA>(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
+        constexpr int RLA = rows_occ<DT, D, LD>() == 2 ? 1 : WIDE_LA;
+        f32x16 s = Pl::template rowprod<RLA>(qi, kf, f32x16{}, L);          // Sᵀ  (col x row)
+        f32x16 dp = Pl::template rowprod<RLA>(qi + SLOT, df, f32x16{}, L);  // dPᵀ (col x row)
         if constexpr (SELB<DT, D, 0>()) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[r] = __builtin_fmaf(s[r], c2, -lse2);  // in place
@@ -572,7 +583,7 @@ __global__ __launch_bounds__(256, 1) void bwd_rows_kernel(BwdArgs a) {
           }
         }
       }
-      Pl::template trprod<WIDE_LA>(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
+      Pl::template trprod<(rows_occ<DT, D, LD>() == 2 ? 1 : WIDE_LA)>(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
     }
     pin_agpr(dk);
 #ifndef XDOT_AB_NOWAIT
