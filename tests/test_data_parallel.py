@@ -223,6 +223,39 @@ def _fused_frozen_body(rank, ws):
             torch.testing.assert_close(p2.grad, p1.grad, rtol=1e-10, atol=1e-12, msg=n2)
 
 
+def _fused_no_sync_body(rank, ws):
+    """Gradient accumulation with the fused module node: micro-batch 1 under no_sync(), micro-batch
+    2 outside it, for two steps.  The muted backward must not mark its delivered gradients, so the
+    last backward's are counted and the buckets launch (deliver() under _muted)."""
+    import xdot
+    from xdot.parallel import GradSync, allreduce_gradients, broadcast_parameters
+
+    torch.manual_seed(rank)
+    m1 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    broadcast_parameters(m1)
+    m2 = xdot.DistributedDotProductAttn(32, num_heads=4, add_bias=True, impl="flash").double()
+    m2.load_state_dict(m1.state_dict())
+    sync = GradSync(m2, bucket_mb=0.0001)
+    g = torch.Generator().manual_seed(13 + rank)
+    for step in range(2):
+        xs = [torch.rand(1, 6, 32, generator=g, dtype=torch.float64) for _ in range(2)]
+        for p in list(m1.parameters()) + list(m2.parameters()):
+            p.grad = None
+        for x in xs:
+            m1(x, x, x, None).square().sum().backward()
+        allreduce_gradients(m1)
+        with sync.no_sync():
+            m2(xs[0], xs[0], xs[0], None).square().sum().backward()
+        m2(xs[1], xs[1], xs[1], None).square().sum().backward()
+        sync.wait()
+        for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            torch.testing.assert_close(p2.grad, p1.grad, rtol=1e-10, atol=1e-12, msg=f"step {step} {n2}")
+
+
+def test_gradsync_fused_module_no_sync_accumulation():
+    run_gloo(_fused_no_sync_body, 2)
+
+
 def test_gradsync_fused_module_called_twice():
     run_gloo(_fused_twice_body, 2)
 

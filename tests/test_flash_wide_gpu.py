@@ -255,3 +255,57 @@ def test_flash_wide_row_splits(gpu, monkeypatch, dtype):
             assert torch.isfinite(b).all()
             assert _rel(b, a) <= tol, f"splits {sp}: {_rel(b, a):.2e}"
         _check(case, inputs, got, 2e-6 if dtype == torch.float32 else 2e-2)
+
+
+def _fp32_wide_module(gpu):
+    import xdot
+
+    torch.manual_seed(3)
+    m = xdot.DistributedDotProductAttn(768, num_heads=2, impl="flash", distributed=False).to(gpu)
+    x = torch.randn(1, 160, 768, device=gpu)
+    mask = torch.rand(1, 160, 160, device=gpu) < 0.3
+    mask[..., -1] = False
+    return m, x, mask
+
+
+def test_fp32_wide_retain_graph_twice(gpu):
+    """Exact fp32 D = 384 (the reference example's heads), backward twice through a retained graph:
+    with the separate dS buffer (default) S is intact, so the second pass gives the same gradients
+    again (the first backward used to drop the buffer and the second failed)."""
+    m, x, mask = _fp32_wide_module(gpu)
+    loss = m(x, x, x, mask).square().mean()
+    loss.backward(retain_graph=True)
+    g1 = [p.grad.clone() for p in m.parameters()]
+    loss.backward()
+    for p, a in zip(m.parameters(), g1):
+        torch.testing.assert_close(p.grad, 2 * a, rtol=1e-5, atol=1e-9)
+
+
+def test_fp32_wide_retain_graph_in_place_raises(gpu, monkeypatch):
+    """In the in-place score-buffer mode (no dS buffer) the first backward overwrites S; a second
+    backward at fp32 D = 384 (no recompute kernel) must fail with a clear error, not a launch code."""
+    from xdot.utils.env import FLAGS
+
+    monkeypatch.setattr(FLAGS, "fp32_scores_dsbuf", False)
+    m, x, mask = _fp32_wide_module(gpu)
+    loss = m(x, x, x, mask).square().mean()
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="retained graph"):
+        loss.backward()
+
+
+def test_fp32_no_grad_forward_takes_no_score_buffer(gpu, monkeypatch):
+    """no_grad / inference forwards never allocate the fp32 score buffers, and the
+    wide exact-fp32 forward then runs the non-storing kernel (same output as with the buffer)."""
+    from xdot.ops import flash
+
+    calls = []
+    orig = flash.score_buffers
+    monkeypatch.setattr(flash, "score_buffers", lambda *a, **k: calls.append(a) or orig(*a, **k))
+    m, x, mask = _fp32_wide_module(gpu)
+    with torch.no_grad():
+        y0 = m(x, x, x, mask)
+    assert calls == []
+    y1 = m(x, x, x, mask)
+    assert len(calls) == 1
+    torch.testing.assert_close(y0, y1.detach(), rtol=1e-6, atol=1e-7)

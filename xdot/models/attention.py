@@ -215,7 +215,7 @@ class DistributedDotProductAttn(nn.Module):
                     sync = (gs, id(self))
                 return AttnBlockFn.apply(keys, queries, attn_mask, self.keys.weight, self.keys.bias, wq, bq, wv, bv,
                                          self.composition.weight, self.composition.bias, self.num_heads, scale, comm,
-                                         self.chunk_plan, sync)
+                                         self.chunk_plan, sync, torch.is_grad_enabled())
             # gathered side first: its all-gather runs while the row-side GEMM computes
             qv = self._project_qv(queries, values)
             pending = start_gather(qv, comm, chunks=self.chunk_plan)

@@ -74,7 +74,8 @@ def _ready_on(t, side):
 class AttnBlockFn(torch.autograd.Function):
     @staticmethod
     @_ext.pinned
-    def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan, sync=None):
+    def forward(ctx, xk, xqv, mask, wk, bk, wq, bq, wv, bv, wc, bc, H, scale, comm, chunk_plan, sync=None,
+                grad_on=True):
         wqv = _rows(wq, wv)
         bqv = _rows(bq, bv) if bq is not None else None
         n = comm.world_size
@@ -96,7 +97,8 @@ class AttnBlockFn(torch.autograd.Function):
         pre = xk.shape[-1] == wk.shape[1] and prescale_wanted(qv[..., :wk.shape[0]], qv, H)
         k = proj(xk, wk, bk, alpha=scale * _LOG2E if pre else 1.0)
         actx = _Ctx()
-        o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending, pre)  # k_prescaled
+        actx.needs_input_grad = (any(ctx.needs_input_grad),) * 2  # a backward can run (score buffers)
+        o = SeqParallelAttention.forward(actx, k, qv, mask, H, scale, comm, pending, pre, grad_on)  # k_prescaled
         out = proj(o, wc, bc)
         ctx.actx = actx
         ctx.sync = sync  # (GradSync, module key) or None
@@ -175,4 +177,7 @@ class AttnBlockFn(torch.autograd.Function):
             for t in (dwc, dbc, dwk, dbk) + tuple(p.grad for p in ctx.params if p is not None and sync is not None):
                 if t is not None:
                     t.record_stream(cur)
-        return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None, None)
+        # the attention's tensors were only borrowed from ctx.saved_tensors (rebuilt from there by
+        # every backward): do not keep them alive through the node after this backward
+        ctx.actx._saved = None
+        return (dxk, dxqv, None, dwk, dbk, dwq, dbq, dwv, dbv, dwc, dbc, None, None, None, None, None, None)

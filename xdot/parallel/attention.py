@@ -467,9 +467,10 @@ class SeqParallelAttention(torch.autograd.Function):
 
     @staticmethod
     @_ext.pinned
-    def forward(ctx, k, qv, mask, H, scale, comm, pending=None, k_prescaled=False):
+    def forward(ctx, k, qv, mask, H, scale, comm, pending=None, k_prescaled=False, grad_on=True):
         """``k_prescaled``: ``k`` already holds ``rows * scale * log2 e`` (:func:`prescale_wanted`;
-        the fused module folds it into the k projection's epilogue)."""
+        the fused module folds it into the k projection's epilogue).  ``grad_on``: grad mode at the
+        call (inside ``forward`` it is always off, and ``needs_input_grad`` ignores it)."""
         check_consistent(comm, "seq_parallel_attention", k, qv, H)
         C = k.shape[-1]
         B, R = k.shape[0], k.shape[1]
@@ -499,7 +500,11 @@ class SeqParallelAttention(torch.autograd.Function):
         mask = getattr(mask, "raw", mask)
         segmented = n > 1 and (FLAGS.local_first or len(chunks) > 1)
         sbuf = dsbuf = None
-        if use_hip and k.dtype == torch.float32 and (len(chunks) == 1 or B == 1):
+        # a backward can run on this forward (grad mode is off inside Function.forward: autograd's
+        # needs_input_grad, or the fused node's, says it); without one no score buffer is taken
+        # (no 20 GB allocation and store pass for inference / no_grad forwards)
+        need_bwd = bool(grad_on) and any(getattr(ctx, "needs_input_grad", (True,))[:2])
+        if use_hip and k.dtype == torch.float32 and need_bwd and (len(chunks) == 1 or B == 1):
             # fp32 (exact or split): score buffer (flash.score_buffer) when it fits: the backward
             # then reads S / dS instead of recomputing them.  One kernel over the whole gathered
             # side (in fp32 the own-block-first segmentation hides < 5 % of a rank's forward)
@@ -512,14 +517,14 @@ class SeqParallelAttention(torch.autograd.Function):
                 if sbs is not None:
                     sbuf, dsbuf = sbs
                     segmented = False
-        if use_hip and k.dtype == torch.float32 and D > WIDE_F32_NEEDS_SCORES and sbuf is None:
-            # no kernel recomputes an fp32 head this wide (three D-wide register sets): the torch path
-            import warnings
-
-            warnings.warn(f"xdot: exact fp32 head dim {D} needs the flash score buffer, which does not fit; "
-                          "running the torch attention path", RuntimeWarning)
-            use_hip = False
-            fm = 0
+        if use_hip and k.dtype == torch.float32 and D > WIDE_F32_NEEDS_SCORES and sbuf is None and need_bwd:
+            # no kernel recomputes an fp32 head this wide (three D-wide register sets) and the torch
+            # path would materialise a score matrix larger than the buffer that did not fit
+            raise RuntimeError(
+                f"xdot: training exact-fp32 attention at head dim {D} needs the flash score buffer "
+                f"({4 * flash.score_buffer_numel(B, H, R, n * qv.shape[1]) / 2**30:.1f} GiB), which does not fit "
+                f"within XDOT_FP32_SCORES_FRAC={FLAGS.fp32_scores_frac} of the free device memory: shorten the "
+                "sequence, raise XDOT_FP32_SCORES_FRAC, or run the module in bf16")
         if not segmented:
             if use_hip:
                 if len(chunks) > 1:  # several gather chunks, one buffer in (chunk, rank, row) order
@@ -540,16 +545,25 @@ class SeqParallelAttention(torch.autograd.Function):
         else:
             o, lse, bufs = _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescaled, fm)
             mks = [packed_full] if packed_full is not None else None  # backward packs its own (cached)
-        ctx.save_for_backward(k, o, lse, *bufs)
+        # the score buffers travel as saved tensors: autograd frees them after the backward unless
+        # the graph is retained (a ctx attribute would keep 20-40 GB alive as long as the graph is
+        # referenced, e.g. through the previous step's loss)
+        sbt = tuple(t for t in (sbuf, dsbuf) if t is not None)
+        ctx.save_for_backward(k, o, lse, *bufs, *sbt)
         ctx.mks, ctx.mask, ctx.chunks, ctx.H, ctx.scale, ctx.comm, ctx.use_hip = mks, mask, chunks, H, scale, comm, use_hip
         ctx.prescaled, ctx.fp32_mode = prescaled, fm
-        ctx.sbuf = (sbuf, dsbuf)  # consumed by the first backward (in place: S overwritten with dS)
+        # (has S buffer, has dS buffer); the in-place mode (S only) is consumed by the first backward
+        ctx.sb_kind = (sbuf is not None, dsbuf is not None)
         return o
 
     @staticmethod
     @_ext.pinned
     def backward(ctx, do):
         k, o, lse, *bufs = ctx.saved_tensors
+        has_s, has_ds = getattr(ctx, "sb_kind", (False, False))
+        nsb = int(has_s) + int(has_ds)
+        sbt = bufs[len(bufs) - nsb:] if nsb else []
+        bufs = bufs[:len(bufs) - nsb]
         comm, H, scale, chunks = ctx.comm, ctx.H, ctx.scale, ctx.chunks
         n = comm.world_size
         C = k.shape[-1]
@@ -590,10 +604,22 @@ class SeqParallelAttention(torch.autograd.Function):
             hi.wait_stream(cur)
             handles, outs = [], []
             gdt = k.dtype if not FLAGS.grad_fp32 else torch.float32
-            # score buffer: S -> dS in the column kernel, then dK from dS; a second backward through
-            # a retained graph recomputes (the buffer no longer holds S)
-            sbuf, dsbuf = getattr(ctx, "sbuf", None) or (None, None)
-            ctx.sbuf = None
+            # score buffer: S -> dS in the column kernel, then dK from dS.  With a separate dS buffer
+            # S stays intact, so a second backward through a retained graph reads it again; in place
+            # (S overwritten with dS) the first backward consumes it and a second one recomputes
+            sbuf = sbt[0] if has_s else None
+            dsbuf = sbt[-1] if has_ds else None
+            if has_s and not has_ds:
+                if getattr(ctx, "sb_used", False):
+                    sbuf = None
+                ctx.sb_used = True
+            if (sbuf is None and k.dtype == torch.float32 and C // H > WIDE_F32_NEEDS_SCORES
+                    and ctx.fp32_mode == 0):
+                raise RuntimeError(
+                    f"xdot: a second backward through a retained graph of exact-fp32 attention at head dim "
+                    f"{C // H} needs the scores, which the first backward overwrote in place (no kernel "
+                    "recomputes an fp32 head this wide); set XDOT_FP32_SCORES_DS=1 with room for the "
+                    "separate dS buffer, or do not retain the graph")
             ev_cols = None
             with _on_stream(hi, cur):
                 delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
@@ -693,7 +719,7 @@ class SeqParallelAttention(torch.autograd.Function):
         for h in handles:
             if h is not None:
                 h.wait()
-        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None
+        return dk.to(k.dtype), dqv.to(k.dtype), None, None, None, None, None, None, None
 
 
 def gather_plan(qv_shape, qv: Tensor, comm: _comm.Communicator, chunks: Optional[int] = None):
@@ -732,7 +758,8 @@ def seq_parallel_attention_packed(k: Tensor, qv: Tensor, mask: Optional[Tensor],
             raise ValueError(f"mask must be (B, R, T)=({k.shape[0]}, {k.shape[1]}, {T}), got {tuple(mask.shape)}")
         if isinstance(mask, torch.Tensor):
             mask = mask.to(torch.bool)
-    return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm, pending)
+    return SeqParallelAttention.apply(k, qv, mask, num_heads, float(scale), comm, pending, False,
+                                      torch.is_grad_enabled())
 
 
 def seq_parallel_attention(k: Tensor, q: Tensor, v: Tensor, mask: Optional[Tensor], num_heads: int,

@@ -174,7 +174,11 @@ class GradSync:
             self._muted = prev
 
     def note_use(self, key) -> None:
-        """A fused node's forward (``key``: its module) ran with gradients enabled."""
+        """A fused node's forward (``key``: its module) ran with gradients enabled.  Forwards
+        under :meth:`no_sync` are not counted: their backward runs muted and goes through
+        AccumulateGrad, so only the forwards whose gradients are reduced decide :meth:`sole_use`."""
+        if self._muted:
+            return
         self._uses[key] = self._uses.get(key, 0) + 1
 
     def sole_use(self, key) -> bool:
@@ -198,6 +202,8 @@ class GradSync:
                     p.grad = g.detach()
                 else:
                     p.grad.add_(g)
+            if self._muted:  # no_sync(): accumulated only; NOT marked delivered, so the gradient of
+                return       # a later unmuted backward through AccumulateGrad is still counted
             for p, g in pairs:
                 if g is not None and id(p) in self._index:  # (a parameter outside the buckets is
                     self._dlv.add(id(p))                   # accumulated, never reduced here)
