@@ -252,12 +252,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_rows_kernel(BwdArgs a) {
         pipe_body(qs, vs, sseed, false, 0ull);
       }
     }
-#ifdef XDOT_AB_NOWAIT  // timing-only variant (results are wrong): no wait for in-flight tiles
-    if (kt + PF >= kt_end) wait_vm<0>();
-#else
     if (kt + PF < kt_end) wait_vm<NG * (PF - 1)>();
     else wait_vm<0>();
-#endif
     raw_barrier();
   };
 

@@ -257,11 +257,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_cols2_kernel(BwdArgs a) {
       flag = __builtin_amdgcn_readfirstlane((f0 == 1 && f1 == 1) ? 1 : ((f0 == 0 && (f1 == 0 || 2 * rt + 1 >= NRB32)) ? 0 : 2));
     }
     if (flag != 1 && c0 < a.T) body(ks, ds, ls, dls, ws, flag == 2);
-#ifdef XDOT_AB_NOWAIT  // timing-only variant (results are wrong): no wait for the next tile
-    if (rt + 1 >= rt_end) wait_vm<0>();
-#else
     wait_vm<0>();  // tile rt+1 landed (the only DMAs in flight)
-#endif
     raw_barrier();
   };
   for (int rt = rt_beg; rt < rt_end; rt += 2) {

@@ -230,15 +230,13 @@ __device__ __forceinline__ int flag_at(const uint8_t* flags, int b, int NRB32, i
   return (int)((w >> (8 * (idx & 3))) & 0xffu);
 }
 
-// Deep prefetch of a strided stream of score blocks (score-buffer kernels): XDOT_SB_PF blocks in
+// Deep prefetch of a strided stream of score blocks (score-buffer kernels): SB_PF blocks in
 // flight per wave in a register ring.  The loop is unrolled by the ring depth so that each step's
 // slot is a compile-time index: no in-flight register is ever copied (a copy would wait for its
 // load).  body(i, J) handles stream element i from slot J::value, then refills that slot with
 // element i + PF.  One 4-KiB block per tile is too little to cover HBM latency when the tile's
 // products are short (the dV and dK passes: one product per tile).
-#ifndef XDOT_SB_PF
-#define XDOT_SB_PF 1  // 1 / 2 / 3 measured equal (profiles/r5_fp32.md): no ring copies at 1
-#endif
+constexpr int SB_PF = 1;  // depths 1 / 2 / 3 measured equal (profiles/r5_fp32.md): no ring copies at 1
 template <int N> struct Ic { static constexpr int value = N; };
 template <int PF, class F> __device__ __forceinline__ void ring_loop(int beg, int end, F&& body) {
   static_assert(PF >= 1 && PF <= 4, "ring depth");

@@ -136,18 +136,10 @@ __device__ __forceinline__ void load_frag(float (&f)[D / 2], const float* p, boo
 
 // acc += img rows (lane&31) · fragᵀ over the head dim (A from the image, B from registers).
 // The image reads run one 4-MFMA group ahead, fenced by sched_barrier: with one wave per SIMD a
-// read issued right before its MFMAs exposes the whole LDS latency (XDOT_F32_NOPIPE: unfenced).
+// read issued right before its MFMAs exposes the whole LDS latency.
 template <int D>
 __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D / 2], f32x16 acc, int lane) {
   const float* p = img + (lane & 31) * Cfg<D>::P + 4 * (lane >> 5);
-#ifdef XDOT_F32_NOPIPE
-#pragma unroll
-  for (int g = 0; g < D / 8; ++g) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(p + 8 * g);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc = mm(a[t], f[4 * g + t], acc);
-  }
-#else
   f32x4 a0 = *reinterpret_cast<const f32x4*>(p);
 #pragma unroll
   for (int g = 0; g < D / 8; ++g) {
@@ -158,7 +150,6 @@ __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D /
     __builtin_amdgcn_sched_barrier(0);
     a0 = a1;
   }
-#endif
   return acc;
 }
 
@@ -171,14 +162,6 @@ template <int D>
 __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16 (&out)[D / 32], int lane) {
   const int hf = lane >> 5;
   constexpr int DB = D / 32;
-#ifdef XDOT_F32_NOPIPE
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const float* row = img + ((s & 3) + 8 * (s >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
-#pragma unroll
-    for (int db = 0; db < DB; ++db) out[db] = mm(row[db * 32], x[s], out[db]);
-  }
-#else
   // ring of PD + 1 operand sets: tile index s + PD is read while the MFMAs of s issue (the loop
   // is fully unrolled, so every ring slot is a compile-time register set)
   constexpr int PD = XDOT_F32_TRPD;
@@ -197,7 +180,6 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
     for (int db = 0; db < DB; ++db) out[db] = mm(rr[s % (PD + 1)][db], x[s], out[db]);
     __builtin_amdgcn_sched_barrier(0);
   }
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -658,7 +640,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
 
-  constexpr int PF = XDOT_SB_PF;
+  constexpr int PF = fa::SB_PF;
   DmaStager<D, 1> dm;
   dm.init(wave, lane, (int)(a.ldkv * 4));
   f32x16 q[PF];
@@ -739,7 +721,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     const int rr = rt * 32 + tid;
     return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
   };
-  constexpr int PF = XDOT_SB_PF;
+  constexpr int PF = fa::SB_PF;
   DmaStager<D, 1> dm;
   dm.init(wave, lane, C * 4);
   f32x16 q[PF];

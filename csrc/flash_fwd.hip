@@ -316,13 +316,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         for (int r = 0; r < 16; ++r) sn[tt][r] = NEG_INF;
     }
     // Q(kt+2) and V(kt+1) (issued one iteration ago) complete; this iteration's DMAs fly on
-#ifdef XDOT_AB_NOWAIT  // timing-only variant (results are wrong): no wait for in-flight tiles
-    if (!dq && !dv) wait_vm<0>();
-#else
     if (dq) wait_vm<NQ + NV>();
     else if (dv) wait_vm<NV>();
     else wait_vm<0>();
-#endif
     raw_barrier();
   };
 

@@ -246,50 +246,20 @@ template <class Pl> struct Dma32 {
       pk[i / 2] |= (uint32_t)(r | ((16 * c) << 5)) << (16 * (i & 1));
     }
   }
-  template <int F>
-  static __device__ __forceinline__ void runs(const char* base, const uint32_t (&o)[PPW], uint32_t lds) {
-    constexpr int N = PPW - F < 5 ? PPW - F : 5;
-    if constexpr (N > 0) {
-      fa::GldsRun<N>::run(base, o + F, lds + F * 1024);
-      runs<F + N>(base, o, lds);
-    }
-  }
   // tile rows past rmax (past T / R) re-read row rmax: callers mask them; padding chunks and the
   // slack rows past 32 load a valid dummy address.
   // SKIP: pieces wholly past the image are not loaded (their LDS stays free for other data; the
   // waves then issue different counts, so only callers that drain with vmcnt(0) may use it)
   template <bool SKIP = false>
   __device__ __forceinline__ void issue(const char* base, int stride_bytes, int rmax, char* img, int) const {
-#ifdef XDOT_WIDE_RUN  // opt-in: runs measured 1-2 % slower here (r5s55), unlike the narrow kernels
-    if constexpr (!SKIP) {  // the wave's PPW consecutive pieces as runs of <= 5 DMAs (one M0 setup each)
-      uint32_t o[PPW];
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) {
-        const uint32_t r = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1), 5);
-        const uint32_t c16 = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1) + 5, 11);
-        o[i] = (uint32_t)min((int)r, rmax) * (uint32_t)stride_bytes + c16;
-      }
-      runs<0>(base, o, fa::lds_addr(img + wave * PPW * 1024));
-      return;
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       // (SKIP: the piece index through readfirstlane keeps the LDS address an SGPR operand)
       const int pc = SKIP ? __builtin_amdgcn_readfirstlane(wave * PPW + i) : wave * PPW + i;
       if (SKIP && pc * 1024 >= BYTES) continue;  // wave-uniform
-#ifdef XDOT_WIDE_NOPK  // A/B: recompute the piece's row / chunk at every issue
-      const int p = pc * 1024 + lane * 16;
-      const int r = min(p / Pl::ROW, 31);
-      int c = (p % Pl::ROW) >> 4;
-      if (Pl::SWZ) c ^= (r >> 2) & 3;
-      if (c >= Pl::VALID || p >= BYTES) c = 0;
-      fa::glds16(base, (uint32_t)(min(r, rmax) * stride_bytes + c * 16), img + pc * 1024);
-#else
       const uint32_t r = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1), 5);
       const uint32_t c16 = __builtin_amdgcn_ubfe(pk[i / 2], 16 * (i & 1) + 5, 11);
       fa::glds16(base, (uint32_t)min((int)r, rmax) * (uint32_t)stride_bytes + c16, img + pc * 1024);
-#endif
     }
   }
 };
@@ -305,31 +275,19 @@ template <class Pl> constexpr bool dbl2() { return 4 * Dma32<Pl>::SLOT + 1024 <=
 // profiles/r5_wide_long.md).  K: 0 row side, 1 dV pass, 2 dQ pass.  The instantiations whose
 // registers this would spill (two D-wide sets and D = 384 / fp32 D = 256) keep the per-score form.
 template <int DT, int D, int K> constexpr bool SELB() {
-#ifdef XDOT_WIDE_NOSELB
-  return false;
-#else
   return K == 1 || !(D == 384 || (DT == DT_F32 && D == 256));
-#endif
 }
 // The 16-bit D = 256 dV pass at two workgroups per CU: 128 accumulator AGPRs + the Q fragment
 // in 128 VGPRs (operand reads one ahead), and its four 20-KiB images fill 80 KiB exactly, so the
 // lse2 / δ rows move into the dO slots' 2 KiB of slack (aux_in_slack)
 template <int DT, int D, bool DQ, bool LS> constexpr int cols_occ() {
-#ifdef XDOT_WIDE_COLS_OCC1
-  return 1;
-#else
   return (DT != DT_F32 && D == 256 && !DQ && !LS) ? 2 : 1;
-#endif
 }
 template <int DT, int D, bool DQ, bool LS> constexpr bool aux_in_slack() { return cols_occ<DT, D, DQ, LS>() == 2; }
 // 16-bit D <= 256: 128 accumulator AGPRs + the K fragment fit 256 registers, so two workgroups
 // share a CU and one wave's softmax VALU runs beside the other's MFMAs (LDS: 2 x 80 KB at D = 256)
 template <int DT, int D> constexpr int fwd_occ() {
-#ifdef XDOT_WIDE_OCC1
-  return 1;
-#else
   return (DT != DT_F32 && D <= 256) ? 2 : 1;
-#endif
 }
 template <int DT, int D, bool SS>
 __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a) {
@@ -434,9 +392,7 @@ __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a)
       dm.issue(vb + nx, ldb, a.T - 1 - (kt + 1) * 32, vimg(kt + 1), wave);
       wait_vm<DM::PPW>();  // Q(kt+1) landed (V(kt+1) may still fly: waited above next tile)
     } else {
-#ifndef XDOT_AB_NOWAIT  // timing-only variant (results are wrong): no wait for the next tile's DMA
       wait_vm<0>();
-#endif
     }
     raw_barrier();
   }
@@ -474,11 +430,7 @@ __global__ __launch_bounds__(256, (fwd_occ<DT, D>())) void fwd_kernel(FwdArgs a)
 // share of the registers (operand reads one ahead); its four images fit LDS twice.  D = 160 h = 4
 // row side 2.63 -> 2.29 ms (r5s56)
 template <int DT, int D, bool LD> constexpr int rows_occ() {
-#ifdef XDOT_WIDE_ROWS_OCC1
-  return 1;
-#else
   return (DT != DT_F32 && D <= 160 && !LD) ? 2 : 1;  // D = 192 would spill 84 registers
-#endif
 }
 template <int DT, int D, bool LD>
 __global__ __launch_bounds__(256, (rows_occ<DT, D, LD>())) void bwd_rows_kernel(BwdArgs a) {
@@ -586,9 +538,7 @@ __global__ __launch_bounds__(256, (rows_occ<DT, D, LD>())) void bwd_rows_kernel(
       Pl::template trprod<(rows_occ<DT, D, LD>() == 2 ? 1 : WIDE_LA)>(qi, ds, dk, L);  // dKᵀ += Q_colsᵀ · dSᵀ
     }
     pin_agpr(dk);
-#ifndef XDOT_AB_NOWAIT
     wait_vm<0>();
-#endif
     raw_barrier();
   }
   if (!row_ok) return;
@@ -766,14 +716,10 @@ __global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_ker
         issue_k(rt + 1);
         wait_vm<DM::PPW>();
       } else {
-#ifndef XDOT_AB_NOWAIT
         wait_vm<0>();
-#endif
       }
     } else {
-#ifndef XDOT_AB_NOWAIT
       wait_vm<0>();
-#endif
     }
     pin_agpr(acc);
     raw_barrier();
@@ -790,195 +736,6 @@ __global__ __launch_bounds__(256, (cols_occ<DT, D, DQ, LS>())) void bwd_cols_ker
     for (int g = 0; g < 4; ++g) {
       const float x0 = acc[d][4 * g] * sc, x1 = acc[d][4 * g + 1] * sc, x2 = acc[d][4 * g + 2] * sc, x3 = acc[d][4 * g + 3] * sc;
       if (part) *reinterpret_cast<f32x4*>(part + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};  // fp32 split partial
-      else if (a.dkv16) Pl::store4(reinterpret_cast<T*>(base) + eo + d * 32 + 8 * g + 4 * hf, x0, x1, x2, x3);
-      else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + eo + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// dQ pass, software-pipelined (opt-in; 16-bit, D <= 256, recomputed S): iteration rt issues the S / dP
-// MFMAs of tile rt + 1 and runs tile rt's softmax gradient in their gaps (one score per gap, its
-// lse2 / δ rows read four gaps ahead), then dQ += Kᵀ · dS(rt).  The plain kernel runs the
-// softmax between the dP and dQ MFMAs with nothing beside it (one wave per SIMD).  Three-stage
-// ring [dO][K][lse2 | δ] (tile rt + 1 must be resident one iteration early); two S / dP register
-// sets alternate by the parity of the unroll-by-2.
-template <int DT, int D> constexpr int dqp_stage() { return 2 * Dma32<Pol<DT, D>>::SLOT + 1024; }
-// Measured SLOWER than the plain pass (r5s48-r5s50: D = 256 h = 3 column side 4.90 -> 5.29 ms,
-// D = 160 4.66 -> 5.26 even with each score's chain spread over three gaps), so opt-in only
-// (-DXDOT_WIDE_DQPIPE) and kept as the measured alternative.
-template <int DT, int D> constexpr bool dq_pipe_ok() {
-#ifdef XDOT_WIDE_DQPIPE
-  return DT != DT_F32 && D <= 256 && 3 * dqp_stage<DT, D>() <= 160 * 1024;
-#else
-  return false;
-#endif
-}
-template <int DT, int D>
-__global__ __launch_bounds__(256, 1) void bwd_cols_dq_pipe(BwdArgs a) {
-  using Pl = Pol<DT, D>;
-  using T = typename Pl::T;
-  using DM = Dma32<Pl>;
-  constexpr int DB = D / 32, SLOT = DM::SLOT, NF = Pl::NF, ST = dqp_stage<DT, D>();
-  constexpr int NA = 2 * NF;  // MFMAs per S / dP pair
-  static_assert(NA >= 20, "the softmax chains of 16 scores need 20 gaps");
-  char* const sm = fa::smem;
-  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const auto L = Pl::lanes(lane);
-  const int ncb = (a.T + 127) / 128;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bhs = lin / ncb;
-  const int ns = a.csq > 1 ? a.csq : 1;
-  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
-  const int b = bh / a.H, h = bh % a.H;
-  const int C = a.H * D;
-  const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
-  const bool col_ok = col < a.T;
-  const int NKT64 = (a.T + 63) / 64, NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
-  const int NRT64 = (a.R + 63) / 64, TPAD = (a.T + 127) / 128 * 128;
-  const int NRT = (a.R + 31) / 32;
-  const int rt_beg = (int)((int64_t)sp * NRT / ns), rt_end = (int)((int64_t)(sp + 1) * NRT / ns);
-
-  typename Pl::Frag qf[NF], vf[NF];
-  {
-    const int64_t off = ((int64_t)b * a.T + (col_ok ? col : 0)) * a.ldkv + h * D;
-    Pl::load_frag(qf, reinterpret_cast<const T*>(a.kc) + off, col_ok, hf);
-    Pl::load_frag(vf, reinterpret_cast<const T*>(a.vc) + off, col_ok, hf);
-  }
-#ifndef XDOT_DQP_FRA
-#define XDOT_DQP_FRA 0
-#endif
-  // fragments stay in VGPRs: the AGPRs hold dQ; with both register sets of S / dP live, moving the
-  // Q fragment there too left the allocator shuffling AGPR <-> VGPR copies through the loop
-  constexpr int FRA = XDOT_DQP_FRA;
-  pin_first<FRA>(qf);
-  const int ldb = (int)(C * sizeof(T));
-  const char* kb = reinterpret_cast<const char*>(reinterpret_cast<const T*>(a.rows) + (int64_t)b * a.R * C + h * D);
-  const char* db_ = reinterpret_cast<const char*>(reinterpret_cast<const T*>(a.dout) + (int64_t)b * a.R * C + h * D);
-  const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
-  const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
-  DM dm;
-  dm.init(wave, lane, ldb);
-  auto stage = [&](int t) { return sm + ((t - rt_beg) % 3) * ST; };
-  const float c2 = a.prescaled ? 1.f : a.scale * LOG2E;
-  f32x16 acc[DB];
-#pragma unroll
-  for (int i = 0; i < DB; ++i) acc[i] = f32x16{};
-  pin_agpr(acc);
-  auto issue = [&](int t) {
-    char* st = stage(t);
-    dm.issue(db_ + (int64_t)t * 32 * ldb, ldb, a.R - 1 - t * 32, st, wave);
-    const uint32_t rr = (uint32_t)min(t * 32 + (lane & 31), a.R - 1) * 4;
-    fa::glds4(lse2, rr, st + 2 * SLOT);
-    fa::glds4(dlt, rr, st + 2 * SLOT + 256);
-    dm.issue(kb + (int64_t)t * 32 * ldb, ldb, a.R - 1 - t * 32, st + SLOT, wave);
-  };
-  auto flag_of = [&](int t) {
-    const int f = c0 >= a.T ? 1 : (a.mflags ? flag_at(a.mflags, b, NRB32, NKT4, t, c0 >> 6) : 0);
-    return __builtin_amdgcn_readfirstlane(f);
-  };
-  // S and dP of tile t (plain, no work in the gaps)
-  auto products = [&](int t, f32x16& s, f32x16& dp) {
-    s = Pl::rowprod(stage(t) + SLOT, qf, f32x16{}, L);  // S (row x col)
-    dp = Pl::rowprod(stage(t), vf, f32x16{}, L);        // dP (row x col)
-    pin_first<FRA>(qf);
-  };
-  // softmax gradient of one score: dp <- dS / scale
-  auto grad = [&](f32x16& s, f32x16& dp, int r, float l, float d) {
-    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], c2, -l));
-    dp[r] = p * (dp[r] - d);
-  };
-  auto softmax = [&](int t, f32x16& s, f32x16& dp) {
-    const float* ls = reinterpret_cast<const float*>(stage(t) + 2 * SLOT);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) grad(s, dp, r, ls[tidx(r, hf)], ls[64 + tidx(r, hf)]);
-  };
-  // S / dP of tile tn into (sn, dn) with tile tc's softmax gradient (sc, dc) in the MFMA gaps.
-  // Each score's chain (fma -> exp -> sub, mul) is spread over three gaps, so one gap holds
-  // independent work of three scores (a chain inside one gap outlasts the 32-cycle MFMA); the
-  // tile's lse2 / δ rows are read before the first MFMA and first used two gaps later.
-  auto interleaved = [&](int tn, f32x16& sn, f32x16& dn, int tc, f32x16& sc, f32x16& dc) {
-    const char* ki = stage(tn) + SLOT;
-    const char* di = stage(tn);
-    const float* ls = reinterpret_cast<const float*>(stage(tc) + 2 * SLOT);
-    f32x4 l4[4], d4[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      l4[g] = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hf);
-      d4[g] = *reinterpret_cast<const f32x4*>(ls + 64 + 8 * g + 4 * hf);
-    }
-    auto opnd = [&](int i) { return i < NF ? fa::row_frag<D>(ki, 0, i, L.L) : fa::row_frag<D>(di, 0, i - NF, L.L); };
-    u32x4 buf[3];
-    buf[0] = opnd(0);
-    buf[1] = opnd(1);
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if (i + 2 < NA) buf[(i + 2) % 3] = opnd(i + 2);
-      if (i < NF) sn = fa::mfma32<DT>::run(buf[i % 3], qf[i], i == 0 ? f32x16{} : sn);
-      else dn = fa::mfma32<DT>::run(buf[i % 3], vf[i - NF], i == NF ? f32x16{} : dn);
-      const int rf = i - 2, re = i - 3, rd = i - 4;  // scores at their fma / exp / finish step
-      if (rd >= 0 && rd < 16) dc[rd] = sc[rd] * (dc[rd] - d4[rd >> 2][rd & 3]);
-      if (re >= 0 && re < 16) sc[re] = __builtin_amdgcn_exp2f(sc[re]);
-      if (rf >= 0 && rf < 16) sc[rf] = __builtin_fmaf(sc[rf], c2, -l4[rf >> 2][rf & 3]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    pin_first<FRA>(qf);
-  };
-  // partial tiles (wave-uniform): masked bits / rows past R -> S = -inf before the softmax
-  auto mask_tile = [&](int t, int flag, f32x16& s) {
-    const int vr = a.R - t * 32;
-    if (flag == 2 || vr < 32) {
-      uint32_t w = 0;
-      if (flag == 2 && col_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (t >> 1)) * TPAD + col] >> (32 * (t & 1))));
-      fa::sel_bits16(s, (uint32_t)fa::tile_bits(w, vr, hf), fa::NINF_BITS);
-    }
-  };
-
-  f32x16 sv[2], dv[2];
-  int flagc = 1;
-  if (rt_beg < rt_end) {
-    issue(rt_beg);
-    if (rt_beg + 1 < rt_end) issue(rt_beg + 1);
-    wait_vm<0>();
-    raw_barrier();
-    flagc = flag_of(rt_beg);
-    if (flagc != 1) products(rt_beg, sv[0], dv[0]);
-  }
-  auto iter = [&](auto parc, int rt) {
-    constexpr int PAR = decltype(parc)::value;
-    f32x16 &sc = sv[PAR], &dc = dv[PAR], &sn = sv[PAR ^ 1], &dn = dv[PAR ^ 1];
-    if (rt + 2 < rt_end) issue(rt + 2);  // into the stage tile rt - 1 used (free since its barrier)
-    const int flagn = rt + 1 < rt_end ? flag_of(rt + 1) : 1;
-    if (flagc != 1) mask_tile(rt, flagc, sc);
-    if (flagc != 1 && flagn != 1) {
-      interleaved(rt + 1, sn, dn, rt, sc, dc);
-    } else {
-      if (flagc != 1) softmax(rt, sc, dc);
-      if (flagn != 1) products(rt + 1, sn, dn);
-    }
-    if (flagc != 1) Pl::trprod(stage(rt) + SLOT, dc, acc, L);  // dQᵀ += Kᵀ · dS
-    pin_agpr(acc);
-#ifndef XDOT_AB_NOWAIT
-    wait_vm<0>();  // tile rt + 2 resident for the next iteration's products
-#endif
-    raw_barrier();
-    flagc = flagn;
-  };
-  for (int rt = rt_beg; rt < rt_end; rt += 2) {
-    iter(std::integral_constant<int, 0>{}, rt);
-    if (rt + 1 < rt_end) iter(std::integral_constant<int, 1>{}, rt + 1);
-  }
-  if (!col_ok) return;
-  const float sc = a.prescaled ? LN2 : a.scale;
-  char* base = reinterpret_cast<char*>(a.dkc);
-  const int64_t eo = ((int64_t)b * a.T + col) * a.ldg + h * D;
-  float* const part = ns > 1 ? a.cpq + (((int64_t)sp * a.B + b) * a.T + col) * C + h * D : nullptr;
-#pragma unroll
-  for (int d = 0; d < DB; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float x0 = acc[d][4 * g] * sc, x1 = acc[d][4 * g + 1] * sc, x2 = acc[d][4 * g + 2] * sc, x3 = acc[d][4 * g + 3] * sc;
-      if (part) *reinterpret_cast<f32x4*>(part + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};
       else if (a.dkv16) Pl::store4(reinterpret_cast<T*>(base) + eo + d * 32 + 8 * g + 4 * hf, x0, x1, x2, x3);
       else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(base) + eo + d * 32 + 8 * g + 4 * hf) = f32x4{x0, x1, x2, x3};
     }
@@ -1070,10 +827,7 @@ int wide_cols(const xdot::fa::BwdArgs* a, hipStream_t st) {
   };
   auto dqp = [&](auto LSC) {
     constexpr bool LSV = decltype(LSC)::value;
-    if constexpr (!LSV && dq_pipe_ok<DT, D>())
-      hipLaunchKernelGGL((bwd_cols_dq_pipe<DT, D>), dim3(W * sq), dim3(256), (3 * dqp_stage<DT, D>()), st, *a);
-    else
-      hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, LSV>), dim3(W * sq), dim3(256), (cols_lds<Pl, true, LSV>()), st, *a);
+    hipLaunchKernelGGL((bwd_cols_kernel<DT, D, true, LSV>), dim3(W * sq), dim3(256), (cols_lds<Pl, true, LSV>()), st, *a);
     fin(true);
   };
   if constexpr (DT == xdot::DT_F32) {
@@ -1113,10 +867,7 @@ int wide_occ(int kernel, bool sbuf) {
   if constexpr (recompute_ok<DT, D>()) {
     if (kernel == 0) return wg_per_cu(fwd_kernel<DT, D, false>, fwd_lds<Pl>());
     if (kernel == 1) return wg_per_cu(bwd_rows_kernel<DT, D, false>, rows_lds<Pl, false>());
-    if (kernel == 2) {
-      if constexpr (dq_pipe_ok<DT, D>()) return wg_per_cu(bwd_cols_dq_pipe<DT, D>, 3 * dqp_stage<DT, D>());
-      else return wg_per_cu(bwd_cols_kernel<DT, D, true, false>, cols_lds<Pl, true, false>());
-    }
+    if (kernel == 2) return wg_per_cu(bwd_cols_kernel<DT, D, true, false>, cols_lds<Pl, true, false>());
     return wg_per_cu(bwd_cols_kernel<DT, D, false, false>, cols_lds<Pl, false, false, aux_in_slack<DT, D, false, false>()>());
   }
   return 0;

@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     const int rr = rt * 32 + tid;
     return tid < 32 && rr < a.R ? lse2[rr] : __builtin_inff();
   };
-  constexpr int PF = XDOT_SB_PF;
+  constexpr int PF = fa::SB_PF;
   Tile<D> td;
   f32x16 q[PF];
   float ax = 0.f;
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < DB; ++i) dk[i] = f32x16{};
 
-  constexpr int PF = XDOT_SB_PF;
+  constexpr int PF = fa::SB_PF;
   Tile<D> tq;
   f32x16 q[PF];
   if (kt_beg < kt_end) {

@@ -41,9 +41,6 @@ constexpr int NG = 2 * PPW;           // DMAs per wave per k-tile
 constexpr int EPI = 8 * 16 * 64 * 4;  // wave-private 16 x 64 fp32 epilogue strips
 constexpr int LDS = RING + EPI;       // 160 KiB
 static_assert(LDS <= 160 * 1024, "lds");
-#ifndef XDOT_G2F_ISS
-#define XDOT_G2F_ISS 0  // DMA issue placement (A/B): 0 groups 0-1, 1 staggered by wave half, 2 spread
-#endif
 
 __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
 
@@ -355,15 +352,8 @@ __global__ __launch_bounds__(512) void gemm2_f32_kernel(GemmArgs p, float* __res
 #pragma unroll
         for (int j = 0; j < 2; ++j) fb1[j] = fragB(sb, j, g + 1);
       }
-#if XDOT_G2F_ISS == 1
-      // the two waves of a SIMD (w, w + 4) issue their DMAs in different groups: one of them
-      // always has MFMAs to issue while the other stalls on its DMA issue
-      if ((g >> 1) == (wave >> 2) && pre) issue_part((g & 1) * (NG / 2), ((g & 1) + 1) * (NG / 2));
-#elif XDOT_G2F_ISS == 2
-      if (pre) issue_part(g * (NG / 4), (g + 1) * (NG / 4));  // two per group
-#else
+      // (staggered by wave half or spread over all 4 groups measured the same, profiles/r5_fp32.md §4)
       if (g < 2 && pre) issue_part(g * (NG / 2), (g + 1) * (NG / 2));
-#endif
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
