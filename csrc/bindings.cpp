@@ -837,7 +837,7 @@ at::Tensor proj(const at::Tensor& x, const at::Tensor& w, const c10::optional<at
                     (M - 1) * p.ldc + N <= avail_elems(c),
                 "xdot.proj: operand extents exceed their storage");
     c10::DeviceGuard guard(x.device());
-    rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, force ? 1 : 0, cur_stream(x));
+    rc = xdot_gemm_proj_launch(&p, dt_code(x.scalar_type()), nn ? 1 : 0, (int)force, cur_stream(x));
     if (rc != -3) check_launch((hipError_t)rc, "gemm_proj");
   }
   if (rc == -3) {  // library GEMM (alpha scales the bias too: C = alpha (A op(B) + bias), one rounding)

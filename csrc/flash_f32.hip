@@ -184,9 +184,11 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
 
 // ------------------------------------------------------------------------------------------
 // forward: 4 waves x 32 rows of one (b, h); sweeps 32-column tiles of its column split
-// SS: store the raw scores into a.sbuf (score-buffer mode)
-template <int D, bool SS>
-__global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
+// SS: store the raw scores into a.sbuf (score-buffer mode); SD (with SS): stored by direct 16-dword
+// scatters (fa::blk_store) instead of through the wave-private LDS transpose tile: 16 KiB less LDS
+// per workgroup, so three workgroups fit a CU (52.5 KiB each at D = 96) instead of two
+template <int D, bool SS, bool SD = false>
+__global__ __launch_bounds__(256, SD && D <= 96 ? 3 : 2) void fwd_kernel(FwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     const bool more = kt + 1 < kt_end;
     // the previous tile's S leaves first: its global stores then complete under this tile's
     // products instead of in the wait before its barrier (vmcnt counts stores too)
-    if constexpr (SS) {
+    if constexpr (SS && !SD) {
       if (kt > kt_beg) fa::blk_flush_lds(sbw + (int64_t)(kt - 1) * sbw_step, swl, lane);
     }
     if (more)  // into the stage the previous tile used (all reads of it ended at its barrier)
@@ -249,16 +251,20 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     if (flag != 1) s = rowprod<D>(qi, kf, f32x16{}, lane);  // Sᵀ: col (register) x row (lane)
     // raw S, every tile (skipped tiles store zeros nobody reads): LDS writes here, the transposed
     // global stores at the start of the next tile
-    if constexpr (SS) fa::blk_put_lds(swl, s, lane);
+    if constexpr (SS && !SD) fa::blk_put_lds(swl, s, lane);
+    if constexpr (SS && SD) fa::blk_store(sbw + (int64_t)kt * sbw_step, s, lane);
     if (flag != 1) {
       const int valid = a.T - kt * 32;
       if (flag == 2 || valid < 32) {
         uint32_t w = 0;
         if (flag == 2 && row_ok) w = fa::settle((uint32_t)(a.mbits[((int64_t)b * NKT64 + (kt >> 1)) * a.R + row] >> (32 * (kt & 1))));
+        // lane-half offset applied once: constant shifts / compares per register
+        const uint32_t wh = w >> (4 * hf);
+        const int vh = valid - 4 * hf;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int c = tidx(r, hf);
-          if (((w >> c) & 1u) || c >= valid) s[r] = NEG_INF;
+          const int c = tidx(r, 0);
+          if (((wh >> c) & 1u) || c >= vh) s[r] = NEG_INF;
         }
       }
       float mx = NEG_INF;
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
     fa::wait_vm<0>();  // the next tile's pieces landed
     __syncthreads();
   }
-  if constexpr (SS) {
+  if constexpr (SS && !SD) {
     if (kt_end > kt_beg) fa::blk_flush_lds(sbw + (int64_t)(kt_end - 1) * sbw_step, swl, lane);
   }
 
@@ -567,9 +573,10 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
       }
       if (flag == 2) {  // masked entries: P = dS = 0 (the unmasked loop stays select-free)
         const uint32_t w = col_ok ? fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)))) : 0u;
+        const uint32_t wh = w >> (4 * hf);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if ((w >> tidx(r, hf)) & 1u) s[r] = dp[r] = 0.f;
+          if ((wh >> tidx(r, 0)) & 1u) s[r] = dp[r] = 0.f;
       }
     }
     // dS (over S or apart), every tile (skipped tiles store zeros nobody reads): LDS writes
@@ -691,7 +698,7 @@ __global__ __launch_bounds__(256, 2) void bwd_rows_ds_kernel(BwdArgs a) {
 // column work, no V / K traffic).  Runs BEFORE bwd_cols_kernel<D, true>, which overwrites S with
 // dS.  Same grid as the column kernel; stage = dO image + lse2[32].
 template <int D>
-__global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, D <= 96 ? 4 : 2) void bwd_cols_dv_kernel(BwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB, STG = CF::IMG + 32;
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -752,11 +759,13 @@ __global__ __launch_bounds__(256, 2) void bwd_cols_dv_kernel(BwdArgs a) {
     if (flag != 1) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[r] = ex2(__builtin_fmaf(s[r], c2, -ls[tidx(r, hf)]));
-      if (flag == 2) {  // masked entries: P = 0
+      if (flag == 2) {  // masked entries: P = 0 (the lane-half shift once, then constant shifts:
+                        // no per-register shift amounts held across the loop)
         const uint32_t w = col_ok ? fa::settle((uint32_t)(a.mbits[((int64_t)b * NRT64 + (rt >> 1)) * TPAD + col] >> (32 * (rt & 1)))) : 0u;
+        const uint32_t wh = w >> (4 * hf);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if ((w >> tidx(r, hf)) & 1u) s[r] = 0.f;
+          if ((wh >> tidx(r, 0)) & 1u) s[r] = 0.f;
       }
       trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
     }
@@ -804,12 +813,27 @@ template <int D> constexpr int lds_bytes_sb() { return lds_bytes<D>() + 4 * 4096
     default: return -1;                \
   }
 
+namespace {
+// The score-storing forward scatters S directly (three workgroups per CU at D <= 96): exact fp32
+// step 54.6-55.0 -> 53.6-54.0 ms on one box (profiles/r6_fp32.md).  XDOT_F32_FWD_DIRECT=0: the
+// LDS-transposed store at two workgroups per CU.
+bool fwd_direct_store() {
+  const char* e = std::getenv("XDOT_F32_FWD_DIRECT");  // read per call (A/B in one process)
+  return !(e && *e == '0');
+}
+}  // namespace
+
 extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st) {
   using namespace xdot::fa32;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
   const int nrb = (a->R + 127) / 128;
   const dim3 grid(nrb * a->B * a->H * a->nsplit);
   if (a->sbuf) {
+    if (fwd_direct_store()) {
+#define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
+      XF32_DISPATCH(L)
+#undef L
+    }
 #define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true>), grid, dim3(256), lds_bytes_sb<DV>(), st, *a)
     XF32_DISPATCH(L)
 #undef L
@@ -957,7 +981,8 @@ extern "C" int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int
   int occ = 0;
 #define OC(DV)                                                                                                   \
   if (D == DV)                                                                                                   \
-    occ = kernel == 0 ? (sbuf ? xdot::fa::wg_per_cu(fwd_kernel<DV, true>, lds_bytes_sb<DV>())                  \
+    occ = kernel == 0 ? (sbuf ? (fwd_direct_store() ? xdot::fa::wg_per_cu(fwd_kernel<DV, true, true>, lds_bytes<DV>()) \
+                                                    : xdot::fa::wg_per_cu(fwd_kernel<DV, true>, lds_bytes_sb<DV>())) \
                               : xdot::fa::wg_per_cu(fwd_kernel<DV, false>, lds_bytes<DV>()))                   \
                       : (sbuf ? xdot::fa::wg_per_cu(bwd_rows_ds_kernel<DV>, 2 * Cfg<DV>::IMG * 4)              \
                               : xdot::fa::wg_per_cu(bwd_rows_kernel<DV>, lds_bytes<DV>()));

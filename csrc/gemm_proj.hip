@@ -35,12 +35,6 @@ constexpr int BK = 64;
 #ifndef GP_PRE
 #define GP_PRE 0  // read both k-steps' fragments before the first k-step's MFMAs (A/B knob)
 #endif
-#ifndef GP_NS_BIG
-#define GP_NS_BIG 2  // ring stages of the 128x128 tile (3: 96 KiB, one workgroup per CU)
-#endif
-#ifndef GP_NS_SMALL
-#define GP_NS_SMALL 2  // ring stages of the 64-row tiles
-#endif
 #ifndef GP_BIG
 #define GP_BIG 1  // 0: never the 128x128 tile (64x128 at every M)
 #endif
@@ -73,7 +67,7 @@ template <> __device__ __forceinline__ void dma_run<4>(const void* base, const u
                : "memory", "scc");
 }
 
-template <int BM, int BN, bool NN, int NS_ = (BM >= 128 ? GP_NS_BIG : GP_NS_SMALL)> struct Cfg {
+template <int BM, int BN, bool NN, int NS_> struct Cfg {
   static constexpr int NS = NS_;
   static constexpr int WGM = BM == 256 ? 4 : 2, NW = 2 * WGM, NTH = 64 * NW;  // waves: WGM x 2
   static constexpr int A_BYTES = BM * 128;                 // [BM rows][64 k x 2 B]
@@ -84,14 +78,21 @@ template <int BM, int BN, bool NN, int NS_ = (BM >= 128 ? GP_NS_BIG : GP_NS_SMAL
   static constexpr int WM = BM / WGM, WN = BN / 2, MT = WM / 16, NT = WN / 16;
 };
 
+// lanes 16-31 of x <-> lanes 0-15 of y, and 48-63 of x <-> 32-47 of y
+__device__ __forceinline__ void swap16(uint32_t& x, uint32_t& y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+
 }  // namespace gp
 
-template <int DT, int BM, int BN, bool NN, bool BIAS>
+template <int DT, int BM, int BN, bool NN, bool BIAS, int NS_, bool V16>
 __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjArgs p) {
   using namespace gp;
   using fa::smem;
   using fa::lds_addr;
-  using CF = Cfg<BM, BN, NN>;
+  using CF = Cfg<BM, BN, NN, NS_>;
   using T16 = typename dt_traits<DT>::T;
   static_assert(!NN || BN == 128, "NN: 256-byte mn-contiguous B rows");
   constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW, NS = CF::NS;
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
     }
   }
 
-  // ---- epilogue: + bias (fp32), one rounding, 8-byte stores of 4 consecutive columns ----
+  // ---- epilogue: + bias (fp32), one rounding, 16-byte (V16) or 8-byte stores ----
   f32x4 bv[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -232,13 +233,28 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
   for (int mt = 0; mt < MT; ++mt) {
     const int m = m0 + CF::WM * wm + 16 * mt + l15;
     if (m < p.M) {
+      if constexpr (V16) {
+        // two 16x16 tiles (nt = 2i, 2i+1) paired by v_permlane16_swap: lane group g then holds 8
+        // consecutive columns, 16 (g & 1) + 8 (g >> 1) into the 32-column strip -- 16-byte stores
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const f32x4 v = (acc[mt][nt] + bv[nt]) * p.alpha;
-        u32x2 w;
-        w[0] = fa::pack2<DT>(v[0], v[1]);
-        w[1] = fa::pack2<DT>(v[2], v[3]);
-        *reinterpret_cast<u32x2*>(cp + (int64_t)m * p.ldc + n0 + CF::WN * wn + 16 * nt + 4 * g) = w;
+        for (int i = 0; i < NT / 2; ++i) {
+          const f32x4 x = (acc[mt][2 * i] + bv[2 * i]) * p.alpha, y = (acc[mt][2 * i + 1] + bv[2 * i + 1]) * p.alpha;
+          uint32_t X0 = fa::pack2<DT>(x[0], x[1]), X1 = fa::pack2<DT>(x[2], x[3]);
+          uint32_t Y0 = fa::pack2<DT>(y[0], y[1]), Y1 = fa::pack2<DT>(y[2], y[3]);
+          gp::swap16(X0, Y0);
+          gp::swap16(X1, Y1);
+          *reinterpret_cast<u32x4*>(cp + (int64_t)m * p.ldc + n0 + CF::WN * wn + 32 * i + 16 * (g & 1) + 8 * (g >> 1)) =
+              u32x4{X0, X1, Y0, Y1};
+        }
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const f32x4 v = (acc[mt][nt] + bv[nt]) * p.alpha;
+          u32x2 w;
+          w[0] = fa::pack2<DT>(v[0], v[1]);
+          w[1] = fa::pack2<DT>(v[2], v[3]);
+          *reinterpret_cast<u32x2*>(cp + (int64_t)m * p.ldc + n0 + CF::WN * wn + 16 * nt + 4 * g) = w;
+        }
       }
     }
   }
@@ -248,7 +264,9 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
 
 // Tile choice: the largest tile that still puts >= 2 workgroups on every CU of the 256
 // (NN needs BN = 128).  Returns -3 when the shape / layout is not eligible, or (force = 0) when
-// the product is large enough for the library GEMM to be faster; the caller then runs that.
+// the library GEMM is measured faster for the shape; the caller then runs that.
+// force: 0 auto (kernel or library), 1 kernel with the automatic tile, 2.. one tile configuration
+// (A/B: 2 = 64x64, 3 = 64x128, 4 = 128x128, 5 = 128x128 with a 3-stage ring, 6 = 256x128).
 extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, int force, hipStream_t st) {
   using namespace xdot;
   if (dt != DT_BF16 && dt != DT_F16) return -3;
@@ -257,34 +275,46 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, in
   if (reinterpret_cast<uintptr_t>(a->C) & 7) return -3;
   if (nn && a->N % 128) return -3;
   auto tiles = [&](int bm, int bn) { return (int64_t)((a->M + bm - 1) / bm) * (a->N / bn); };
-  // >= 16384 rows (the N=1 products, 25000 rows): hipBLASLt is 1.1-1.3x faster there; at the
-  // 12500 / 6250 / 3125 rows of N = 2 / 4 / 8 this kernel is 0.84-1.0x its time (profiles/r4_s2.md
-  // §5): decline unless forced
-  if (!force && a->M >= 16384) return -3;
-  int bm = 64, bn = 64;
-  if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) { bm = 256; bn = 128; }
-  else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) bm = bn = 128;
-  else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) bn = 128;
+  int cfg;  // 2..6 as force
+  if (force >= 2) {
+    cfg = force;
+    if (cfg > 6 || (cfg == 2 && nn) || (cfg >= 3 && a->N % 128)) return -3;
+  } else {
+    if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) cfg = 6;
+    else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) cfg = 4;
+    else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) cfg = 3;
+    else cfg = 2;
+  }
+  const int bm = cfg == 6 ? 256 : (cfg >= 4 ? 128 : 64), bn = cfg == 2 ? 64 : 128;
   const int64_t grid = tiles(bm, bn);
   if (grid > 0x7FFFFFFF) return -3;
   const bool bias = a->bias != nullptr;
-#define GPL(DTV, BMV, BNV, NNV, BV)                                                                          \
-  hipLaunchKernelGGL((gemm_proj_kernel<DTV, BMV, BNV, NNV, BV>), dim3((unsigned)grid), dim3(gp::Cfg<BMV, BNV, NNV>::NTH),       \
-                     (gp::Cfg<BMV, BNV, NNV>::LDS), st, *a)
-#define GPB(DTV, BMV, BNV, NNV) \
-  if (bias) GPL(DTV, BMV, BNV, NNV, true); else GPL(DTV, BMV, BNV, NNV, false)
-#define GPD(BMV, BNV, NNV) \
-  if (dt == DT_BF16) { GPB(DT_BF16, BMV, BNV, NNV); } else { GPB(DT_F16, BMV, BNV, NNV); }
+  // 16-byte output stores (paired tiles) when C's rows are 16-byte aligned
+  const bool v16 = a->ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(a->C) & 15) == 0;
+#define GPL(DTV, BMV, BNV, NNV, NSV, BV, VV)                                                                      \
+  hipLaunchKernelGGL((gemm_proj_kernel<DTV, BMV, BNV, NNV, BV, NSV, VV>), dim3((unsigned)grid),                   \
+                     dim3(gp::Cfg<BMV, BNV, NNV, NSV>::NTH), (gp::Cfg<BMV, BNV, NNV, NSV>::LDS), st, *a)
+#define GPV(DTV, BMV, BNV, NNV, NSV, BV) \
+  if (v16) GPL(DTV, BMV, BNV, NNV, NSV, BV, true); else GPL(DTV, BMV, BNV, NNV, NSV, BV, false)
+#define GPB(DTV, BMV, BNV, NNV, NSV) \
+  if (bias) { GPV(DTV, BMV, BNV, NNV, NSV, true); } else { GPV(DTV, BMV, BNV, NNV, NSV, false); }
+#define GPD(BMV, BNV, NNV, NSV) \
+  if (dt == DT_BF16) { GPB(DT_BF16, BMV, BNV, NNV, NSV); } else { GPB(DT_F16, BMV, BNV, NNV, NSV); }
   if (nn) {
-    if (bm == 256) { GPD(256, 128, true); } else if (bm == 128) { GPD(128, 128, true); } else { GPD(64, 128, true); }
+    if (cfg == 6) { GPD(256, 128, true, 2); }
+    else if (cfg == 5) { GPD(128, 128, true, 3); }
+    else if (cfg == 4) { GPD(128, 128, true, 2); }
+    else { GPD(64, 128, true, 2); }
   } else {
-    if (bm == 256) { GPD(256, 128, false); }
-    else if (bm == 128) { GPD(128, 128, false); }
-    else if (bn == 128) { GPD(64, 128, false); }
-    else { GPD(64, 64, false); }
+    if (cfg == 6) { GPD(256, 128, false, 2); }
+    else if (cfg == 5) { GPD(128, 128, false, 3); }
+    else if (cfg == 4) { GPD(128, 128, false, 2); }
+    else if (cfg == 3) { GPD(64, 128, false, 2); }
+    else { GPD(64, 64, false, 2); }
   }
 #undef GPD
 #undef GPB
+#undef GPV
 #undef GPL
   return (int)hipGetLastError();
 }

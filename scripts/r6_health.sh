@@ -7,3 +7,4 @@ rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1 || exit $?
+if [ -n "$R6_EXTRA" ]; then eval "$R6_EXTRA" || exit $?; fi

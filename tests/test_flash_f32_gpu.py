@@ -104,11 +104,15 @@ def test_flash_f32_column_split(gpu, nsplit):
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
 @pytest.mark.parametrize("nsplit", [0, 3])
-def test_flash_f32_score_buffer_bitwise(gpu, case, mask_kind, nsplit):
+@pytest.mark.parametrize("direct", [False, True])
+def test_flash_f32_score_buffer_bitwise(gpu, monkeypatch, case, mask_kind, nsplit, direct):
     """Reading S / dS from the score buffer instead of recomputing them changes nothing: the
     forward, both backward kernels and the column-split partials are BITWISE equal to the
-    recompute path (same MFMA chains), which the fp64 test above bounds."""
+    recompute path (same MFMA chains), which the fp64 test above bounds.  ``direct``: the forward
+    scatters S straight to the buffer (XDOT_F32_FWD_DIRECT=1, three workgroups per CU)."""
     from xdot.ops import flash
+
+    monkeypatch.setenv("XDOT_F32_FWD_DIRECT", "1" if direct else "0")
 
     B, R, N, Rc, H, D = case
     T = N * Rc

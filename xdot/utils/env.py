@@ -93,6 +93,9 @@ variable                    default   effect
 ``XDOT_F32_SPLIT`` (C++)     auto      column splits of the fp32 forward / row-side kernels: auto =
                                       occupancy round model of the fp32 instantiation (up to 8);
                                       fwd = forward only; old = the 16-bit model; n = forced
+``XDOT_F32_FWD_DIRECT`` (C++) 1        the score-storing exact-fp32 forward scatters S straight to the
+                                      buffer (no LDS transpose tile: three workgroups per CU at
+                                      D <= 96); 0 = the LDS-transposed store at two per CU
 ``XDOT_WIDE_SPLIT`` (C++)    auto      split counts of the wide-head (D > 128) kernels from their own
                                       occupancy (row splits of both column passes, column splits
                                       of forward / row side); 0 = previous model; n = forced
