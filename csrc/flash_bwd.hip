@@ -558,17 +558,36 @@ __global__ __launch_bounds__(256) void flash_bwd_rows_sum(BwdArgs a) {
 
 // column-side row-split partials (BwdArgs::csq / csv): out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c],
 // in split order (deterministic), fp32 partials -> output dtype
+// One 16-byte chunk per thread; every split's chunk is loaded before any is added (up to 4 splits in
+// flight per thread) and the chunk index splits with 32-bit math where it fits
 template <int DT>
 __global__ __launch_bounds__(256) void cols_sum_kernel(const float* __restrict__ part, void* __restrict__ out_, int S,
                                                         int64_t rows, int C, int64_t ldo) {
-  const int c4 = C / 4;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * c4) return;
-  const int64_t r = idx / c4;
-  const int c = (int)(idx - r * c4) * 4;
+  const uint32_t c4 = (uint32_t)C / 4;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = rows * c4;
+  if (idx >= total) return;
+  int64_t r;
+  int c;
+  if (total <= 0xFFFFFFFFll) {  // (uniform) 32-bit division
+    const uint32_t i32 = (uint32_t)idx, r32 = i32 / c4;
+    r = r32;
+    c = (int)(i32 - r32 * c4) * 4;
+  } else {
+    r = idx / c4;
+    c = (int)(idx - r * c4) * 4;
+  }
   const int64_t sl = rows * C;
-  f32x4 acc = *reinterpret_cast<const f32x4*>(part + r * C + c);
-  for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(part + s * sl + r * C + c);
+  const float* p = part + r * C + c;
+  f32x4 v[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if (s < S) v[s] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + s * sl));
+  f32x4 acc = v[0];
+#pragma unroll
+  for (int s = 1; s < 4; ++s)
+    if (s < S) acc += v[s];
+  for (int s = 4; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * sl);  // (more than 4 splits)
   if constexpr (DT == DT_F32) {
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out_) + r * ldo + c) = acc;
   } else {

@@ -367,6 +367,43 @@ __global__ __launch_bounds__(256) void prep_kernel(BwdArgs a, const float* out, 
   delta[li] = acc;
 }
 
+// the same, 8 lanes per (b, row, h): each lane a contiguous D / 8 floats of O and dO (the wave reads
+// 8 heads' rows contiguously), a 3-step xor reduction, lane 0 of the 8 writes (the one-thread-per-row
+// form ran 170 us at T = R = 25000, H = 8: one thread streamed 2 x 384 B alone)
+template <int D>
+__global__ __launch_bounds__(256) void prep8_kernel(BwdArgs a, const float* out, float* delta) {
+  constexpr int NV = D / 32;  // float4 per lane
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pr = idx >> 3;  // (b, row, h) pair, h fastest
+  const int sub = (int)(idx & 7);
+  const int64_t npairs = (int64_t)a.B * a.R * a.H;
+  const bool ok = pr < npairs;
+  float acc = 0.f;
+  if (ok) {
+    const int64_t off = pr * D + sub * (D / 8);
+    const f32x4* o = reinterpret_cast<const f32x4*>(out + off);
+    const f32x4* d = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.dout) + off);
+    f32x4 x[NV], y[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      x[i] = o[i];
+      y[i] = d[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) acc += x[i][0] * y[i][0] + x[i][1] * y[i][1] + x[i][2] * y[i][2] + x[i][3] * y[i][3];
+  }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (!ok || sub) return;
+  const int h = (int)(pr % a.H);
+  const int64_t br = pr / a.H;
+  const int row = (int)(br % a.R), b = (int)(br / a.R);
+  const int64_t li = ((int64_t)b * a.H + h) * a.R + row;
+  if (a.lse2) a.lse2[li] = a.lse[li] * LOG2E;
+  delta[li] = acc;
+}
+
 // ------------------------------------------------------------------------------------------
 // backward, row side: dK = scale · Σ_cols dS · Q_cols.  4 waves x 32 rows, column split.
 template <int D>
@@ -540,15 +577,10 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     fa::wait_vm<0>();
     __syncthreads();
   }
-  float* const dwl = sm + 2 * CF::STAGE + wave * 1024;  // dS transpose tile
   for (int rt = rt_beg; rt < rt_end; ++rt) {
     const bool more = rt + 1 < rt_end;
     f32x16 scur;
     if constexpr (LS) scur = snext;
-    // the previous tile's dS leaves first (its stores complete under this tile's products)
-    if constexpr (DS) {
-      if (rt > rt_beg) fa::blk_flush_lds(dsc + (rt - 1) * dstep, dwl, lane);
-    }
     if (more) {
       dm.issue(kdb, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE, CF::IMG);
       ax = aux_load(rt + 1);
@@ -579,9 +611,9 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
           if ((wh >> tidx(r, 0)) & 1u) s[r] = dp[r] = 0.f;
       }
     }
-    // dS (over S or apart), every tile (skipped tiles store zeros nobody reads): LDS writes
-    // before the dQ product, the transposed global stores at the start of the next tile
-    if constexpr (DS) fa::blk_put_lds(dwl, dp, lane);
+    // dS (over S or apart), every tile (skipped tiles store zeros nobody reads): 16 dword
+    // scatters per lane straight into the row kernel's order, before the dQ product
+    if constexpr (DS) fa::blk_store(dsc + rt * dstep, dp, lane);
     if (flag != 1) {
       if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
       trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
@@ -596,9 +628,6 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     }
     fa::wait_vm<0>();  // the next tile's pieces (and S) landed
     __syncthreads();
-  }
-  if constexpr (DS) {
-    if (rt_end > rt_beg) fa::blk_flush_lds(dsc + (rt_end - 1) * dstep, dwl, lane);
   }
   if (!col_ok) return;
   const int64_t prow = ((int64_t)sp * a.B + b) * a.T + col;  // row of the split partials
@@ -800,6 +829,10 @@ __global__ __launch_bounds__(256) void rows_sum_kernel(BwdArgs a, int D) {
 template <int D> constexpr int lds_bytes() { return 2 * Cfg<D>::STAGE * 4; }
 // + one 4-KiB transpose tile per wave for the score-buffer stores (blk_store_lds)
 template <int D> constexpr int lds_bytes_sb() { return lds_bytes<D>() + 4 * 4096; }
+// the column kernels that store dS scatter it directly (no transpose tile): exact fp32 step
+// 52.9 -> 51.9 ms on one box (the LDS-transposed store and its 12.5 % bank conflicts measured
+// slower; profiles/r6_fp32.md)
+template <int D> constexpr int lds_bytes_ds() { return lds_bytes<D>(); }
 
 }  // namespace fa32
 }  // namespace xdot
@@ -854,6 +887,17 @@ extern "C" int xdot_flash_bwd_prep_f32_launch(const xdot::fa::BwdArgs* a, const 
                                               hipStream_t st) {
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
   const int64_t n = (int64_t)a->B * a->R * a->H;
+  if (delta && (D == 32 || D == 64 || D == 96 || D == 128)) {
+    const dim3 grid((unsigned)((8 * n + 255) / 256));
+    const float* o = reinterpret_cast<const float*>(out);
+    switch (D) {
+      case 32: hipLaunchKernelGGL(xdot::fa32::prep8_kernel<32>, grid, dim3(256), 0, st, *a, o, delta); break;
+      case 64: hipLaunchKernelGGL(xdot::fa32::prep8_kernel<64>, grid, dim3(256), 0, st, *a, o, delta); break;
+      case 96: hipLaunchKernelGGL(xdot::fa32::prep8_kernel<96>, grid, dim3(256), 0, st, *a, o, delta); break;
+      default: hipLaunchKernelGGL(xdot::fa32::prep8_kernel<128>, grid, dim3(256), 0, st, *a, o, delta); break;
+    }
+    return 0;
+  }
   hipLaunchKernelGGL(xdot::fa32::prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a,
                      reinterpret_cast<const float*>(out), delta, D);
   return 0;
@@ -894,7 +938,7 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
     const int ps = a->sb_passes ? a->sb_passes : 3;
     const bool dv_first = !a->dsbuf;
 #define LDV(DV) hipLaunchKernelGGL(bwd_cols_dv_kernel<DV>, dim3(W * sv), dim3(256), 2 * (Cfg<DV>::IMG + 32) * 4, st, *a)
-#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), dim3(W * sq), dim3(256), lds_bytes_sb<DV>(), st, *a)
+#define LDQ(DV) hipLaunchKernelGGL((bwd_cols_kernel<DV, true>), dim3(W * sq), dim3(256), lds_bytes_ds<DV>(), st, *a)
 #define L(DV)                            \
   if ((ps & 1) && dv_first) {            \
     LDV(DV);                             \
@@ -915,7 +959,7 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   }
   if (a->dsbuf) {  // dS-only buffer: recompute S, store dS for the row kernel
 #define L(DV)                                                                                                     \
-  hipLaunchKernelGGL((bwd_cols_kernel<DV, false, true>), dim3(W * sq), dim3(256), lds_bytes_sb<DV>(), st, *a); \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, false, true>), dim3(W * sq), dim3(256), lds_bytes_ds<DV>(), st, *a); \
   sum_q();                                                                                                        \
   sum_v(sq)
     XF32_DISPATCH(L)
@@ -940,10 +984,10 @@ template <int D> void f32_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
   const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H;
   const int NRT = (a->R + 31) / 32, cus = xdot_num_cus();
   if (a->sbuf) {
-    *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_sb<D>()));
+    *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_ds<D>()));
     *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, 2 * (Cfg<D>::IMG + 32) * 4));
   } else if (a->dsbuf) {
-    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false, true>, lds_bytes_sb<D>()));
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false, true>, lds_bytes_ds<D>()));
   } else {
     *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, false>, lds_bytes<D>()));
   }

@@ -67,13 +67,16 @@ template <> __device__ __forceinline__ void dma_run<4>(const void* base, const u
                : "memory", "scc");
 }
 
+// NS_: stages of both rings (2 or 3), or 32 = a 3-stage A ring beside a 2-stage B ring (the
+// activations, streamed from HBM, are issued two k-tiles ahead; the L2-resident weights one):
+// 80 KiB at 128x128, so two workgroups still share a CU
 template <int BM, int BN, bool NN, int NS_> struct Cfg {
-  static constexpr int NS = NS_;
+  static constexpr int NA = NS_ == 32 ? 3 : NS_, NB = NS_ == 32 ? 2 : NS_;
   static constexpr int WGM = BM == 256 ? 4 : 2, NW = 2 * WGM, NTH = 64 * NW;  // waves: WGM x 2
   static constexpr int A_BYTES = BM * 128;                 // [BM rows][64 k x 2 B]
   static constexpr int B_BYTES = NN ? 64 * BN * 2 : BN * 128;
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int LDS = NS * STAGE;
+  static constexpr int B_OFF = NA * A_BYTES;               // A ring, then B ring
+  static constexpr int LDS = NA * A_BYTES + NB * B_BYTES;
   static constexpr int APW = A_BYTES / (1024 * NW), BPW = B_BYTES / (1024 * NW);  // 1 KiB pieces per wave
   static constexpr int WM = BM / WGM, WN = BN / 2, MT = WM / 16, NT = WN / 16;
 };
@@ -95,8 +98,8 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
   using CF = Cfg<BM, BN, NN, NS_>;
   using T16 = typename dt_traits<DT>::T;
   static_assert(!NN || BN == 128, "NN: 256-byte mn-contiguous B rows");
-  constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW, NS = CF::NS;
-  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
+  constexpr int MT = CF::MT, NT = CF::NT, APW = CF::APW, BPW = CF::BPW, NA = CF::NA, NB = CF::NB;
+  static_assert((NA == 2 || NA == 3) && NB <= NA, "ring stages");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,10 +135,12 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
   const char* a_base = reinterpret_cast<const char*>(p.A) + (int64_t)m0 * lda2;
   const char* b_base = reinterpret_cast<const char*>(p.B) + (NN ? (int64_t)n0 * 2 : (int64_t)n0 * ldb2);
   const int64_t b_kstep = NN ? 64 * ldb2 : 128;
-  auto issue = [&](int kt, int s) __attribute__((always_inline)) {
-    char* st = smem + s * CF::STAGE;
-    dma_run<APW>(a_base + (int64_t)kt * 128, oa, lds_addr(st + wave * APW * 1024));
-    dma_run<BPW>(b_base + (int64_t)kt * b_kstep, ob, lds_addr(st + CF::A_BYTES + wave * BPW * 1024));
+  auto issue_a = [&](int kt) __attribute__((always_inline)) {
+    dma_run<APW>(a_base + (int64_t)kt * 128, oa, lds_addr(smem + (kt % NA) * CF::A_BYTES + wave * APW * 1024));
+  };
+  auto issue_b = [&](int kt) __attribute__((always_inline)) {
+    dma_run<BPW>(b_base + (int64_t)kt * b_kstep, ob,
+                 lds_addr(smem + CF::B_OFF + (kt % NB) * CF::B_BYTES + wave * BPW * 1024));
   };
 
   // ---- fragment reads (16x16x32 operand: lane l holds mn = base + (l & 15), k = 8 (l >> 4) .. +7) ----
@@ -176,24 +181,29 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // NS-stage ring: k-tile kt lives in stage kt % NS; NS - 1 k-tiles are in flight while one is
-  // consumed.  The wait at the top of iteration kt leaves the DMAs of k-tiles kt+1 .. kt+NS-2
-  // (NPW instructions each) outstanding.
+  // Rings: k-tile kt's A in A-stage kt % NA, its B in B-stage kt % NB.  After the barrier of
+  // iteration kt every wave is done with k-tile kt - 1, so A(kt + NA - 1) and B(kt + NB - 1) go into
+  // the stages it used -- issued B first, then A, so the wait at the top of the next iteration can
+  // leave exactly the A k-tiles beyond it in flight (APW instructions each; vmcnt counts in order).
   constexpr int NPW = APW + BPW;
 #pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (i < KT) issue(i, i);
+  for (int i = 0; i < NA - 1; ++i) {
+    if (i < KT) issue_a(i);
+    if (i < NB - 1 && i < KT) issue_b(i);
+  }
   for (int kt = 0; kt < KT; ++kt) {
-    if constexpr (NS == 3) {
+    if constexpr (NA == 3 && NB == 3) {
       if (kt + 1 < KT) fa::wait_vm<NPW>(); else fa::wait_vm<0>();
+    } else if constexpr (NA == 3) {
+      if (kt + 1 < KT) fa::wait_vm<APW>(); else fa::wait_vm<0>();
     } else {
       fa::wait_vm<0>();
     }
-    fa::raw_barrier();  // k-tile kt visible to every wave; every wave is done with stage (kt - 1) % NS
-    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
-    const char* st = smem + (kt % NS) * CF::STAGE;
-    const char* ai = st;
-    const char* bi = st + CF::A_BYTES;
+    fa::raw_barrier();  // k-tile kt visible to every wave; every wave is done with k-tile kt - 1
+    if (kt + NB - 1 < KT) issue_b(kt + NB - 1);
+    if (kt + NA - 1 < KT) issue_a(kt + NA - 1);
+    const char* ai = smem + (kt % NA) * CF::A_BYTES;
+    const char* bi = smem + CF::B_OFF + (kt % NB) * CF::B_BYTES;
     // GP_PRE: both k-steps' fragments are read up front (the second k-step's reads fly under the
     // first k-step's MFMAs); else each k-step reads, then multiplies
     u32x4 fa_[2][MT], fb_[2][NT];
@@ -266,7 +276,8 @@ __global__ __launch_bounds__(BM == 256 ? 512 : 256) void gemm_proj_kernel(ProjAr
 // (NN needs BN = 128).  Returns -3 when the shape / layout is not eligible, or (force = 0) when
 // the library GEMM is measured faster for the shape; the caller then runs that.
 // force: 0 auto (kernel or library), 1 kernel with the automatic tile, 2.. one tile configuration
-// (A/B: 2 = 64x64, 3 = 64x128, 4 = 128x128, 5 = 128x128 with a 3-stage ring, 6 = 256x128).
+// (A/B: 2 = 64x64, 3 = 64x128, 4 = 128x128, 5 = 128x128 with a 3-stage ring, 6 = 256x128,
+// 7 = 128x128 with the 3-stage A ring beside a 2-stage B ring).
 extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, int force, hipStream_t st) {
   using namespace xdot;
   if (dt != DT_BF16 && dt != DT_F16) return -3;
@@ -278,14 +289,14 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, in
   int cfg;  // 2..6 as force
   if (force >= 2) {
     cfg = force;
-    if (cfg > 6 || (cfg == 2 && nn) || (cfg >= 3 && a->N % 128)) return -3;
+    if (cfg > 7 || (cfg == 2 && nn) || (cfg >= 3 && a->N % 128)) return -3;
   } else {
     if (GP_HUGE && a->N % 128 == 0 && tiles(256, 128) >= 1024) cfg = 6;
     else if (GP_BIG && a->N % 128 == 0 && tiles(128, 128) >= 512) cfg = 4;
     else if (a->N % 128 == 0 && (nn || tiles(64, 128) >= 512)) cfg = 3;
     else cfg = 2;
   }
-  const int bm = cfg == 6 ? 256 : (cfg >= 4 ? 128 : 64), bn = cfg == 2 ? 64 : 128;
+  const int bm = cfg == 6 ? 256 : (cfg >= 4 ? 128 : 64), bn = cfg == 2 ? 64 : 128;  // (cfg 7: 128x128)
   const int64_t grid = tiles(bm, bn);
   if (grid > 0x7FFFFFFF) return -3;
   const bool bias = a->bias != nullptr;
@@ -301,12 +312,14 @@ extern "C" int xdot_gemm_proj_launch(const xdot::ProjArgs* a, int dt, int nn, in
 #define GPD(BMV, BNV, NNV, NSV) \
   if (dt == DT_BF16) { GPB(DT_BF16, BMV, BNV, NNV, NSV); } else { GPB(DT_F16, BMV, BNV, NNV, NSV); }
   if (nn) {
-    if (cfg == 6) { GPD(256, 128, true, 2); }
+    if (cfg == 7) { GPD(128, 128, true, 32); }
+    else if (cfg == 6) { GPD(256, 128, true, 2); }
     else if (cfg == 5) { GPD(128, 128, true, 3); }
     else if (cfg == 4) { GPD(128, 128, true, 2); }
     else { GPD(64, 128, true, 2); }
   } else {
-    if (cfg == 6) { GPD(256, 128, false, 2); }
+    if (cfg == 7) { GPD(128, 128, false, 32); }
+    else if (cfg == 6) { GPD(256, 128, false, 2); }
     else if (cfg == 5) { GPD(128, 128, false, 3); }
     else if (cfg == 4) { GPD(128, 128, false, 2); }
     else if (cfg == 3) { GPD(64, 128, false, 2); }

@@ -147,34 +147,6 @@ def test_flash_f32_score_buffer_checks(gpu):
         flash.fwd(rows.bfloat16(), kc.bfloat16(), kc.bfloat16(), None, 2, 0.1, sbuf=torch.empty(n, device=gpu))
 
 
-@pytest.mark.parametrize("beside", ["dq"])
-def test_module_fp32_dv_pass_schedule(gpu, monkeypatch, beside):
-    """XDOT_FP32_DV_BESIDE: the exact-fp32 dV pass on a third stream beside the dQ pass gives the
-    same loss and gradients, bitwise, as the default (dV beside the row kernel), twice in a row."""
-    import xdot
-    from xdot.utils.comm import LocalComm, use_comm
-    from xdot.utils.env import FLAGS
-
-    def run(sched):
-        monkeypatch.setattr(FLAGS, "fp32_dv_beside", sched)
-        torch.manual_seed(0)
-        with use_comm(LocalComm()):
-            m = xdot.DistributedDotProductAttn(384, num_heads=4, add_bias=True).to(gpu)
-            x = torch.randn(1, 900, 384, device=gpu, requires_grad=True)
-            mask = torch.rand(1, 900, 900, device=gpu) < 0.2
-            mask[..., 0] = False
-            loss = m(x, x, x, mask).square().sum()
-            loss.backward()
-        return loss.detach(), [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
-
-    la, a = run("rows")
-    for _ in range(2):
-        lb, b = run(beside)
-        assert torch.equal(la, lb)
-        for u, v in zip(a, b):
-            assert torch.equal(u, v)
-
-
 def test_module_fp32_score_buffer_matches_recompute(gpu):
     """The fp32 module with the score buffer (default) and without (XDOT_FP32_SCORES=0) gives
     bitwise equal outputs and gradients, twice in a row (determinism), and a retained graph's

@@ -621,15 +621,7 @@ class SeqParallelAttention(torch.autograd.Function):
                     "recomputes an fp32 head this wide); set XDOT_FP32_SCORES_DS=1 with room for the "
                     "separate dS buffer, or do not retain the graph")
             ev_cols = None
-            # XDOT_FP32_DV_BESIDE=dq: the dV pass on a third stream beside the dQ pass; their shared
-            # output is allocated on `hi` BEFORE the prep event, so every earlier use of its memory is
-            # ordered before the third stream's first kernel
-            dv_dq = (FLAGS.fp32_dv_beside == "dq" and hi is not cur and sbuf is not None and dsbuf is not None
-                     and len(bufs) == 1)
             with _on_stream(hi, cur):
-                pre_dkv = None
-                if dv_dq:
-                    pre_dkv = torch.empty((B, bufs[0].shape[1], 2 * C), dtype=torch.float32, device=k.device)
                 delta, lse2 = flash.bwd_prep(do, o, lse, H)  # one prep pass for both kernels
                 ev = _prep_event(hi.device)
                 ev.record(hi)
@@ -644,26 +636,15 @@ class SeqParallelAttention(torch.autograd.Function):
                                  fp32_mode=ctx.fp32_mode, sbuf=sbuf)
                     if dsbuf is not None and sbuf is not None:
                         # dQ pass (S -> dS), then the row kernel (reads dS) on `cur` concurrently
-                        # with the dV pass (reads S) here -- or (XDOT_FP32_DV_BESIDE=dq) the dV pass on
-                        # a third stream beside the dQ pass from the start (dS goes to its own buffer,
-                        # so the two passes only share reads of S)
-                        if dv_dq:  # fp32 only: the gradient halves are fp32 either way
-                            dvs = _side_stream(do.device, 0, "dv")
-                            dvs.wait_event(ev)  # δ / lse2 ready (the prep pass on `hi`)
-                            with _on_stream(dvs, hi):
-                                flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                               dsbuf=dsbuf, passes=1, out_dkv=pre_dkv, **cargs)
-                            for t in (pre_dkv, delta, lse2, do, o, lse, sbuf):
-                                t.record_stream(dvs)
+                        # with the dV pass (reads S) here.  (The dV pass beside the dQ pass on a third
+                        # stream instead measured 54.62 vs 54.71 ms, and one rep ran 171 ms:
+                        # profiles/r6_fp32.md)
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                                dsbuf=dsbuf, passes=2, out_dkv=pre_dkv, **cargs)
+                                                dsbuf=dsbuf, passes=2, **cargs)
                         ev_cols = torch.cuda.Event()
                         ev_cols.record(hi)
-                        if dv_dq:
-                            hi.wait_stream(dvs)  # the reduce-scatter below needs both halves
-                        else:
-                            flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                           dsbuf=dsbuf, passes=1, out_dkv=dkv, **cargs)
+                        flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
+                                       dsbuf=dsbuf, passes=1, out_dkv=dkv, **cargs)
                     else:
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
                                                 dsbuf=dsbuf, **cargs)

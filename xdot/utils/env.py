@@ -69,9 +69,6 @@ variable                    default   effect
 ``XDOT_WGRAD_PAIR``         1         the fused backward's dWk and dW[q|v] in one launch (A/B knob)
 ``XDOT_ROWS_SPLIT``         0         column splits of the fused backward's row-side kernel (0: the
                                       launcher's occupancy model; A/B knob)
-``XDOT_FP32_DV_BESIDE``      rows      with S and dS buffers, the fp32 column side's dV pass runs beside the
-                                      row kernel (``rows``: after the dQ pass) or beside the dQ pass
-                                      (``dq``: on a third stream from the start of the backward)
 ``XDOT_F32_PROJ``           1         exact-fp32 projections / weight gradients on the exact-fp32 GEMM kernels (both fp32 modes)
                                       (0: the library's fp32 GEMM)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
@@ -160,7 +157,6 @@ class _Flags:
         self.fp32_scores = _flag("XDOT_FP32_SCORES", default="1")
         self.fp32_scores_frac = _num("XDOT_FP32_SCORES_FRAC", 0.5)
         self.fp32_scores_dsbuf = _flag("XDOT_FP32_SCORES_DS", default="1")
-        self.fp32_dv_beside = _str("XDOT_FP32_DV_BESIDE", "rows")
         self.fp32_ds_only = _str("XDOT_FP32_DS_ONLY", "split")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
