@@ -699,7 +699,10 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   float* dsb = sbuf_ptr(dsbuf, g, H, rows, fp32_mode, "xdot.flash_bwd_cols (dS buffer)");
   // a dS buffer alone: dS-only mode (the recomputing column kernel stores dS, D <= 128)
   TORCH_CHECK(!dsb || sb || g.D <= 128, "xdot.flash_bwd_cols: a dS buffer without the score buffer needs D <= 128");
-  TORCH_CHECK(passes >= 1 && passes <= 3 && (passes == 3 || (sb && dsb)),
+  // passes 4: the fused exact-fp32 column pass (dQ and dV in one kernel); other families run both
+  // passes (3) instead
+  if (passes == 4 && (!sb || fp32_mode != 0 || g.D > 128 || rows.scalar_type() != at::kFloat)) passes = 3;
+  TORCH_CHECK(passes >= 1 && passes <= 4 && (passes >= 3 || (sb && dsb)),
               "xdot.flash_bwd_cols: single passes (1 = dV, 2 = dQ) need the score and dS buffers");
   TORCH_CHECK(out.sizes() == rows.sizes() && out.is_contiguous() && out.scalar_type() == rows.scalar_type(),
               "xdot.flash_bwd_cols: out shape/dtype");
@@ -754,7 +757,7 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
   if (dt != xdot::DT_F32 || g.D > 128 || (!a.prescaled && !a.dkv16)) {
     int sq = 1, sv = 1;  // (the single-pass recompute kernels use sq for both halves: sv == sq there)
     TORCH_CHECK(xdot_flash_cols_splits(&a, dt, (int)g.D, &sq, &sv) == 0, "xdot.flash_bwd_cols: split config");
-    const bool run_q = !sb || (passes & 2), run_v = !sb || (passes & 1);
+    const bool run_q = !sb || passes == 4 || (passes & 2), run_v = !sb || passes == 4 || (passes & 1);
     if (run_q && sq > 1) {
       cpq = at::empty({sq, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
       a.cpq = cpq.data_ptr<float>();

@@ -503,7 +503,9 @@ __global__ __launch_bounds__(256, D >= 128 ? 1 : 2) void bwd_rows_kernel(BwdArgs
 // DS (dS-only buffer mode, recompute kernel): S recomputed as without a buffer, dS stored into
 // a.dsbuf for the row kernel (the split family's memory-bound mode: 40 GB of score traffic per
 // step instead of 100)
-template <int D, bool LS, bool DS = LS>
+// DV (with LS: the fused column pass, BwdArgs::sb_passes == 4): dV = Σ_rows Pᵀ · dO is accumulated here
+// too, from the P this pass computes anyway -- three products per tile, S read once, no dV pass
+template <int D, bool LS, bool DS = LS, bool DV = !LS>
 __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(BwdArgs a) {
   using CF = Cfg<D>;
   constexpr int DB = CF::DB;
@@ -540,23 +542,28 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
                   : nullptr;
   const int64_t dstep = sown ? (int64_t)NKT32 * 1024 : 0;
   const int64_t sstep = (int64_t)NKT32 * 1024;
+  // S of the next tile prefetched into registers (the fused pass has no room for the second set:
+  // it loads each tile's S at the tile's top, issued last, landing under the dP product)
+  constexpr bool PF = LS && !DV;
   f32x16 snext{};
-  if (LS && rt_beg < rt_end) snext = blk_load(sbc + rt_beg * sstep, lane);
+  if (PF && rt_beg < rt_end) snext = blk_load(sbc + rt_beg * sstep, lane);
   const float* kb = reinterpret_cast<const float*>(a.rows) + (int64_t)b * a.R * C + h * D;
   const float* db_ = reinterpret_cast<const float*>(a.dout) + (int64_t)b * a.R * C + h * D;
   const float* lse2 = a.lse2 + ((int64_t)b * a.H + h) * a.R;
   const float* dlt = a.delta + ((int64_t)b * a.H + h) * a.R;
   const float c2 = a.scale * LOG2E, NEG_INF = -__builtin_inff();
-  f32x16 dq[DB], dv[LS ? 1 : DB];
+  f32x16 dq[DB], dv[DV ? DB : 1];
 #pragma unroll
   for (int i = 0; i < DB; ++i) dq[i] = f32x16{};
-  if constexpr (!LS) {
+  if constexpr (DV) {
 #pragma unroll
     for (int i = 0; i < DB; ++i) dv[i] = f32x16{};
     // loop-carried accumulators live in AGPRs (unpinned they sit in VGPRs and are copied into
     // AGPRs and back around every trprod: ~4 VALU moves per MFMA, VALU/MFMA 4.3 measured)
-    fa::pin_agpr(dq);
-    fa::pin_agpr(dv);
+    if constexpr (!LS) {  // (the fused pass at two waves per SIMD leaves the split to the allocator)
+      fa::pin_agpr(dq);
+      fa::pin_agpr(dv);
+    }
   }
 
   // row constants of a tile: lse2 (+inf past R: P = 0) and δ, by threads 0..63
@@ -580,12 +587,13 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   for (int rt = rt_beg; rt < rt_end; ++rt) {
     const bool more = rt + 1 < rt_end;
     f32x16 scur;
-    if constexpr (LS) scur = snext;
+    if constexpr (PF) scur = snext;
     if (more) {
       dm.issue(kdb, C, (int64_t)(rt + 1) * 32, a.R - 1 - (rt + 1) * 32, sm + ((rt + 1 - rt_beg) & 1) * CF::STAGE, CF::IMG);
       ax = aux_load(rt + 1);
-      if constexpr (LS) snext = blk_load(sbc + (rt + 1) * sstep, lane);
+      if constexpr (PF) snext = blk_load(sbc + (rt + 1) * sstep, lane);
     }
+    if constexpr (LS && !PF) scur = blk_load(sbc + rt * sstep, lane);
     const float* ki = sm + ((rt - rt_beg) & 1) * CF::STAGE;
     const float* di = ki + CF::IMG;
     const float* ls = ki + 2 * CF::IMG;  // lse2[32], δ[32]
@@ -615,9 +623,9 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     // scatters per lane straight into the row kernel's order, before the dQ product
     if constexpr (DS) fa::blk_store(dsc + rt * dstep, dp, lane);
     if (flag != 1) {
-      if constexpr (!LS) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
-      trprod<D>(ki, dp, dq, lane);                     // dQᵀ += Kᵀ · dS
-      if constexpr (!LS) {
+      if constexpr (DV) trprod<D>(di, s, dv, lane);  // dVᵀ += dOᵀ · P
+      trprod<D>(ki, dp, dq, lane);                    // dQᵀ += Kᵀ · dS
+      if constexpr (DV && !LS) {
         fa::pin_agpr(dq);
         fa::pin_agpr(dv);
       }
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
     for (int g = 0; g < 4; ++g) {
       *reinterpret_cast<f32x4*>(pq + db * 32 + 8 * g + 4 * hf) =
           f32x4{dq[db][4 * g] * sc, dq[db][4 * g + 1] * sc, dq[db][4 * g + 2] * sc, dq[db][4 * g + 3] * sc};
-      if constexpr (!LS)
+      if constexpr (DV)
         *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
             f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
     }
@@ -934,6 +942,14 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   auto sum_v = [&](int s) {
     if (s > 1) xdot_flash_cols_sum_launch(a->cpv, a->dvc, s, rows, C, a->ldg, xdot::DT_F32, st);
   };
+  if (a->sbuf && a->sb_passes == 4) {  // fused: dP, dQ and dV in one pass (S -> dS)
+#define L(DV)                                                                                                  \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, true, true, true>), dim3(W * sq), dim3(256), lds_bytes_ds<DV>(), st, *a); \
+  sum_q();                                                                                                       \
+  sum_v(sq)
+    XF32_DISPATCH(L)
+#undef L
+  }
   if (a->sbuf) {  // in place: dV from S first, then dQ (S -> dS); with a dS buffer dQ first
     const int ps = a->sb_passes ? a->sb_passes : 3;
     const bool dv_first = !a->dsbuf;
@@ -983,7 +999,9 @@ template <int D> void f32_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
   using namespace xdot::fa32;
   const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H;
   const int NRT = (a->R + 31) / 32, cus = xdot_num_cus();
-  if (a->sbuf) {
+  if (a->sbuf && a->sb_passes == 4) {
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true, true, true>, lds_bytes_ds<D>()));
+  } else if (a->sbuf) {
     *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_ds<D>()));
     *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, 2 * (Cfg<D>::IMG + 32) * 4));
   } else if (a->dsbuf) {

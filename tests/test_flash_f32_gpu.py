@@ -104,12 +104,13 @@ def test_flash_f32_column_split(gpu, nsplit):
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("mask_kind", ["none", "random", "blocks"])
 @pytest.mark.parametrize("nsplit", [0, 3])
-@pytest.mark.parametrize("direct", [False, True])
-def test_flash_f32_score_buffer_bitwise(gpu, monkeypatch, case, mask_kind, nsplit, direct):
+@pytest.mark.parametrize("direct,passes", [(False, 3), (True, 3), (True, 4)])
+def test_flash_f32_score_buffer_bitwise(gpu, monkeypatch, case, mask_kind, nsplit, direct, passes):
     """Reading S / dS from the score buffer instead of recomputing them changes nothing: the
     forward, both backward kernels and the column-split partials are BITWISE equal to the
     recompute path (same MFMA chains), which the fp64 test above bounds.  ``direct``: the forward
-    scatters S straight to the buffer (XDOT_F32_FWD_DIRECT=1, three workgroups per CU)."""
+    scatters S straight to the buffer (XDOT_F32_FWD_DIRECT=1, three workgroups per CU); ``passes``
+    4: the fused column pass (dP, dQ and dV in one kernel, S -> dS in place)."""
     from xdot.ops import flash
 
     monkeypatch.setenv("XDOT_F32_FWD_DIRECT", "1" if direct else "0")
@@ -125,7 +126,7 @@ def test_flash_f32_score_buffer_bitwise(gpu, monkeypatch, case, mask_kind, nspli
     dr1 = flash.bwd_rows(do, rows, kb, vb, l1, dl1, mk, H, scale, nsplit=nsplit, fp32_mode=0)
     sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)  # no stale zeros
     o2, l2 = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=nsplit, fp32_mode=0, sbuf=sb)
-    dkv2, dl2 = flash.bwd_cols(do, rows, kb, vb, o2, l2, mk, H, scale, fp32_mode=0, sbuf=sb)
+    dkv2, dl2 = flash.bwd_cols(do, rows, kb, vb, o2, l2, mk, H, scale, fp32_mode=0, sbuf=sb, passes=passes)
     dr2 = flash.bwd_rows(do, rows, kb, vb, l2, dl2, mk, H, scale, nsplit=nsplit, fp32_mode=0, sbuf=sb)
     assert torch.equal(o1, o2) and torch.equal(l1, l2)
     assert torch.equal(dkv1, dkv2), f"d cols {_rel(dkv2, dkv1):.2e}"
@@ -145,6 +146,35 @@ def test_flash_f32_score_buffer_checks(gpu):
             flash.fwd(rows, kc, kc, None, 2, 0.1, fp32_mode=fm, sbuf=torch.empty(n - 1, device=gpu))
     with pytest.raises(RuntimeError, match="fp32"):
         flash.fwd(rows.bfloat16(), kc.bfloat16(), kc.bfloat16(), None, 2, 0.1, sbuf=torch.empty(n, device=gpu))
+
+
+def test_module_fp32_fused_cols(gpu, monkeypatch):
+    """XDOT_F32_FUSED_COLS=1 (one fused column pass, one in-place score buffer) at a shape with
+    column row splits: loss and gradients within 1e-6 of the two-pass default, fp64-bounded like
+    the rest, and deterministic run to run."""
+    import xdot
+    from xdot.utils.comm import LocalComm, use_comm
+    from xdot.utils.env import FLAGS
+
+    def run(fused):
+        monkeypatch.setattr(FLAGS, "f32_fused_cols", fused)
+        torch.manual_seed(0)
+        with use_comm(LocalComm()):
+            m = xdot.DistributedDotProductAttn(384, num_heads=4, add_bias=True).to(gpu)
+            x = torch.randn(1, 2600, 384, device=gpu, requires_grad=True)
+            mask = torch.rand(1, 2600, 2600, device=gpu) < 0.2
+            mask[..., 0] = False
+            loss = m(x, x, x, mask).square().mean()
+            loss.backward()
+        return loss.detach(), [p.grad.clone() for p in m.parameters()] + [x.grad.clone()]
+
+    la, a = run(False)
+    lb, b = run(True)
+    lc, c = run(True)
+    assert torch.equal(lb, lc) and all(torch.equal(u, v) for u, v in zip(b, c))
+    assert _rel(lb, la) <= 1e-6
+    for u, v in zip(a, b):
+        assert _rel(v, u) <= 1e-6
 
 
 def test_module_fp32_score_buffer_matches_recompute(gpu):

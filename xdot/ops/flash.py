@@ -230,12 +230,20 @@ def score_buffer(B: int, H: int, R: int, T: int, device) -> Optional[torch.Tenso
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
-def score_buffers(B: int, H: int, R: int, T: int, device):
+def fused_cols_wanted(fp32_mode: int, D: int) -> bool:
+    """The exact-fp32 backward's column side as ONE fused pass (dP, dQ and dV per tile, S
+    overwritten with dS in place; ``XDOT_F32_FUSED_COLS``) instead of a dQ pass and a dV pass:
+    exact family, D <= 128."""
+    return FLAGS.f32_fused_cols and fp32_mode == 0 and D <= 128
+
+
+def score_buffers(B: int, H: int, R: int, T: int, device, dsbuf: bool = True):
     """(S buffer, dS buffer) for the backward's concurrent schedule, (S buffer, None) for the
     in-place one, or None (recompute): like :func:`score_buffer`, the dS buffer only when both fit
     within ``XDOT_FP32_SCORES_FRAC`` of the free device memory.  With a separate dS buffer the
     column side runs its dQ pass first (S -> dS), then its dV pass (reads S) CONCURRENTLY with the
-    row kernel (reads dS): two one-product kernels side by side instead of back to back."""
+    row kernel (reads dS): two one-product kernels side by side instead of back to back.
+    ``dsbuf=False``: the S buffer only (in place)."""
     if not FLAGS.fp32_scores:
         return None
     n = score_buffer_numel(B, H, R, T)
@@ -243,7 +251,7 @@ def score_buffers(B: int, H: int, R: int, T: int, device):
     free, _ = torch.cuda.mem_get_info(dev)
     cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
     room = FLAGS.fp32_scores_frac * (free + cached)
-    if 8 * n <= room and FLAGS.fp32_scores_dsbuf:
+    if 8 * n <= room and FLAGS.fp32_scores_dsbuf and dsbuf:
         both = torch.empty(2 * n, dtype=torch.float32, device=dev)
         return both[:n], both[n:]
     if 4 * n <= room:

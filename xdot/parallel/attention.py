@@ -513,7 +513,9 @@ class SeqParallelAttention(torch.autograd.Function):
                 if dsbuf is not None:
                     segmented = False
             else:
-                sbs = flash.score_buffers(B, H, R, n * qv.shape[1], k.device)
+                # the fused exact column pass overwrites S with dS in place: no second buffer
+                sbs = flash.score_buffers(B, H, R, n * qv.shape[1], k.device,
+                                          dsbuf=not flash.fused_cols_wanted(fm, D))
                 if sbs is not None:
                     sbuf, dsbuf = sbs
                     segmented = False
@@ -646,8 +648,10 @@ class SeqParallelAttention(torch.autograd.Function):
                         flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
                                        dsbuf=dsbuf, passes=1, out_dkv=dkv, **cargs)
                     else:
+                        # (fused exact pass: dP, dQ and dV in one kernel, S -> dS in place)
+                        fused = sbuf is not None and dsbuf is None and flash.fused_cols_wanted(ctx.fp32_mode, C // H)
                         dkv, _ = flash.bwd_cols(do, k, g[..., :C], g[..., C:], o, lse, mks[0], H, scale, delta,
-                                                dsbuf=dsbuf, **cargs)
+                                                dsbuf=dsbuf, passes=4 if fused else 3, **cargs)
                         if sbuf is not None or dsbuf is not None:  # the row kernel reads the dS this kernel wrote
                             ev_cols = torch.cuda.Event()
                             ev_cols.record(hi)

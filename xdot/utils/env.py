@@ -50,6 +50,10 @@ variable                    default   effect
 ``XDOT_FP32_SCORES_FRAC``   0.5       ... only when that fits this fraction of the free device memory
 ``XDOT_FP32_SCORES_DS``     1         ... and a second buffer for dS when both fit: the column side's
                                       dV pass then runs concurrently with the row kernel
+``XDOT_F32_FUSED_COLS``      1         exact fp32, D <= 128: the column side as ONE fused pass (dP, dQ, dV per
+                                      tile; S overwritten with dS in place, one score buffer) instead
+                                      of a dQ pass and a dV pass (step 51.5-51.9 -> 50.1 ms, one box;
+                                      profiles/r6_fp32.md)
 ``XDOT_FP32_DS_ONLY``       split     fp32 families that keep only the dS buffer (the forward stores
                                       nothing, the single-pass column kernel recomputes S and stores
                                       dS, the row kernel reads it: 40 GB of score traffic per step
@@ -157,6 +161,7 @@ class _Flags:
         self.fp32_scores = _flag("XDOT_FP32_SCORES", default="1")
         self.fp32_scores_frac = _num("XDOT_FP32_SCORES_FRAC", 0.5)
         self.fp32_scores_dsbuf = _flag("XDOT_FP32_SCORES_DS", default="1")
+        self.f32_fused_cols = _flag("XDOT_F32_FUSED_COLS", default="1")
         self.fp32_ds_only = _str("XDOT_FP32_DS_ONLY", "split")
         self.fused_module = _flag("XDOT_FUSED_MODULE", default="1")
         self.wgrad_side = _flag("XDOT_WGRAD_SIDE", default="0")
