@@ -91,7 +91,9 @@ def main():
         assert sb is not None, "score buffer does not fit"
     # (timing only: after the first bwd_cols the buffer holds dS, which later calls read as S)
     out, lse = flash.fwd(rk, kc, vc, mk, H, scale, a.nsplit, prescaled=ps, sbuf=sb)
-    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb)
+    # score-buffer mode: the fused exact column pass where the module uses it (XDOT_F32_FUSED_COLS)
+    cpasses = 4 if sb is not None and flash.fused_cols_wanted(flash.fp32_code(dt), D) else 3
+    dkv, delta = flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb, passes=cpasses)
     gemm = 2.0 * B * R * T * H * D
     np_cols, np_rows = (3, 1) if sb is not None else (4, 3)
     res = []
@@ -103,8 +105,8 @@ def main():
         res.append({"kernel": "flash_fwd" + ("+S" if sb is not None else ""), "ms": ms, "min_ms": mn,
                     "TFLOPs": 2 * gemm / ms / 1e9})
     if a.only in ("all", "bwd_cols"):
-        ms, mn = timeit(lambda: flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb),
-                        a.iters)
+        ms, mn = timeit(lambda: flash.bwd_cols(do, rk, kc, vc, out, lse, mk, H, scale, prescaled=ps, sbuf=sb,
+                                               passes=cpasses), a.iters)
         res.append({"kernel": "flash_bwd_cols" + ("(S->dS)" if sb is not None else ""), "ms": ms, "min_ms": mn,
                     "TFLOPs": np_cols * gemm / ms / 1e9})
     if a.only in ("all", "bwd_rows"):

@@ -244,10 +244,13 @@ class GradSync:
                 self.comm.all_reduce_multi(grads, op=op, async_op=True)
             self._handles.append((i, grads, h, nat))
             return
-        # converted straight into the flat buffer (one multi-tensor copy, not a cast + a cat per
-        # gradient: the fp32 reduce of bf16 gradients launched ~3 small kernels per parameter)
+        # converted straight into the flat buffer, one full-grid conversion kernel per gradient
+        # (torch._foreach_copy_'s multi-tensor kernel ran ~14 us per 768 x 768 gradient on MI355X,
+        # a few blocks per tensor: 8 of them were 110 us of the emulated N=8 rank step,
+        # profiles/r6_rank.md)
         flat = torch.empty(sum(p.numel() for p in b), dtype=rdt, device=g0.device)
-        torch._foreach_copy_(_views(flat, b), [p.grad for p in b])
+        for v, p in zip(_views(flat, b), b):
+            v.copy_(p.grad)
         h = self.comm.all_reduce(flat, op=op, async_op=True)
         self._handles.append((i, flat, h, nat))
 
@@ -283,8 +286,8 @@ class GradSync:
                 continue
             if self.op == "avg" and not nat:
                 flat.div_(ws)
-            b = self.buckets[i]
-            torch._foreach_copy_([p.grad for p in b], _views(flat, b))
+            for p, v in zip(self.buckets[i], _views(flat, self.buckets[i])):
+                p.grad.copy_(v)
         if split:
             rest = self._outside_params(optimizer)
             optimizer.step(params=list(self.buckets[self._handles[last][0]]) + rest)
