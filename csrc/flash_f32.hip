@@ -140,6 +140,7 @@ __device__ __forceinline__ void load_frag(float (&f)[D / 2], const float* p, boo
 template <int D>
 __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D / 2], f32x16 acc, int lane) {
   const float* p = img + (lane & 31) * Cfg<D>::P + 4 * (lane >> 5);
+  __builtin_amdgcn_s_setprio(1);  // the MFMA block at raised priority (step -0.2 ms, profiles/r6_fp32.md)
   f32x4 a0 = *reinterpret_cast<const f32x4*>(p);
 #pragma unroll
   for (int g = 0; g < D / 8; ++g) {
@@ -150,6 +151,7 @@ __device__ __forceinline__ f32x16 rowprod(const float* img, const float (&f)[D /
     __builtin_amdgcn_sched_barrier(0);
     a0 = a1;
   }
+  __builtin_amdgcn_s_setprio(0);
   return acc;
 }
 
@@ -165,6 +167,7 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
   // ring of PD + 1 operand sets: tile index s + PD is read while the MFMAs of s issue (the loop
   // is fully unrolled, so every ring slot is a compile-time register set)
   constexpr int PD = XDOT_F32_TRPD;
+  __builtin_amdgcn_s_setprio(1);  // the MFMA block at raised priority (step -0.2 ms, profiles/r6_fp32.md)
   float rr[PD + 1][DB];
   auto rd = [&](int s, float (&dst)[DB]) {
     const float* row = img + ((s & 3) + 8 * (s >> 2) + 4 * hf) * Cfg<D>::P + (lane & 31);
@@ -180,6 +183,7 @@ __device__ __forceinline__ void trprod(const float* img, const f32x16& x, f32x16
     for (int db = 0; db < DB; ++db) out[db] = mm(rr[s % (PD + 1)][db], x[s], out[db]);
     __builtin_amdgcn_sched_barrier(0);
   }
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // ------------------------------------------------------------------------------------------
