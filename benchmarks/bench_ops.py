@@ -55,24 +55,29 @@ def parse(argv=None):
     ap.add_argument("--p2p-gbps", type=float, default=None, help="emulated ring-hop link rate (GB/s, --emulate)")
     ap.add_argument("--schedule", default=None, choices=["gather", "ring"],
                     help="product schedule (default XDOT_OPS_SCHEDULE / gather); also used by the *_fb modes")
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu"],
+                    help="cpu: gloo ranks on the CPU even where a GPU is visible (BASELINE config 1)")
     ap.add_argument("--emulate", type=int, default=None, metavar="N",
                     help="run ONE rank of an N-rank job on this device (EmulatedComm: collectives are "
                          "device-local copies) -- per-rank compute of the reference's N=3 setup on 1 GPU")
     return ap.parse_args(argv)
 
 
+_CUDA = [torch.cuda.is_available()]  # the timed device (False with --device cpu)
+
+
 def _mem():
-    return torch.cuda.memory_allocated() if torch.cuda.is_available() else 0
+    return torch.cuda.memory_allocated() if _CUDA[0] else 0
 
 
 def _peak_reset():
-    if torch.cuda.is_available():
+    if _CUDA[0]:
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats()
 
 
 def _peak():
-    return torch.cuda.max_memory_allocated() if torch.cuda.is_available() else 0
+    return torch.cuda.max_memory_allocated() if _CUDA[0] else 0
 
 
 def cold_call(fn, *args):
@@ -90,7 +95,7 @@ def timed(fn, args, iters, warmup):
         fn(*args)
     ts = []
     for _ in range(iters):
-        if torch.cuda.is_available():
+        if _CUDA[0]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             fn(*args)
@@ -113,12 +118,14 @@ def main(argv=None):
     from xdot.utils import comm as C
     import xdot.parallel.functional as F
 
-    comm = C.EmulatedComm(a.emulate, link_gbps=a.link_gbps, p2p_gbps=a.p2p_gbps) if a.emulate else C.init("auto")
+    cpu = a.device == "cpu" or not torch.cuda.is_available()
+    _CUDA[0] = not cpu
+    comm = C.EmulatedComm(a.emulate, link_gbps=a.link_gbps, p2p_gbps=a.p2p_gbps) if a.emulate else \
+        C.init("gloo" if a.device == "cpu" else "auto", set_device=not cpu)
     ctx = C.use_comm(comm)  # the functional ops pick up the thread's communicator
     ctx.__enter__()
     n, rank = comm.world_size, comm.rank
-    dev = torch.device("cuda", C.get_local_rank() % max(1, torch.cuda.device_count())) \
-        if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device("cpu") if cpu else torch.device("cuda", C.get_local_rank() % max(1, torch.cuda.device_count()))
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[a.dtype]

@@ -6,7 +6,7 @@ O=gpurun_out/${1:-cfg}
 mkdir -p $O
 # 1. distributed_matmul_nt CPU/gloo world_size=2, T=256 d=64 offset=32 (plumbing, no GPU)
 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 \
-  benchmarks/bench_ops.py --mode nt --T 256 --dim 64 --offset 32 --iters 5 --warmup 1 > $O/c1_nt_gloo2.log 2>&1 || echo c1-failed >> $O/c1_nt_gloo2.log
+  benchmarks/bench_ops.py --mode nt --T 256 --dim 64 --offset 32 --iters 5 --warmup 1 --device cpu > $O/c1_nt_gloo2.log 2>&1 || echo c1-failed >> $O/c1_nt_gloo2.log
 echo c1
 # 2. DistributedDotProductAttn 1xMI355X, T=5000 d=768 heads=8 bf16
 timeout -k 10 200 python bench.py --seq-len 5000 --steps 50 --warmup 10 > $O/c2_attn_T5000.log 2>&1
