@@ -76,8 +76,8 @@ variable                    default   effect
 ``XDOT_F32_PROJ``           1         exact-fp32 projections / weight gradients on the exact-fp32 GEMM kernels (both fp32 modes)
                                       (0: the library's fp32 GEMM)
 ``XDOT_PROJ``               1         projection forward / input gradient on csrc/gemm_proj.hip
-                                      (1: where it beats the library, i.e. below 16384 rows;
-                                      2: every eligible shape; 0: library)
+                                      (1 / 2: every eligible shape, the 25000-row N=1 products
+                                      included since round 6; 0: library)
 ``XDOT_RING_OVERLAP``       auto      ring attention backward on two streams (auto: >= 1024 row
                                       tiles of 128 x heads)
 ``XDOT_RING_BIDIR``         1         ring attention: half of every block each way round the ring
