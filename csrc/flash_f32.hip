@@ -994,17 +994,21 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
 }
 
 namespace {
-// XDOT_CSPLIT: unset / "auto" = occupancy round model, "0" / "1" = no split, n = n splits (<= 4)
+// XDOT_CSPLIT: unset / "auto" = occupancy round model, "0" / "1" = no split, n = n splits (<= 8)
 int csplit_env() {
   const char* e = std::getenv("XDOT_CSPLIT");  // read per call (tests switch it)
-  return (!e || !*e || !std::strcmp(e, "auto")) ? -1 : std::max(1, std::min(4, std::atoi(e)));
+  return (!e || !*e || !std::strcmp(e, "auto")) ? -1 : std::max(1, std::min(8, std::atoi(e)));
 }
 template <int D> void f32_splits(const xdot::fa::BwdArgs* a, int* sq, int* sv) {
   using namespace xdot::fa32;
   const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H;
   const int NRT = (a->R + 31) / 32, cus = xdot_num_cus();
   if (a->sbuf && a->sb_passes == 4) {
-    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true, true, true>, lds_bytes_ds<D>()));
+    // up to 8 splits priced at 0.4 % each (as the fp32 forward): a split costs the fused pass two
+    // fp32 partial copies of the gathered-side gradient (~0.06 ms at T = 25000), its last-round
+    // tail ~1.4 ms at 4 splits
+    *sq = *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true, true, true>, lds_bytes_ds<D>()),
+                                      8, 0.004);
   } else if (a->sbuf) {
     *sq = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_kernel<D, true>, lds_bytes_ds<D>()));
     *sv = xdot::fa::pick_csplit(W, NRT, cus * xdot::fa::wg_per_cu(bwd_cols_dv_kernel<D>, 2 * (Cfg<D>::IMG + 32) * 4));
