@@ -6,7 +6,8 @@ NAME=$1; REV=$2; SRCS=$3
 python -m xdot.build > /dev/null
 B=build/variant_$NAME
 rm -rf $B; mkdir -p $B/src
-cp csrc/*.h $B/src/
+# headers from REV too (a header change is part of the variant)
+for h in $(git ls-tree --name-only $REV csrc/ | grep '\.h$'); do git show $REV:$h > $B/src/$(basename $h); done
 for SRC in $SRCS; do git show $REV:csrc/$SRC > $B/src/$SRC; done
 ABI=$(python -c "import torch; print(int(torch._C._GLIBCXX_USE_CXX11_ABI))")
 TLIB=$(python -c "import torch, os; print(os.path.join(os.path.dirname(torch.__file__), 'lib'))")
