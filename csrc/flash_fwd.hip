@@ -256,6 +256,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
       // 32-cycle MFMA gap is ~39 issue cycles): the exps of P's last 8 columns (pf[3]) move into
       // block B, whose MFMAs run k-step-major so pf[3] is first needed at MFMA 3*DB >= 9
       constexpr int NX = DB >= 3 ? 8 : 0, JA = 32 - NX;
+      // blocks A and B at raised issue priority, the row-max / rescale tail below at 0: a partner
+      // wave's MFMA blocks then win the SIMD over this wave's tail (step -0.5 %, profiles/r6_fp32.md)
+      __builtin_amdgcn_s_setprio(1);
       u32x4 pf[4];
       auto p_of = [&](int j) {
         sc[j >> 4][j & 15] = PS ? fast_exp2(sc[j >> 4][j & 15]) : fast_exp2(__builtin_fmaf(sc[j >> 4][j & 15], c2, -m_use));
@@ -307,6 +310,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         }
       }
       l_run += ls;
+      __builtin_amdgcn_s_setprio(0);
       if (flag_n != 0 || (kt + 2) * 64 > a.T) mask_tile(sn, kt + 1, flag_n, nxt);
       rescale_to(row_max(sn), sn);
     } else {
