@@ -45,7 +45,7 @@ def parse(argv=None):
                          "JSON line per N and a speed-up / efficiency summary line")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10,
-                    help="untimed steps first (10: about 1 %% faster timed steps than 3 on the same box, scripts/warm_ab.sh)")
+                    help="untimed steps first (10: about 1 %% faster timed steps than 3 on the same box, scripts/archive/warm_ab.sh)")
     ap.add_argument("--seq-len", type=int, default=25000, help="global T")
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--heads", type=int, default=8)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU verification pass (run via gpurun from the repo root):
 #   tests marked gpu -> bench.py -> rocprofv3 kernel stats of bench.py.
-# Usage: bash scripts/gpu_check.sh <tag> [pytest selector] [bench args...]
+# Usage: bash scripts/archive/gpu_check.sh <tag> [pytest selector] [bench args...]
 # Every GPU step has its own time limit; a failing/killed step stops the chain.
 set -o pipefail
 TAG=${1:-run}; SEL=${2:-tests}; shift 2 2>/dev/null

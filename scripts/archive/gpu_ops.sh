@@ -2,7 +2,7 @@
 # Reference per-op benchmark configs (benchmark_results/*.json: fp32, D=768, T=75000/scale, N=3)
 # on one MI355X: N=3 per-rank work via --emulate 3 (collectives are device-local copies) and
 # the whole problem on one GPU (N=1).  Records go to gpurun_out/ops/ops.json.
-# Usage (via gpurun): bash scripts/gpu_ops.sh
+# Usage (via gpurun): bash scripts/archive/gpu_ops.sh
 set -e
 O=gpurun_out/ops
 mkdir -p $O

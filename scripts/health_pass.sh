@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 health pass at HEAD: full GPU suite, smoke, default bench (bf16 + exact / split fp32
+# Health pass at HEAD: full GPU suite, smoke, default bench (bf16 + exact / split fp32
 # fields), masked / unmasked ratio (interleaved), BASELINE config 1 on gloo
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6final}; mkdir -p $OUT
