@@ -978,6 +978,45 @@ at::Tensor flash_prescale(const at::Tensor& x, double scale) {
   return out;
 }
 
+// dst[i] <- src[i] converted to dst[i]'s dtype (fp32 / bf16 / fp16), every pair in one launch per
+// CAST_MAX_T pairs (GradSync: 16-bit gradients <-> the fp32 buffers its all-reduce sums)
+void cast_multi(at::TensorList src, at::TensorList dst) {
+  Range rr_("xdot.cast_multi");
+  const size_t n = src.size();
+  TORCH_CHECK(dst.size() == n, "xdot.cast_multi: list sizes");
+  if (n == 0) return;
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda() && src[i].device() == dst[0].device() &&
+                    dst[i].device() == dst[0].device(),
+                "xdot.cast_multi: GPU tensors on one device");
+    TORCH_CHECK(src[i].is_contiguous() && dst[i].is_contiguous() && src[i].numel() == dst[i].numel(),
+                "xdot.cast_multi: contiguous tensors of equal numel");
+    TORCH_CHECK(dt_code(src[i].scalar_type()) >= 0 && dt_code(dst[i].scalar_type()) >= 0,
+                "xdot.cast_multi: fp32 / bf16 / fp16 only");
+  }
+  c10::DeviceGuard guard(dst[0].device());
+  for (size_t c0 = 0; c0 < n; c0 += xdot::CAST_MAX_T) {
+    xdot::CastArgs a{};
+    int blk = 0;
+    a.nt = (int)std::min<size_t>(xdot::CAST_MAX_T, n - c0);
+    for (int i = 0; i < a.nt; ++i) {
+      const size_t k = c0 + i;
+      a.src[i] = src[k].data_ptr();
+      a.dst[i] = dst[k].data_ptr();
+      a.n[i] = src[k].numel();
+      a.sdt[i] = dt_code(src[k].scalar_type());
+      a.ddt[i] = dt_code(dst[k].scalar_type());
+      a.blk0[i] = blk;
+      const int64_t nb = (a.n[i] + xdot::CAST_BLOCK_ELEMS - 1) / xdot::CAST_BLOCK_ELEMS;
+      TORCH_CHECK(blk + nb < (1LL << 31), "xdot.cast_multi: too many elements");
+      blk += (int)nb;
+    }
+    a.blk0[a.nt] = blk;
+    TORCH_CHECK(xdot_cast_multi_launch(&a, cur_stream(dst[0])) == 0, "xdot.cast_multi: dtype");
+    check_launch(hipGetLastError(), "cast_multi");
+  }
+}
+
 // one AdamW step for lists of same-dtype params / grads with fp32 moments (chunks of 32)
 void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_avg, at::TensorList exp_avg_sq,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
@@ -1430,6 +1469,7 @@ TORCH_LIBRARY(xdot, m) {
   m.def("flash_bwd_rows_sum(Tensor dpart, int H, Tensor like) -> Tensor");
   m.def("flash_fwd_merge(Tensor(a!) opart, Tensor lpart, Tensor(b!) lrun, int H) -> ()");
   m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
+  m.def("cast_multi(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
         "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
@@ -1497,6 +1537,7 @@ TORCH_LIBRARY_IMPL(xdot, CUDA, m) {
   m.impl("flash_fwd_merge", &flash_fwd_merge);
   m.impl("sum_partials_into", &sum_partials_into);
   m.impl("adamw_step", &adamw_step);
+  m.impl("cast_multi", &cast_multi);
   m.impl("ipc_all_gather", &ipc_all_gather);
   m.impl("ipc_reduce_scatter", &ipc_reduce_scatter);
 }

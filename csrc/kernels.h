@@ -134,6 +134,18 @@ struct AdamArgs {
   const float* step_dev[ADAM_MAX_T];
   const float* lr_dev;
 };
+// multi-tensor dtype conversion (csrc/optim.hip): dst[i] = (dst dtype) src[i] for up to CAST_MAX_T
+// tensor pairs per launch (GradSync's fp32 reduce buffers <-> 16-bit gradients)
+constexpr int CAST_MAX_T = 32;
+constexpr int CAST_BLOCK_ELEMS = 256 * 8;
+struct CastArgs {
+  const void* src[CAST_MAX_T];
+  void* dst[CAST_MAX_T];
+  int64_t n[CAST_MAX_T];
+  int sdt[CAST_MAX_T], ddt[CAST_MAX_T];
+  int blk0[CAST_MAX_T + 1];  // first block of each pair (prefix sum)
+  int nt;
+};
 // projection GEMM (csrc/gemm_proj.hip): C[M, N] = A[M, K] . op(B) (+ bias[N]); A k-contiguous,
 // B = W[N, K] (NT, forward) or W[K, N] (NN, input gradient), 16-bit, C row-major
 struct ProjArgs {
@@ -223,6 +235,8 @@ int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, 
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
 int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
+// a->nt conversions in one launch (DT_F32 / DT_BF16 / DT_F16 each side)
+int xdot_cast_multi_launch(const xdot::CastArgs* a, hipStream_t st);
 int xdot_mse_fwd_launch(const void* y, const void* t, void* dy, float* part, int nparts, void* loss, int64_t n, int dt,
                         hipStream_t st);
 // merge a->nsplit partial slots (a->opart, a->lpart) into a->out / a->lse

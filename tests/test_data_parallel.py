@@ -1,4 +1,5 @@
 """Replicated-parameter helpers: broadcast, bucketed Sum all-reduce, overlapped GradSync."""
+import pytest
 import torch
 
 from _dist import run_gloo
@@ -334,3 +335,89 @@ def test_gradsync_native_avg_matches_sum_then_divide(monkeypatch):
     for ra, rb in zip(a, b):
         for ga, gb in zip(ra, rb):
             torch.testing.assert_close(ga, gb, rtol=1e-6, atol=1e-7)
+
+
+def _wire_body(r, mode):
+    """Thread rank r of test_gradsync_fp32_wire_delivery (see there)."""
+    from xdot.parallel import GradSync
+    from xdot.utils import comm as C
+
+    W = C.get_comm().world_size
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 6, bias=False), torch.nn.Linear(6, 4, bias=False)).to(torch.bfloat16)
+    ps = list(m.parameters())
+    sync = GradSync(m, comm=C.get_comm(), bucket_mb=1.0 if mode == "flat" else 1e-5, reduce_dtype=torch.float32)
+
+    def g32(rank, p, salt):
+        g = torch.Generator().manual_seed(100 * rank + 10 * salt + p.shape[0])
+        return torch.randn(p.shape, generator=g) * (rank + 1)
+
+    pre = {}
+    if mode == "no_sync":  # a muted micro-batch first: delivered (and accumulated) in bf16
+        with sync.no_sync():
+            assert all(sync.wire_dtype(p) == torch.bfloat16 for p in ps)
+            sync.deliver([(p, g32(r, p, 1).to(torch.bfloat16)) for p in ps])
+        pre = {id(p): [g32(k, p, 1).to(torch.bfloat16).float() for k in range(W)] for p in ps}
+    assert all(sync.wire_dtype(p) == torch.float32 for p in ps)
+    if mode == "flat":  # one bucket: p0 on the fp32 wire, p1 in bf16 -> flattened, converted in one pass
+        sync.deliver([(ps[0], g32(r, ps[0], 2)), (ps[1], g32(r, ps[1], 2).to(torch.bfloat16))])
+    else:
+        sync.deliver([(p, g32(r, p, 2)) for p in ps])
+    sync.wait()
+    for i, p in enumerate(ps):
+        parts = [g32(k, p, 2) for k in range(W)]
+        if mode == "flat" and i == 1:
+            parts = [t.to(torch.bfloat16).float() for t in parts]
+        if id(p) in pre:
+            parts = [a + b for a, b in zip(parts, pre[id(p)])]
+        want = sum(parts[1:], parts[0]).to(torch.bfloat16)
+        assert p.grad is not None and p.grad.dtype == torch.bfloat16
+        torch.testing.assert_close(p.grad, want, rtol=0, atol=0)
+    return True
+
+
+@pytest.mark.parametrize("mode", ["inplace", "no_sync", "flat"])
+def test_gradsync_fp32_wire_delivery(mode):
+    """GradSync(reduce_dtype=fp32) with bf16 parameters: a fused node hands over fp32 weight
+    gradients (wire_dtype), which are all-reduced in place and written into p.grad once, rounded
+    from the fp32 sum; micro-batches accumulated under no_sync() are added in fp32; a bucket that
+    mixes a wire gradient with a bf16 one goes through the flat fp32 buffer.  Bitwise equal to
+    rounding the fp32 sum of every rank's contribution (3 thread ranks)."""
+    from xdot.utils import comm as C
+
+    assert all(C.ThreadGroup(3).run(lambda r: _wire_body(r, mode)))
+
+
+def _fused_wire_body(rank, ws):
+    """bf16 fused module under GradSync(reduce_dtype=fp32): its node hands fp32 weight gradients
+    over (wire_dtype) and the reduced p.grad matches an fp64 copy of the module + plain
+    allreduce_gradients to bf16 accuracy, for two steps."""
+    import xdot
+    from xdot.parallel import GradSync, allreduce_gradients, broadcast_parameters
+
+    torch.manual_seed(rank)
+    m1 = xdot.DistributedDotProductAttn(32, num_heads=4, impl="flash").double()
+    broadcast_parameters(m1)
+    m2 = xdot.DistributedDotProductAttn(32, num_heads=4, impl="flash").to(torch.bfloat16)
+    m2.load_state_dict({k: v.to(torch.bfloat16) for k, v in m1.state_dict().items()})
+    m1.load_state_dict({k: v.to(torch.bfloat16).double() for k, v in m2.state_dict().items()})
+    sync = GradSync(m2, bucket_mb=0.0001, reduce_dtype=torch.float32)
+    assert all(sync.wire_dtype(p) == torch.float32 for p in m2.parameters())
+    g = torch.Generator().manual_seed(17 + rank)
+    for step in range(2):
+        x = torch.rand(1, 8, 32, generator=g, dtype=torch.float64).to(torch.bfloat16)
+        for p in list(m1.parameters()) + list(m2.parameters()):
+            p.grad = None
+        m1(x.double(), x.double(), x.double(), None).square().sum().backward()
+        allreduce_gradients(m1)
+        m2(x, x, x, None).float().square().sum().backward()
+        assert len(sync._g32) == 4 and all(t.dtype == torch.float32 for t in sync._g32.values())
+        sync.wait()
+        for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            assert p2.grad is not None and p2.grad.dtype == torch.bfloat16, n2
+            err = float((p2.grad.double() - p1.grad).norm() / p1.grad.norm())
+            assert err < 3e-2, (step, n2, err)
+
+
+def test_gradsync_fused_module_fp32_wire_gloo():
+    run_gloo(_fused_wire_body, 2)

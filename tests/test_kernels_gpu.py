@@ -166,3 +166,24 @@ def test_all_row_chunking_gpu(gpu, dt, offset):
         assert out.dtype == dt
         tol = 1e-3 if dt == torch.float32 else 0.15
         assert (out.float() - ref).abs().max().item() < tol * ref.abs().max().item() ** 0.5, chunking
+
+
+def test_cast_multi_kernel(gpu):
+    """csrc/optim.hip cast_multi (GradSync's 16-bit <-> fp32 conversions, one launch for many
+    pairs) against torch's .to(): every dtype pair, sizes with and without a full 8-element tail,
+    offset (not 16-byte aligned) views, more pairs than one launch holds."""
+    import xdot._ext as ext
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    dts = [torch.float32, torch.bfloat16, torch.float16]
+    srcs, dsts = [], []
+    for i, n in enumerate([1, 7, 8, 9, 2048, 2049, 768 * 768, 40001] * 5):
+        sdt, ddt = dts[i % 3], dts[(i // 3) % 3]
+        base = (torch.randn(n + 3, generator=g) * 4).to(gpu, sdt)
+        srcs.append(base[3:] if i % 4 == 1 else base[:n])  # offset views: scalar path
+        out = torch.full((n + 1,), float("nan"), device=gpu, dtype=ddt)
+        dsts.append(out[1:] if i % 5 == 2 else out[:n])
+    assert len(srcs) > 32
+    ext.ops().cast_multi(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        torch.testing.assert_close(d, s.to(d.dtype), rtol=0, atol=0)

@@ -121,13 +121,6 @@ class AttnBlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         # output projection: d(o) for the attention on this stream; its weight / bias gradients
         # (only needed by the optimizer) on a second stream, under the attention backward
-        side = _wgrad_stream(dout)
-        if side is None:
-            do, dwc, dbc = linear_backward(dout, o, wc, True, ng[9], hc and ng[10])
-        else:
-            do, _, _ = linear_backward(dout, o, wc, True, False, False)
-            dout._xdot_ready_on = _ready_on(dout, side)
-            _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=False)
         wk_, bk_, wq_, bq_, wv_, bv_, wc_, bc_ = ctx.params
         sync = None
         if ctx.sync is not None:
@@ -135,6 +128,17 @@ class AttnBlockFn(torch.autograd.Function):
             # deliver only when this forward was the parameters' ONLY use since the last wait():
             # a module called twice has its gradients summed by autograd (AccumulateGrad) first
             sync = gs if gs.sole_use(key) else None
+        # weight gradients handed to GradSync in its wire dtype (fp32 for a bf16 module reduced in
+        # fp32: straight from the kernels' fp32 sums, no conversion pass before the all-reduce)
+        wdt = (lambda *ps: torch.float32 if any(p is not None and sync.wire_dtype(p) == torch.float32 for p in ps)
+               else None) if sync is not None else (lambda *ps: None)
+        side = _wgrad_stream(dout)
+        if side is None:
+            do, dwc, dbc = linear_backward(dout, o, wc, True, ng[9], hc and ng[10], dw_dtype=wdt(wc_, bc_))
+        else:
+            do, _, _ = linear_backward(dout, o, wc, True, False, False)
+            dout._xdot_ready_on = _ready_on(dout, side)
+            _, dwc, dbc = linear_backward(dout, o, wc, False, ng[9], hc and ng[10], join=False, dw_dtype=wdt(wc_, bc_))
         # the current stream is only looked up when a side stream is in play (host cost per call)
         cur = torch.cuda.current_stream(dout.device) if side is not None else None
         if sync is not None:  # hand the output projection's gradients to GradSync now: their
@@ -147,19 +151,20 @@ class AttnBlockFn(torch.autograd.Function):
         # gradient runs there, under the row-side kernel (linear_backward)
         qv_on = getattr(dqv, "_xdot_ready_on", None) if native_wgrad(dqv, xqv) else None  # (as linear_backward)
         need_wk, need_wqv = ng[3], ng[5] or ng[7]
+        kdt, qvdt = wdt(wk_, bk_), wdt(wq_, bq_, wv_, bv_)
         if side is None and qv_on is None and need_wk and need_wqv:
             # one stream: dWk and dW[q|v] in ONE launch (weight_grad_pair)
-            dxk, _, dbk = linear_backward(dk, xk, wk, ng[0], False, hk and ng[4])
-            dxqv, _, dbqv = linear_backward(dqv, xqv, wqv, ng[1], False, hq and (ng[6] or ng[8]))
-            dwk, dwqv = weight_grad_pair(dk, xk, dqv, xqv, wk.dtype)
+            dxk, _, dbk = linear_backward(dk, xk, wk, ng[0], False, hk and ng[4], dw_dtype=kdt)
+            dxqv, _, dbqv = linear_backward(dqv, xqv, wqv, ng[1], False, hq and (ng[6] or ng[8]), dw_dtype=qvdt)
+            dwk, dwqv = weight_grad_pair(dk, xk, dqv, xqv, kdt or qvdt or wk.dtype)
         else:
             if side is None:
-                dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], need_wk, hk and ng[4])
+                dxk, dwk, dbk = linear_backward(dk, xk, wk, ng[0], need_wk, hk and ng[4], dw_dtype=kdt)
             else:
                 dk._xdot_ready_on = _ready_on(dk, side)
                 dxk, _, _ = linear_backward(dk, xk, wk, ng[0], False, False)
-                _, dwk, dbk = linear_backward(dk, xk, wk, False, need_wk, hk and ng[4], join=False)
-            dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], need_wqv, hq and (ng[6] or ng[8]))
+                _, dwk, dbk = linear_backward(dk, xk, wk, False, need_wk, hk and ng[4], join=False, dw_dtype=kdt)
+            dxqv, dwqv, dbqv = linear_backward(dqv, xqv, wqv, ng[1], need_wqv, hq and (ng[6] or ng[8]), dw_dtype=qvdt)
         n = ctx.nq
         dwq = dwv = dbq = dbv = None
         # the packed products cover both halves; hand back only what is asked for (a frozen

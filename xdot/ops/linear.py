@@ -189,11 +189,12 @@ def weight_grad_pair(dy0: torch.Tensor, x0: torch.Tensor, dy1: torch.Tensor, x1:
 
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, need_dx: bool, need_dw: bool,
-                    need_db: bool, join: bool = True):
+                    need_db: bool, join: bool = True, dw_dtype: Optional[torch.dtype] = None):
     """Gradients of ``F.linear(x, weight, bias)``: (dx, dw, db), each None when not needed.  dw is
-    the split-K MFMA weight gradient (fp32 accumulation).  When ``dy._xdot_ready_on`` names a
-    stream, dw / db are computed there; ``join=False`` leaves ordering the current stream after
-    them (and ``record_stream`` of dw / db on it) to the caller."""
+    the split-K MFMA weight gradient (fp32 accumulation), in ``dw_dtype`` (default: the weight's;
+    fp32 for GradSync's fp32 wire, :meth:`xdot.parallel.GradSync.wire_dtype`), db likewise.  When
+    ``dy._xdot_ready_on`` names a stream, dw / db are computed there; ``join=False`` leaves ordering
+    the current stream after them (and ``record_stream`` of dw / db on it) to the caller."""
     dx = dw = db = None
     dy2 = dy.reshape(-1, dy.shape[-1])
     if need_dx:
@@ -204,10 +205,10 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, nee
     cur = torch.cuda.current_stream(dy.device) if side is not None else None
     with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
         if need_dw:
-            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), weight.dtype)
+            dw = weight_grad(dy2, x.reshape(-1, x.shape[-1]), dw_dtype or weight.dtype)
         if need_db:
             ct = torch.float32 if dy.dtype in (torch.bfloat16, torch.float16) else dy.dtype
-            db = dy2.sum(0, dtype=ct).to(dy.dtype)
+            db = dy2.sum(0, dtype=ct).to(dw_dtype or dy.dtype)
     if side is not None and (need_dw or need_db):
         # the fused attention backward produced dy on its priority stream while its row-side
         # kernel still runs on `cur`: the weight / bias gradients run there too, overlapping

@@ -87,6 +87,20 @@ def allreduce_gradients(module_or_params, op: str = "sum", comm: Optional[_comm.
         _flat_apply(b, red)
 
 
+def _cast_into(srcs: List[torch.Tensor], dsts: List[torch.Tensor]) -> None:
+    """``dst.copy_(src)`` for every pair (dtype conversion): ONE xdot launch for all the GPU pairs
+    (csrc/optim.hip ``cast_multi``) instead of one elementwise kernel per tensor."""
+    if not srcs:
+        return
+    from .. import _ext
+
+    if dsts[0].is_cuda and _ext.use_hip(dsts[0]):
+        _ext.ops().cast_multi([s.contiguous() for s in srcs], dsts)
+        return
+    for src, dst in zip(srcs, dsts):
+        dst.copy_(src)
+
+
 @functools.lru_cache(maxsize=None)
 def _takes_params(opt_cls) -> bool:
     """Does ``opt_cls.step`` accept ``params=`` (a partial step, e.g. :class:`xdot.FusedAdamW`)?"""
@@ -122,7 +136,11 @@ class GradSync:
       (default) raises naming it, ``unused="zero"`` reduces it as a zero gradient (every rank
       must then do the same, as with DDP's ``find_unused_parameters``);
     * ``reduce_dtype``: dtype of the all-reduce (e.g. ``torch.float32`` for bf16 gradients: one
-      rounding at the end instead of one per ring step).  Default: the gradients' dtype.
+      rounding at the end instead of one per ring step).  Default: the gradients' dtype.  A fused
+      node asks :meth:`wire_dtype` and then hands over fp32 weight gradients of 16-bit parameters
+      straight from its fp32 accumulators: they are reduced in place, and ``wait()`` writes
+      ``p.grad`` once, rounded from the reduced fp32 sum (no conversion pass before the
+      all-reduce, no rounding to 16 bits before the sum).
     """
 
     def __init__(self, module: nn.Module, comm: Optional[_comm.Communicator] = None,
@@ -150,6 +168,7 @@ class GradSync:
         self._rest: List[torch.Tensor] = []
         self._attached = []
         self._dlv = set()  # ids of parameters whose gradient was delivered this round
+        self._g32 = {}     # id(p) -> fp32 gradient delivered for a 16-bit parameter (wire_dtype)
         self._uses = {}    # fused-module forwards since the last wait() (note_use / sole_use)
         if self.comm.world_size > 1:
             for p in params:
@@ -187,17 +206,39 @@ class GradSync:
         one step) must leave the summing to autograd's AccumulateGrad."""
         return self._uses.get(key, 0) == 1
 
+    def wire_dtype(self, p) -> torch.dtype:
+        """dtype in which a fused node should hand ``p``'s gradient to :meth:`deliver`: fp32 for a
+        16-bit parameter reduced here in fp32 this round (``reduce_dtype=torch.float32``, not under
+        :meth:`no_sync`), else the parameter's own."""
+        from ..utils.env import FLAGS
+
+        if (FLAGS.grad_wire32 and self.reduce_dtype == torch.float32 and p.dtype in (torch.bfloat16, torch.float16)
+                and not self._muted and self.comm.world_size > 1 and id(p) in self._index):
+            return torch.float32
+        return p.dtype
+
     @torch.no_grad()
     def deliver(self, pairs, stream=None) -> None:
         """Gradients computed early inside a multi-parameter backward node: accumulate each
         into ``p.grad`` (as autograd's AccumulateGrad would) and count it for its bucket, the
         bucket's all-reduce ordered after ``stream`` (where the gradients were computed).  The
-        node then returns None for these parameters."""
+        node then returns None for these parameters.  A gradient in :meth:`wire_dtype` fp32 for a
+        16-bit parameter is held (and reduced) as is; :meth:`wait` writes ``p.grad`` from it."""
+        cur = torch.cuda.current_stream() if stream is not None else None
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
             for p, g in pairs:
                 if g is None:
                     continue
+                if g.dtype != p.dtype:
+                    if self.wire_dtype(p) == g.dtype:
+                        if p.grad is not None:  # earlier micro-batches accumulated under no_sync()
+                            g = g.add_(p.grad)
+                        if cur is not None:
+                            g.record_stream(cur)  # wait() writes p.grad from it on the current stream
+                        self._g32[id(p)] = g
+                        continue
+                    g = g.to(p.dtype)
                 if p.grad is None:
                     p.grad = g.detach()
                 else:
@@ -229,30 +270,28 @@ class GradSync:
         b = self.buckets[i]
         self._launched[i] = True
         for p in b:
-            if p.grad is None:  # unused="zero": reduce a zero gradient
+            if p.grad is None and id(p) not in self._g32:  # unused="zero": reduce a zero gradient
                 p.grad = torch.zeros_like(p)
-        g0 = b[0].grad
-        rdt = self.reduce_dtype or g0.dtype
+        ts = [self._g32[id(p)] if id(p) in self._g32 else p.grad for p in b]
+        rdt = self.reduce_dtype or ts[0].dtype
         # "avg" in the collective itself where the backend has it (RCCL): no division pass
         nat = self.op == "avg" and self.comm.native_avg
         op = "avg" if nat else "sum"
-        if all(p.grad.is_contiguous() and p.grad.dtype == rdt for p in b):
-            # the gradients reduced in place (one grouped launch for a several-tensor bucket): no
-            # flatten / copy-back passes
-            grads = [p.grad for p in b]
-            h = self.comm.all_reduce(g0, op=op, async_op=True) if len(b) == 1 else \
-                self.comm.all_reduce_multi(grads, op=op, async_op=True)
-            self._handles.append((i, grads, h, nat))
+        if all(t.is_contiguous() and t.dtype == rdt for t in ts):
+            # reduced in place (one grouped launch for a several-tensor bucket): no flatten pass;
+            # the fp32 wire gradients are written into p.grad by wait()
+            h = self.comm.all_reduce(ts[0], op=op, async_op=True) if len(b) == 1 else \
+                self.comm.all_reduce_multi(ts, op=op, async_op=True)
+            back = [(t, p) for t, p in zip(ts, b) if id(p) in self._g32]
+            self._handles.append((i, ts, h, nat, back))
             return
-        # converted straight into the flat buffer, one full-grid conversion kernel per gradient
+        # converted straight into the flat buffer, every gradient of the bucket in one launch
         # (torch._foreach_copy_'s multi-tensor kernel ran ~14 us per 768 x 768 gradient on MI355X,
-        # a few blocks per tensor: 8 of them were 110 us of the emulated N=8 rank step,
-        # profiles/r6_rank.md)
-        flat = torch.empty(sum(p.numel() for p in b), dtype=rdt, device=g0.device)
-        for v, p in zip(_views(flat, b), b):
-            v.copy_(p.grad)
+        # one elementwise copy per gradient ~5 us each: profiles/r6_fp32.md §4)
+        flat = torch.empty(sum(p.numel() for p in b), dtype=rdt, device=ts[0].device)
+        _cast_into(ts, _views(flat, b))
         h = self.comm.all_reduce(flat, op=op, async_op=True)
-        self._handles.append((i, flat, h, nat))
+        self._handles.append((i, flat, h, nat, list(zip(_views(flat, b), b))))
 
     @torch.no_grad()
     def wait(self, optimizer=None) -> bool:
@@ -276,23 +315,33 @@ class GradSync:
             for i in missing:  # bucket index order: the same on every rank
                 self._launch(i)
         last = len(self._handles) - 1
-        for k, (i, flat, h, nat) in enumerate(self._handles):
+        back = []  # (reduced tensor, parameter) pairs whose p.grad is written in one launch
+        for k, (i, flat, h, nat, bk) in enumerate(self._handles):
             if split and k == last:  # everything reduced so far steps under the last all-reduce
-                optimizer.step(params=[p for j, _, _, _ in self._handles[:last] for p in self.buckets[j]])
+                self._write_back(back)
+                back = []
+                optimizer.step(params=[p for j, *_ in self._handles[:last] for p in self.buckets[j]])
             h.wait()
-            if isinstance(flat, list):  # reduced in place
-                if self.op == "avg" and not nat:
-                    torch._foreach_div_(flat, ws)
-                continue
             if self.op == "avg" and not nat:
-                flat.div_(ws)
-            for p, v in zip(self.buckets[i], _views(flat, self.buckets[i])):
-                p.grad.copy_(v)
+                if isinstance(flat, list):  # reduced in place
+                    torch._foreach_div_(flat, ws)
+                else:
+                    flat.div_(ws)
+            back.extend(bk)
+        self._write_back(back)
         if split:
             rest = self._outside_params(optimizer)
             optimizer.step(params=list(self.buckets[self._handles[last][0]]) + rest)
         self._reset()
         return split
+
+    @staticmethod
+    def _write_back(pairs) -> None:
+        """p.grad <- the reduced values (rounded to p's dtype), every pair in one launch."""
+        for _, p in pairs:
+            if p.grad is None:
+                p.grad = torch.empty_like(p)
+        _cast_into([t for t, _ in pairs], [p.grad for _, p in pairs])
 
     def _outside_params(self, optimizer) -> List[torch.Tensor]:
         """Parameters the optimizer holds that are not in this GradSync's buckets (a second
@@ -310,6 +359,7 @@ class GradSync:
     def _reset(self):
         self._handles.clear()
         self._dlv = set()
+        self._g32 = {}
         self._uses = {}
         self._seen = [set() for _ in self.buckets]
         self._launched = [False] * len(self.buckets)

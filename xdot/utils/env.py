@@ -32,6 +32,9 @@ variable                    default   effect
                                       (0: wait for the whole gather)  [collective]
 ``XDOT_GRAD_FP32``          0         reduce-scatter the gathered-side gradient partials in fp32
                                       (default: rounded once to bf16/fp16 in the kernel)  [collective]
+``XDOT_GRAD_WIRE32``        1         fused node hands 16-bit weight gradients to GradSync(reduce_dtype=
+                                      fp32) in fp32, straight from the kernels' sums (0: in the
+                                      parameter dtype, converted before the all-reduce)  [collective]
 ``XDOT_IPC``                0         all-gathers / reduce-scatters as native xGMI pull kernels over
                                       HIP IPC (``csrc/ipc.hip``)  [collective]
 ``XDOT_IPC_MB``             512       IPC staging MiB per slot (routes IPC vs RCCL by size)  [collective]
@@ -151,6 +154,7 @@ class _Flags:
         self.gather_chunks = _num("XDOT_GATHER_CHUNKS", 0, int)  # 0: auto
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
+        self.grad_wire32 = _flag("XDOT_GRAD_WIRE32", default="1")
         self.ipc = _flag("XDOT_IPC")
         self.ipc_mb = _num("XDOT_IPC_MB", 512.0)
         self.ipc_wgs = _num("XDOT_IPC_WGS", 64, int)
@@ -179,7 +183,7 @@ class _Flags:
 FLAGS = _Flags()
 
 # flags that change the number (or dtype) of the collectives an op issues
-COLLECTIVE_KNOBS = ("check", "chunk_budget_mb", "ops_schedule", "gather_chunks", "local_first", "grad_fp32",
+COLLECTIVE_KNOBS = ("check", "chunk_budget_mb", "ops_schedule", "gather_chunks", "local_first", "grad_fp32", "grad_wire32",
                     "ipc", "ipc_mb", "ipc_wgs", "ring_bidir")
 
 
