@@ -1018,9 +1018,11 @@ void cast_multi(at::TensorList src, at::TensorList dst) {
 }
 
 // one AdamW step for lists of same-dtype params / grads with fp32 moments (chunks of 32)
+// grad_out (optional, one per parameter): the gradients are fp32 (GradSync's reduced sums of
+// 16-bit parameters) and each is also written into grad_out[i] in the parameter dtype
 void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_avg, at::TensorList exp_avg_sq,
                 double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
-                at::TensorList step_ts, const c10::optional<at::Tensor>& lr_t) {
+                at::TensorList step_ts, const c10::optional<at::Tensor>& lr_t, at::TensorList grad_out) {
   Range rr_("xdot.adamw_step");
   const size_t n = params.size();
   const bool dev_state = step_ts.size() > 0;
@@ -1034,14 +1036,21 @@ void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_
                 "xdot.adamw_step: lr_t must be a one-element fp32 device tensor");
   }
   TORCH_CHECK(grads.size() == n && exp_avg.size() == n && exp_avg_sq.size() == n, "xdot.adamw_step: list sizes");
+  const bool g32 = grad_out.size() > 0;
+  TORCH_CHECK(!g32 || grad_out.size() == n, "xdot.adamw_step: one grad_out per parameter");
   TORCH_CHECK(step >= 1, "xdot.adamw_step: step counts from 1");
   if (n == 0) return;
   const auto dtype = params[0].scalar_type();
   for (size_t i = 0; i < n; ++i) {
     TORCH_CHECK(params[i].is_cuda() && params[i].is_contiguous() && params[i].scalar_type() == dtype,
                 "xdot.adamw_step: contiguous GPU params of one dtype");
-    TORCH_CHECK(grads[i].sizes() == params[i].sizes() && grads[i].is_contiguous() && grads[i].scalar_type() == dtype,
+    TORCH_CHECK(grads[i].sizes() == params[i].sizes() && grads[i].is_contiguous() &&
+                    grads[i].scalar_type() == (g32 ? at::kFloat : dtype),
                 "xdot.adamw_step: grad shape/dtype");
+    if (g32)
+      TORCH_CHECK(dtype != at::kFloat && grad_out[i].sizes() == params[i].sizes() && grad_out[i].is_contiguous() &&
+                      grad_out[i].scalar_type() == dtype && grad_out[i].device() == params[i].device(),
+                  "xdot.adamw_step: grad_out (16-bit parameters, parameter shape / dtype)");
     for (const at::Tensor* s : {&exp_avg[i], &exp_avg_sq[i]})
       TORCH_CHECK(s->numel() == params[i].numel() && s->is_contiguous() && s->scalar_type() == at::kFloat,
                   "xdot.adamw_step: fp32 moments");
@@ -1059,6 +1068,7 @@ void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_
       a.m[i] = exp_avg[k].data_ptr<float>(); a.v[i] = exp_avg_sq[k].data_ptr<float>();
       a.n[i] = params[k].numel();
       a.step_dev[i] = dev_state ? step_ts[k].data_ptr<float>() : nullptr;
+      a.gout[i] = g32 ? grad_out[k].data_ptr() : nullptr;
       a.blk0[i] = blk;
       const int64_t nb = (a.n[i] + xdot::ADAM_BLOCK_ELEMS - 1) / xdot::ADAM_BLOCK_ELEMS;
       TORCH_CHECK(blk + nb < (1LL << 31), "xdot.adamw_step: too many elements");
@@ -1069,6 +1079,7 @@ void adamw_step(at::TensorList params, at::TensorList grads, at::TensorList exp_
     a.bc1 = bc1; a.bc2_sqrt = std::sqrt(bc2);
     a.dev_state = dev_state ? 1 : 0;
     a.lr_dev = dev_state ? lr_t->data_ptr<float>() : nullptr;
+    a.g32 = g32 ? 1 : 0;
     TORCH_CHECK(xdot_adamw_launch(&a, dt_code(dtype), cur_stream(params[0])) == 0, "xdot.adamw_step: dtype");
     check_launch(hipGetLastError(), "adamw_step");
   }
@@ -1471,7 +1482,8 @@ TORCH_LIBRARY(xdot, m) {
   m.def("sum_partials_into(Tensor part, Tensor(a!) out) -> ()");
   m.def("cast_multi(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("adamw_step(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, float lr, "
-        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t) -> ()");
+        "float beta1, float beta2, float eps, float weight_decay, int step, Tensor[] step_ts, Tensor? lr_t, "
+        "Tensor(d!)[] grad_out) -> ()");
   m.def("flash_bwd_rows(Tensor dout, Tensor rows, Tensor kc, Tensor vc, Tensor lse, Tensor delta, Tensor? bits, "
         "Tensor? flags, int H, float scale, int nsplit=0, bool prescaled=False, int fp32_mode=0, Tensor? sbuf=None, "
         "Tensor? dsbuf=None) -> Tensor");

@@ -133,6 +133,11 @@ struct AdamArgs {
   int dev_state;
   const float* step_dev[ADAM_MAX_T];
   const float* lr_dev;
+  // g32 = 1: the gradients are fp32 (GradSync's reduced fp32 sums of 16-bit parameters) and each
+  // is also written, rounded to the parameter dtype, into gout (the parameter's .grad): the
+  // write-back pass of GradSync.wait() folded into the update
+  int g32;
+  void* gout[ADAM_MAX_T];
 };
 // multi-tensor dtype conversion (csrc/optim.hip): dst[i] = (dst dtype) src[i] for up to CAST_MAX_T
 // tensor pairs per launch (GradSync's fp32 reduce buffers <-> 16-bit gradients)

@@ -15,16 +15,18 @@
 
 namespace xdot {
 
-template <int DT>
+template <int DT, bool G32 = false>
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   using TP = typename dt_traits<DT>::T;
+  using TG = typename std::conditional<G32, float, TP>::type;  // gradient storage type
   const int blk = blockIdx.x;
   int t_ = 0;
   while (t_ + 1 < a.nt && blk >= a.blk0[t_ + 1]) ++t_;  // wave-uniform search over <= 32 entries
   const int64_t base = (int64_t)(blk - a.blk0[t_]) * ADAM_BLOCK_ELEMS + threadIdx.x * 4;
   const int64_t n = a.n[t_];
   TP* p = reinterpret_cast<TP*>(a.p[t_]);
-  const TP* g = reinterpret_cast<const TP*>(a.g[t_]);
+  const TG* g = reinterpret_cast<const TG*>(a.g[t_]);
+  TP* go = G32 ? reinterpret_cast<TP*>(a.gout[t_]) : nullptr;
   float* m = a.m[t_];
   float* v = a.v[t_];
   float bc1 = a.bc1, bc2_sqrt = a.bc2_sqrt, lr = a.lr;
@@ -42,23 +44,28 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   };
   // full, aligned 4-element group: one vector load / store per operand (the tensors start at
   // allocator-aligned addresses; the check is wave-uniform per tensor)
-  constexpr int PB = 4 * (int)sizeof(TP);
-  if (base + 3 < n && ((uintptr_t)p | (uintptr_t)g) % PB == 0 && ((uintptr_t)m | (uintptr_t)v) % 16 == 0) {
+  constexpr int PB = 4 * (int)sizeof(TP), GB = 4 * (int)sizeof(TG);
+  if (base + 3 < n && (uintptr_t)p % PB == 0 && (uintptr_t)g % GB == 0 && (uintptr_t)go % PB == 0 &&
+      ((uintptr_t)m | (uintptr_t)v) % 16 == 0) {
     using PV = typename std::conditional<PB == 16, u32x4, u32x2>::type;
-    union { PV u; TP e[4]; } pp, gg;
+    using GV = typename std::conditional<GB == 16, u32x4, u32x2>::type;
+    union { PV u; TP e[4]; } pp, gw;
+    union { GV u; TG e[4]; } gg;
     pp.u = *reinterpret_cast<const PV*>(p + base);
-    gg.u = *reinterpret_cast<const PV*>(g + base);
+    gg.u = *reinterpret_cast<const GV*>(g + base);
     f32x4 mm = *reinterpret_cast<const f32x4*>(m + base), vv = *reinterpret_cast<const f32x4*>(v + base);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float mi = mm[e], vi = vv[e];
       pp.e[e] = (TP)upd((float)pp.e[e], (float)gg.e[e], mi, vi);
+      if constexpr (G32) gw.e[e] = (TP)gg.e[e];
       mm[e] = mi;
       vv[e] = vi;
     }
     *reinterpret_cast<f32x4*>(m + base) = mm;
     *reinterpret_cast<f32x4*>(v + base) = vv;
     *reinterpret_cast<PV*>(p + base) = pp.u;
+    if constexpr (G32) *reinterpret_cast<PV*>(go + base) = gw.u;
     return;
   }
 #pragma unroll
@@ -66,6 +73,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
     const int64_t i = base + e;
     if (i >= n) break;
     const float gi = (float)g[i];
+    if constexpr (G32) go[i] = (TP)gi;
     const float mi = a.beta1 * m[i] + (1.f - a.beta1) * gi;
     const float vi = a.beta2 * v[i] + (1.f - a.beta2) * gi * gi;
     m[i] = mi;
@@ -170,7 +178,11 @@ extern "C" int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st
   if (a->nt <= 0) return 0;
   const dim3 grid((unsigned)a->blk0[a->nt]);
   if (grid.x == 0) return 0;
-  if (dt == DT_F32) hipLaunchKernelGGL(adamw_kernel<DT_F32>, grid, dim3(256), 0, st, *a);
+  if (a->g32) {
+    if (dt == DT_BF16) hipLaunchKernelGGL((adamw_kernel<DT_BF16, true>), grid, dim3(256), 0, st, *a);
+    else if (dt == DT_F16) hipLaunchKernelGGL((adamw_kernel<DT_F16, true>), grid, dim3(256), 0, st, *a);
+    else return -1;
+  } else if (dt == DT_F32) hipLaunchKernelGGL(adamw_kernel<DT_F32>, grid, dim3(256), 0, st, *a);
   else if (dt == DT_BF16) hipLaunchKernelGGL(adamw_kernel<DT_BF16>, grid, dim3(256), 0, st, *a);
   else if (dt == DT_F16) hipLaunchKernelGGL(adamw_kernel<DT_F16>, grid, dim3(256), 0, st, *a);
   else return -1;

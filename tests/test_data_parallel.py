@@ -343,7 +343,6 @@ def _wire_body(r, mode):
     from xdot.utils import comm as C
 
     W = C.get_comm().world_size
-    torch.manual_seed(0)
     m = torch.nn.Sequential(torch.nn.Linear(8, 6, bias=False), torch.nn.Linear(6, 4, bias=False)).to(torch.bfloat16)
     ps = list(m.parameters())
     sync = GradSync(m, comm=C.get_comm(), bucket_mb=1.0 if mode == "flat" else 1e-5, reduce_dtype=torch.float32)
@@ -421,3 +420,41 @@ def _fused_wire_body(rank, ws):
 
 def test_gradsync_fused_module_fp32_wire_gloo():
     run_gloo(_fused_wire_body, 2)
+
+
+def _wire_opt_body(r):
+    """Thread rank r of test_gradsync_fp32_wire_split_step_matches_plain_step."""
+    from xdot.ops.optim import FusedAdamW
+    from xdot.parallel import GradSync
+    from xdot.utils import comm as C
+
+    out = []
+    for split in (True, False):
+        m = torch.nn.Sequential(torch.nn.Linear(8, 6, bias=False), torch.nn.Linear(6, 4, bias=False)).to(torch.bfloat16)
+        ps = list(m.parameters())
+        gen0 = torch.Generator().manual_seed(0)  # per-thread generator (threads share the global one)
+        with torch.no_grad():
+            for p in ps:
+                p.copy_(torch.randn(p.shape, generator=gen0))
+        opt = FusedAdamW(ps, lr=1e-2)
+        sync = GradSync(m, comm=C.get_comm(), bucket_mb=1e-5, reduce_dtype=torch.float32)
+        for step in range(2):
+            gen = torch.Generator().manual_seed(10 * r + step)
+            sync.deliver([(p, torch.randn(p.shape, generator=gen)) for p in ps])
+            stepped = sync.wait(optimizer=opt if split else None)
+            assert stepped == split
+            if not stepped:
+                opt.step()
+            opt.zero_grad()
+        out.append([p.detach().clone() for p in ps])
+    for a, b in zip(*out):  # the CPU update reads the same rounded gradient either way
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    return True
+
+
+def test_gradsync_fp32_wire_split_step_matches_plain_step():
+    """wait(optimizer=FusedAdamW) hands the reduced fp32 gradients to the optimizer (grads=), which
+    writes p.grad itself: same parameters as wait() + a plain step (3 thread ranks, CPU update)."""
+    from xdot.utils import comm as C
+
+    assert all(C.ThreadGroup(3).run(_wire_opt_body))

@@ -187,3 +187,36 @@ def test_cast_multi_kernel(gpu):
     ext.ops().cast_multi(srcs, dsts)
     for s, d in zip(srcs, dsts):
         torch.testing.assert_close(d, s.to(d.dtype), rtol=0, atol=0)
+
+
+def test_fused_adamw_fp32_grads(gpu):
+    """FusedAdamW.step(params=, grads=) with fp32 gradients of bf16 parameters (GradSync's reduced
+    sums): the update uses the fp32 values and writes each, rounded, into p.grad (one launch);
+    == torch.optim.AdamW on fp32 copies; a parameter without an override uses its own p.grad."""
+    from xdot.ops.optim import FusedAdamW
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    shapes = [(768, 768), (1536, 768), (5,), (999, 7)]
+    p32 = [torch.randn(*s, generator=g) for s in shapes]
+    gr = [torch.randn(*s, generator=g) for s in shapes]
+    kw = dict(lr=3e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.05)
+    ours = [p.to(gpu, torch.bfloat16).requires_grad_(True) for p in p32]
+    buf = torch.zeros(1 + p32[3].numel(), device=gpu, dtype=torch.bfloat16)  # unaligned: scalar path
+    buf[1:].copy_(p32[3].flatten().to(gpu, torch.bfloat16))
+    ours[3] = buf[1:].view(p32[3].shape).detach().requires_grad_(True)
+    ref = [p.to(gpu).requires_grad_(True) for p in p32]
+    o1, o2 = FusedAdamW(ours, **kw), torch.optim.AdamW(ref, **kw)
+    for s in range(3):
+        g32 = [(x * (s + 1)).to(gpu) for x in gr]
+        for p, q, x in zip(ours, ref, g32):
+            q.grad = x.clone()
+            p.grad = None
+        ours[2].grad = g32[2].to(torch.bfloat16)  # no override: its own bf16 gradient
+        q2 = ref[2]
+        q2.grad = ours[2].grad.float()
+        o1.step(params=ours, grads=[g32[0], g32[1], None, g32[3]])
+        o2.step()
+        for i in (0, 1, 3):
+            torch.testing.assert_close(ours[i].grad, g32[i].to(torch.bfloat16), rtol=0, atol=0)
+    for p, q in zip(ours, ref):
+        torch.testing.assert_close(p.float(), q.detach(), rtol=2e-2, atol=2e-2)

@@ -51,10 +51,14 @@ class FusedAdamW(torch.optim.Optimizer):
             for p in group["params"]:
                 p.grad = None
 
-    def step(self, closure=None, params=None):
+    def step(self, closure=None, params=None, grads=None):
         """``params``: update only these parameters (each must then be updated once per step —
         :meth:`xdot.parallel.GradSync.wait` with ``optimizer=`` splits a step this way so the
         early buckets' update overlaps the last gradient all-reduce).  Not with ``capturable``.
+        ``grads`` (with ``params``, aligned, entries may be None): fp32 gradients to use instead of
+        ``p.grad`` for 16-bit parameters (GradSync's reduced fp32 sums); the kernel also writes each
+        into ``p.grad``, rounded to the parameter dtype (GradSync's write-back pass folded into the
+        update).
 
         torch wraps every optimizer's ``step`` in a profiler range plus the step-hook loops
         (``Optimizer.profile_hook_step``): ~35 µs of host per call, twice per training step when
@@ -63,31 +67,47 @@ class FusedAdamW(torch.optim.Optimizer):
         it: a registered step hook (per optimizer or global) or an active autograd profiler."""
         if (self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks or _optim_mod._global_optimizer_pre_hooks
                 or _optim_mod._global_optimizer_post_hooks or torch.autograd._profiler_enabled()):
-            return _hooked_step(self, closure, params)
+            return _hooked_step(self, closure, params, grads)
         prev = torch.is_grad_enabled()
         torch._C._set_grad_enabled(False)
         try:
-            return self._step_impl(closure, params)
+            return self._step_impl(closure, params, grads)
         finally:
             torch._C._set_grad_enabled(prev)
 
     step.hooked = True  # torch.optim.Optimizer._patch_step_function: leave this step unwrapped
 
-    def _step_impl(self, closure=None, params=None):
+    def _step_impl(self, closure=None, params=None, grads=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
         only = None
+        over = {}  # id(p) -> fp32 gradient replacing p.grad (written into p.grad by the update)
         if params is not None:
             if self.capturable:
                 raise RuntimeError("FusedAdamW(capturable=True).step(params=...) is not supported")
+            params = list(params)
             only = {id(p) for p in params}
+            if grads is not None:
+                over = {id(p): g for p, g in zip(params, grads) if g is not None}
+        elif grads is not None:
+            raise ValueError("FusedAdamW.step(grads=...) needs params=")
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             buckets = {}
             for p in group["params"]:
-                if p.grad is None or (only is not None and id(p) not in only):
+                if only is not None and id(p) not in only:
+                    continue
+                g32 = over.get(id(p))
+                if g32 is not None:
+                    if p.grad is None:
+                        p.grad = torch.empty_like(p)
+                    if not (g32.dtype == torch.float32 and p.dtype in (torch.bfloat16, torch.float16)
+                            and g32.is_contiguous() and p.grad.is_contiguous() and g32.shape == p.shape):
+                        p.grad.copy_(g32)  # (the kernel takes fp32 gradients of 16-bit parameters only)
+                        g32 = None
+                if p.grad is None:
                     continue
                 st = self.state[p]
                 if not st:
@@ -106,20 +126,23 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["step"] = int(st["step"].item())
                 st["step"] += 1
                 if hip:
-                    buckets.setdefault((p.dtype, p.device, st["step"]), []).append(p)
+                    buckets.setdefault((p.dtype, p.device, st["step"], g32 is not None), []).append(p)
                 else:
+                    if g32 is not None:
+                        p.grad.copy_(g32)
                     self._torch_update(p, st, group, b1, b2)
-            for (dt, dev, step), ps in buckets.items():
+            for (dt, dev, step, ov), ps in buckets.items():
                 steps, lr_t = [], None
                 if self.capturable:
                     steps = [self.state[p]["step"] for p in ps]
                     torch._foreach_add_(steps, 1.0)  # device ops: advance on every graph replay too
                     lr_t = self._lr_tensor(gi, group, dev)
                     step = 1
-                _ext.ops().adamw_step(ps, [p.grad.contiguous() for p in ps], [self.state[p]["exp_avg"] for p in ps],
+                gs = [over[id(p)] for p in ps] if ov else [p.grad.contiguous() for p in ps]
+                _ext.ops().adamw_step(ps, gs, [self.state[p]["exp_avg"] for p in ps],
                                       [self.state[p]["exp_avg_sq"] for p in ps], float(group["lr"]), float(b1),
                                       float(b2), float(group["eps"]), float(group["weight_decay"]), int(step),
-                                      steps, lr_t)
+                                      steps, lr_t, [p.grad for p in ps] if ov else [])
         return loss
 
     @staticmethod
@@ -168,8 +191,8 @@ class FusedAdamW(torch.optim.Optimizer):
 
 
 @torch.no_grad()
-def _unwrapped_step(self, closure=None, params=None):
-    return self._step_impl(closure, params)
+def _unwrapped_step(self, closure=None, params=None, grads=None):
+    return self._step_impl(closure, params, grads)
 
 
 # torch's own wrapper (profiler range + pre/post step hooks) around the same update, for the

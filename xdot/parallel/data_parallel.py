@@ -107,6 +107,13 @@ def _takes_params(opt_cls) -> bool:
     return "params" in inspect.signature(opt_cls.step).parameters
 
 
+@functools.lru_cache(maxsize=None)
+def _takes_grads(opt_cls) -> bool:
+    """Does ``opt_cls.step`` also take ``grads=`` (fp32 gradients it writes into ``p.grad`` itself,
+    :class:`xdot.FusedAdamW`)?"""
+    return "grads" in inspect.signature(opt_cls.step).parameters
+
+
 
 def _views(flat: torch.Tensor, params) -> List[torch.Tensor]:
     """Consecutive views of a flat bucket shaped like each parameter's gradient."""
@@ -165,6 +172,7 @@ class GradSync:
         self._hooks = []
         self._muted = False
         self._rest_key = None
+        self._held_key, self._held = None, set()
         self._rest: List[torch.Tensor] = []
         self._attached = []
         self._dlv = set()  # ids of parameters whose gradient was delivered this round
@@ -318,9 +326,8 @@ class GradSync:
         back = []  # (reduced tensor, parameter) pairs whose p.grad is written in one launch
         for k, (i, flat, h, nat, bk) in enumerate(self._handles):
             if split and k == last:  # everything reduced so far steps under the last all-reduce
-                self._write_back(back)
+                self._step_with(optimizer, [p for j, *_ in self._handles[:last] for p in self.buckets[j]], back)
                 back = []
-                optimizer.step(params=[p for j, *_ in self._handles[:last] for p in self.buckets[j]])
             h.wait()
             if self.op == "avg" and not nat:
                 if isinstance(flat, list):  # reduced in place
@@ -328,12 +335,28 @@ class GradSync:
                 else:
                     flat.div_(ws)
             back.extend(bk)
-        self._write_back(back)
         if split:
             rest = self._outside_params(optimizer)
-            optimizer.step(params=list(self.buckets[self._handles[last][0]]) + rest)
+            self._step_with(optimizer, list(self.buckets[self._handles[last][0]]) + rest, back)
+        else:
+            self._write_back(back)
         self._reset()
         return split
+
+    def _step_with(self, optimizer, params, back) -> None:
+        """``optimizer.step(params=params)`` after writing the reduced values of ``back`` into
+        ``p.grad`` -- by the optimizer itself where it takes fp32 ``grads=`` (FusedAdamW: the write-
+        back folded into its update launch), else in one :meth:`_write_back` launch."""
+        over = {}
+        if back and _takes_grads(type(optimizer)):
+            held = self._held_ids(optimizer)
+            over = {id(p): t for t, p in back if id(p) in held and t.dtype == torch.float32
+                    and p.dtype in (torch.bfloat16, torch.float16)}
+        self._write_back([(t, p) for t, p in back if id(p) not in over])
+        if over:
+            optimizer.step(params=params, grads=[over.get(id(p)) for p in params])
+        else:
+            optimizer.step(params=params)
 
     @staticmethod
     def _write_back(pairs) -> None:
@@ -342,6 +365,14 @@ class GradSync:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
         _cast_into([t for t, _ in pairs], [p.grad for _, p in pairs])
+
+    def _held_ids(self, optimizer) -> set:
+        """ids of the parameters ``optimizer`` holds (cached per optimizer and parameter count)."""
+        key = (id(optimizer), sum(len(g["params"]) for g in optimizer.param_groups))
+        if self._held_key != key:
+            self._held = {id(p) for g in optimizer.param_groups for p in g["params"]}
+            self._held_key = key
+        return self._held
 
     def _outside_params(self, optimizer) -> List[torch.Tensor]:
         """Parameters the optimizer holds that are not in this GradSync's buckets (a second
