@@ -120,7 +120,7 @@ class FusedAdamW(torch.optim.Optimizer):
                     if not hip:
                         raise RuntimeError("FusedAdamW(capturable=True) needs contiguous bf16/fp16/fp32 GPU parameters")
                     st["step"] = self._dev_step_of(st["step"], p.device)
-                    buckets.setdefault((p.dtype, p.device, 0), []).append(p)
+                    buckets.setdefault((p.dtype, p.device, 0, False), []).append(p)
                     continue
                 if torch.is_tensor(st["step"]):  # a state loaded from a capturable optimizer
                     st["step"] = int(st["step"].item())
