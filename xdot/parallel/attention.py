@@ -26,7 +26,7 @@ schedule with a torch reference implementation of steps 2-5.
 """
 from __future__ import annotations
 
-import contextlib
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -320,16 +320,6 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
         opart = torch.empty(sum(ns), B, R, C, dtype=torch.float32, device=k.device)
         lpart = torch.empty(sum(ns), B, H, R, dtype=torch.float32, device=k.device)
         slot = [0, 0]  # next partial slot, next entry of ns
-        # Segments write disjoint partial slots, so they need not run one after the other: the
-        # chunks alternate between the current stream and a side stream (own block: current;
-        # chunk 0: side; chunk 1: current; ...), so a segment's last part-full workgroup round
-        # overlaps the next segment's first instead of idling (each launch of the N=8 rank is
-        # 1-2 rounds of short workgroups).  Joined before the combine.
-        cur = torch.cuda.current_stream(k.device) if k.is_cuda else None
-        side = None
-        if FLAGS.fwd_seg_streams and k.is_cuda and len(widths) > 1:
-            side = _side_stream(k.device, 0, tag="fwdseg")
-            side.wait_stream(cur)  # k, [q|v] and the partial buffers are ready
 
         def run(kc, vc, mk):
             bits, flags = (mk.bits, mk.flags) if mk is not None else (None, None)
@@ -344,23 +334,17 @@ def _segmented_forward(k, qv, mask, H, scale, pending, n, rank, use_hip, prescal
             run(qv[..., :C], qv[..., C:], mk)
         bufs = []
         for c, (r0, rc) in enumerate(chunks):
-            on_side = side is not None and (c % 2 == 0) == local_first
-            with _on_stream(side, cur) if on_side else contextlib.nullcontext():
-                g = flash.gathered_to_btc(pending.wait(c))          # (B, N*rc, 2C)
-                if on_side and B > 1:
-                    g.record_stream(cur)  # (a permuted copy made on the side stream, used later by backward)
-                bufs.append(g)
-                for _, j0, j1 in (p for p in plan if p[0] == c):
-                    if j1 == -1:  # merged: every rank of the chunk, the own columns masked out
-                        mk = _own_excluded_mask(mask, B, R, n, rank, r0, rc, k.device)
-                        run(g[..., :C], g[..., C:], mk)
-                        continue
-                    mk = flash.prepare_mask_cached(mask, B, R, (j1 - j0) * rc, tag=("seg", r0, rc, n, j0, j1),
-                                                   view=_mask_cols(B, R, n, j0, j1, r0, rc))
-                    seg = g[:, j0 * rc:j1 * rc]
-                    run(seg[..., :C], seg[..., C:], mk)
-        if side is not None:
-            cur.wait_stream(side)
+            g = flash.gathered_to_btc(pending.wait(c))          # (B, N*rc, 2C)
+            bufs.append(g)
+            for _, j0, j1 in (p for p in plan if p[0] == c):
+                if j1 == -1:  # merged: every rank of the chunk, the own columns masked out
+                    mk = _own_excluded_mask(mask, B, R, n, rank, r0, rc, k.device)
+                    run(g[..., :C], g[..., C:], mk)
+                    continue
+                mk = flash.prepare_mask_cached(mask, B, R, (j1 - j0) * rc, tag=("seg", r0, rc, n, j0, j1),
+                                               view=_mask_cols(B, R, n, j0, j1, r0, rc))
+                seg = g[:, j0 * rc:j1 * rc]
+                run(seg[..., :C], seg[..., C:], mk)
         o, lse = ops.flash_fwd_combine(opart, lpart, int(H), k)
         perm = pending.permuted()
         return o, lse, ([perm] if perm is not None else bufs)

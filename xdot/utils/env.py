@@ -30,8 +30,6 @@ variable                    default   effect
                                       profiles/r2_gather_chunks.md)  [collective]
 ``XDOT_LOCAL_FIRST``        1         fused forward: the rank's own block runs under the gather
                                       (0: wait for the whole gather)  [collective]
-``XDOT_FWD_SEG_STREAMS``    1         segmented multi-rank forward: gathered chunks alternate between the
-                                      current and a side stream (segment tails overlap)
 ``XDOT_GRAD_FP32``          0         reduce-scatter the gathered-side gradient partials in fp32
                                       (default: rounded once to bf16/fp16 in the kernel)  [collective]
 ``XDOT_GRAD_WIRE32``        1         fused node hands 16-bit weight gradients to GradSync(reduce_dtype=
@@ -155,7 +153,6 @@ class _Flags:
         self.ops_schedule = _str("XDOT_OPS_SCHEDULE", "gather")
         self.gather_chunks = _num("XDOT_GATHER_CHUNKS", 0, int)  # 0: auto
         self.local_first = _flag("XDOT_LOCAL_FIRST", default="1")
-        self.fwd_seg_streams = _flag("XDOT_FWD_SEG_STREAMS", default="1")
         self.grad_fp32 = _flag("XDOT_GRAD_FP32")
         self.grad_wire32 = _flag("XDOT_GRAD_WIRE32", default="1")
         self.ipc = _flag("XDOT_IPC")
