@@ -198,20 +198,27 @@ def test_flash_column_split(gpu, nsplit, masked):
     assert (d1.float() - d2.float()).abs().max().item() <= 2e-2 * d1.float().abs().max().item()
 
 
-def test_flash_bwd_delta_and_given_delta(gpu):
-    """δ op == rowsum(dO·O) in fp32; passing δ to bwd_cols gives the same gradients."""
+@pytest.mark.parametrize("D,dt", [(64, torch.bfloat16), (96, torch.bfloat16), (32, torch.float16), (128, torch.bfloat16)])
+def test_flash_bwd_delta_and_given_delta(gpu, D, dt):
+    """δ op == rowsum(dO·O) in fp32 (the 8-lanes-per-row prep kernel), lse2 == lse · log2 e;
+    passing δ to bwd_cols gives the same gradients."""
+    import math
+
     from xdot.ops import flash
 
-    B, R, T, H, D = 2, 70, 300, 4, 64
+    B, R, T, H = 2, 70, 300, 4
     g = torch.Generator(device="cpu").manual_seed(7)
-    rows = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
-    kc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
-    vc = torch.randn(B, T, H * D, generator=g).to(gpu, torch.bfloat16)
-    do = torch.randn(B, R, H * D, generator=g).to(gpu, torch.bfloat16)
+    rows = torch.randn(B, R, H * D, generator=g).to(gpu, dt)
+    kc = torch.randn(B, T, H * D, generator=g).to(gpu, dt)
+    vc = torch.randn(B, T, H * D, generator=g).to(gpu, dt)
+    do = torch.randn(B, R, H * D, generator=g).to(gpu, dt)
     o, lse = flash.fwd(rows, kc, vc, None, H, 0.125)
     delta = flash.bwd_delta(do, o, H)
     ref = (do.float() * o.float()).view(B, R, H, D).sum(-1).transpose(1, 2)
     torch.testing.assert_close(delta, ref, rtol=1e-4, atol=1e-4)
+    delta2, lse2 = flash.bwd_prep(do, o, lse, H)
+    assert torch.equal(delta2, delta)
+    torch.testing.assert_close(lse2, lse * (1 / math.log(2)), rtol=1e-6, atol=1e-6)
     dkv1, d1 = flash.bwd_cols(do, rows, kc, vc, o, lse, None, H, 0.125)
     dkv2, d2 = flash.bwd_cols(do, rows, kc, vc, o, lse, None, H, 0.125, delta)
     assert d2.data_ptr() == delta.data_ptr()
