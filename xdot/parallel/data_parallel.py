@@ -364,7 +364,11 @@ class GradSync:
         for _, p in pairs:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
-        _cast_into([t for t, _ in pairs], [p.grad for _, p in pairs])
+        ok = [(t, p) for t, p in pairs if p.grad.is_contiguous()]
+        _cast_into([t for t, _ in ok], [p.grad for _, p in ok])
+        for t, p in pairs:
+            if not p.grad.is_contiguous():  # (a .grad the user set as a strided view)
+                p.grad.copy_(t)
 
     def _held_ids(self, optimizer) -> set:
         """ids of the parameters ``optimizer`` holds (cached per optimizer and parameter count)."""
