@@ -68,3 +68,44 @@ def test_ring_peak_memory_independent_of_ring_length(gpu):
     assert f8 - f4 > 0.8 * grown, (f4, f8)
     assert abs(r8 - r4) < 0.1 * (f8 - f4), (r4, r8)
     assert r8 < f8, (r8, f8)
+
+
+@pytest.mark.parametrize("link", [None, 2.0])
+def test_fp32_weight_gradient_wire_matches_parameter_dtype_wire(gpu, monkeypatch, link):
+    """GradSync(reduce_dtype=fp32) on a bf16 fused module (emulated 4-rank step, all-reduce = the
+    local gradient): with the fp32 wire (XDOT_GRAD_WIRE32, default) the node hands over the weight
+    gradients' fp32 sums and wait() rounds them into p.grad; without it the kernels round to bf16
+    and GradSync converts to fp32 and back.  Same rounding of the same sums: p.grad bitwise equal.
+    With FusedAdamW in the split step (the update reads the fp32 values and writes p.grad) the
+    gradients stay bitwise equal and the parameters agree to bf16 rounding."""
+    import xdot
+    from xdot.parallel import GradSync
+    from xdot.utils.comm import EmulatedComm
+    from xdot.utils.env import FLAGS
+
+    def run(wire, opt_step):
+        monkeypatch.setattr(FLAGS, "grad_wire32", wire)
+        comm = EmulatedComm(4, rank=1, link_gbps=link, p2p_gbps=link)
+        torch.manual_seed(0)
+        m = xdot.DistributedDotProductAttn(256, num_heads=4, comm=comm).to(gpu, torch.bfloat16)
+        sync = GradSync(m, comm=comm, bucket_mb=0.05, reduce_dtype=torch.float32)
+        opt = xdot.FusedAdamW(m.parameters(), lr=1e-3) if opt_step else None
+        g = torch.Generator(device="cpu").manual_seed(3)
+        x = torch.randn(1, 300, 256, generator=g).to(gpu, torch.bfloat16)
+        m(x, x, x, None).float().square().sum().backward()
+        if wire:
+            assert sync._g32 and all(t.dtype == torch.float32 for t in sync._g32.values())
+        else:
+            assert not sync._g32
+        stepped = sync.wait(optimizer=opt)
+        assert stepped == opt_step
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in m.parameters()], [p.detach().clone() for p in m.parameters()]
+
+    for opt_step in (False, True):
+        g1, p1 = run(True, opt_step)
+        g0, p0 = run(False, opt_step)
+        for a, b in zip(g1, g0):
+            assert a.dtype == torch.bfloat16 and torch.equal(a, b)
+        for a, b in zip(p1, p0):
+            torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-4)
