@@ -26,7 +26,6 @@ schedule with a torch reference implementation of steps 2-5.
 """
 from __future__ import annotations
 
-
 from typing import List, Optional, Tuple
 
 import torch
