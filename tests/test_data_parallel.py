@@ -458,3 +458,38 @@ def test_gradsync_fp32_wire_split_step_matches_plain_step():
     from xdot.utils import comm as C
 
     assert all(C.ThreadGroup(3).run(_wire_opt_body))
+
+
+def test_gradsync_one_deliver_one_grouped_all_reduce(monkeypatch):
+    """Buckets completed by ONE deliver() call are reduced by one grouped all-reduce (the fused
+    node's end-of-backward weight gradients: one RCCL launch instead of one per bucket); values
+    equal rounding the fp32 sum (3 thread ranks)."""
+    from xdot.parallel import GradSync
+    from xdot.utils import comm as C
+
+    calls = {"multi": 0}
+    orig_multi = C.ThreadComm.all_reduce_multi
+
+    def multi(self, ts, op="sum", async_op=False):
+        if self.rank == 0:
+            calls["multi"] += 1
+        return orig_multi(self, ts, op, async_op)
+
+    monkeypatch.setattr(C.ThreadComm, "all_reduce_multi", multi)
+
+    def body(r):
+        m = torch.nn.Sequential(*[torch.nn.Linear(8, 8, bias=False) for _ in range(3)]).to(torch.bfloat16)
+        ps = list(m.parameters())
+        sync = GradSync(m, comm=C.get_comm(), bucket_mb=1e-5, reduce_dtype=torch.float32)
+        assert len(sync.buckets) == 3
+        gs = lambda rank: [torch.full(p.shape, 0.25 * (rank + 1) + i) for i, p in enumerate(ps)]
+        sync.deliver(list(zip(ps, gs(r))))
+        sync.wait()
+        W = C.get_comm().world_size
+        for i, p in enumerate(ps):
+            want = sum(g[i] for g in map(gs, range(W))).to(torch.bfloat16)
+            assert torch.equal(p.grad, want)
+        return True
+
+    assert all(C.ThreadGroup(3).run(body))
+    assert calls["multi"] == 1

@@ -174,8 +174,12 @@ class AttnBlockFn(torch.autograd.Function):
         if dbqv is not None:
             dbq, dbv = (dbqv[:n] if ng[6] else None), (dbqv[n:] if ng[8] else None)
         if sync is not None:
-            sync.deliver([(wq_, dwq), (bq_, dbq), (wv_, dwv), (bv_, dbv)], stream=qv_on)
-            sync.deliver([(wk_, dwk), (bk_, dbk)], stream=side)
+            qv_pairs, k_pairs = [(wq_, dwq), (bq_, dbq), (wv_, dwv), (bv_, dbv)], [(wk_, dwk), (bk_, dbk)]
+            if qv_on is side:  # one call: the buckets it completes share one grouped all-reduce
+                sync.deliver(qv_pairs + k_pairs, stream=side)
+            else:
+                sync.deliver(qv_pairs, stream=qv_on)
+                sync.deliver(k_pairs, stream=side)
             dwq = dbq = dwv = dbv = dwk = dbk = None
         if side is not None:  # the gradients handed on are complete on this stream
             cur.wait_stream(side)

@@ -173,6 +173,7 @@ class GradSync:
         self._muted = False
         self._rest_key = None
         self._held_key, self._held = None, set()
+        self._batch = None  # buckets completed inside one deliver() call (launched together)
         self._rest: List[torch.Tensor] = []
         self._attached = []
         self._dlv = set()  # ids of parameters whose gradient was delivered this round
@@ -253,10 +254,19 @@ class GradSync:
                     p.grad.add_(g)
             if self._muted:  # no_sync(): accumulated only; NOT marked delivered, so the gradient of
                 return       # a later unmuted backward through AccumulateGrad is still counted
-            for p, g in pairs:
-                if g is not None and id(p) in self._index:  # (a parameter outside the buckets is
-                    self._dlv.add(id(p))                   # accumulated, never reduced here)
-                    self._on_grad(p, delivered=True)
+            # buckets completed by this call are reduced together: ONE grouped collective for the
+            # in-place ones (RCCL: one launch instead of one per bucket, each a small-message
+            # latency on the step's tail)
+            self._batch = []
+            try:
+                for p, g in pairs:
+                    if g is not None and id(p) in self._index:  # (a parameter outside the buckets is
+                        self._dlv.add(id(p))                   # accumulated, never reduced here)
+                        self._on_grad(p, delivered=True)
+                batch = self._batch
+            finally:
+                self._batch = None
+            self._launch_many(batch)
 
     def _on_grad(self, p, delivered: bool = False):
         if self._muted:
@@ -272,20 +282,51 @@ class GradSync:
                 "run one backward per wait(), or accumulate earlier micro-batches under sync.no_sync()")
         self._seen[i].add(id(p))
         if len(self._seen[i]) == len(self.buckets[i]):
-            self._launch(i)
+            if self._batch is not None:
+                self._batch.append(i)
+            else:
+                self._launch(i)
 
-    def _launch(self, i):
+    def _bucket_tensors(self, i):
+        """(tensors to reduce, reduce dtype, in place?) of bucket i."""
         b = self.buckets[i]
-        self._launched[i] = True
         for p in b:
             if p.grad is None and id(p) not in self._g32:  # unused="zero": reduce a zero gradient
                 p.grad = torch.zeros_like(p)
         ts = [self._g32[id(p)] if id(p) in self._g32 else p.grad for p in b]
         rdt = self.reduce_dtype or ts[0].dtype
+        return ts, rdt, all(t.is_contiguous() and t.dtype == rdt for t in ts)
+
+    def _launch_many(self, idx) -> None:
+        """Launch buckets ``idx`` (completed together): the in-place ones as ONE grouped
+        all-reduce (each bucket's entry shares its handle), the others one by one."""
+        group = []
+        for i in idx:
+            ts, rdt, inplace = self._bucket_tensors(i)
+            if inplace and (not group or group[0][2] == rdt):
+                group.append((i, ts, rdt))
+            else:
+                self._launch(i)
+        if len(group) < 2:
+            for i, _, _ in group:
+                self._launch(i)
+            return
+        nat = self.op == "avg" and self.comm.native_avg
+        allt = [t for _, ts, _ in group for t in ts]
+        h = self.comm.all_reduce_multi(allt, op="avg" if nat else "sum", async_op=True)
+        for i, ts, _ in group:
+            self._launched[i] = True
+            back = [(t, p) for t, p in zip(ts, self.buckets[i]) if id(p) in self._g32]
+            self._handles.append((i, ts, h, nat, back))
+
+    def _launch(self, i):
+        b = self.buckets[i]
+        self._launched[i] = True
+        ts, rdt, inplace = self._bucket_tensors(i)
         # "avg" in the collective itself where the backend has it (RCCL): no division pass
         nat = self.op == "avg" and self.comm.native_avg
         op = "avg" if nat else "sum"
-        if all(t.is_contiguous() and t.dtype == rdt for t in ts):
+        if inplace:
             # reduced in place (one grouped launch for a several-tensor bucket): no flatten pass;
             # the fp32 wire gradients are written into p.grad by wait()
             h = self.comm.all_reduce(ts[0], op=op, async_op=True) if len(b) == 1 else \
