@@ -570,13 +570,15 @@ int rows_split(int64_t B, int64_t R, int64_t T, int64_t H) {
 // whole and splits only its last `rem` blocks into enough column pieces to fill one more round;
 // only those tail rows go through partials and the (compact) combine.  Chosen when the round
 // model says it beats the uniform split; -> (whole, rem, split) per XCD, or false.
-bool head_heavy_plan(int64_t NB, int64_t T, int* whole, int* rem, int* split) {
+// S: resident workgroups per XCD (64: 32 CUs x 2; the exact-fp32 forward runs 3 per CU); su: the
+// uniform split to beat (0: the 16-bit forward's pick_split)
+bool head_heavy_plan(int64_t NB, int64_t T, int* whole, int* rem, int* split, int64_t S = 64, int su = 0) {
   if (NB % 8) return false;
-  const int64_t m = NB / 8, S = 64, nkt = (T + 63) / 64;
+  const int64_t m = NB / 8, nkt = (T + 63) / 64;
   const int64_t full = m / S, r = m % S;
   if (r == 0 || full == 0) return false;
-  const int su = pick_split(NB, T, 512, 0);
-  const double cu = (double)((NB * su + 511) / 512) * ((double)nkt / su + 8.0);
+  if (su <= 0) su = pick_split(NB, T, 8 * S, 0);
+  const double cu = (double)((NB * su + 8 * S - 1) / (8 * S)) * ((double)nkt / su + 8.0);
   double best = 1e300;
   int bs = 0;
   for (int s = 1; s <= 16; ++s) {
@@ -618,11 +620,17 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& rows, const at::T
   const int rpw = xdot_flash_fwd_rows_per_wg();
   const int64_t NB = ((g.R + rpw - 1) / rpw) * g.B * H;
   int hw = 0, hr = 0, hs = 0;
-  const bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && g.D <= 128 && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
+  bool heavy = nsplit == 0 && rows.scalar_type() != at::kFloat && g.D <= 128 && head_heavy_plan(NB, g.T, &hw, &hr, &hs);
   int ns = heavy ? hs : pick_split(NB, g.T, 512, nsplit);
   if (nsplit == 0 && rows.scalar_type() == at::kFloat) {  // fp32 kernels: their own occupancy / tile model
     const int f = xdot_flash_f32_row_splits(0, (int)fp32_mode, (int)g.D, sb != nullptr, NB, g.T);
     if (f > 0) ns = f;
+    // exact fp32 (D <= 128): the head-heavy grid when the round model prefers it over that split
+    const int occ = fp32_mode == 0 && g.D <= 128 && xdot_flash_f32_heavy() ? xdot_flash_f32_fwd_occ((int)g.D, sb != nullptr) : 0;
+    if (occ > 0 && head_heavy_plan(NB, g.T, &hw, &hr, &hs, (int64_t)occ * (xdot_num_cus() / 8), ns)) {
+      heavy = true;
+      ns = hs;
+    }
   }
   if (nsplit == 0 && g.D > 128) {  // wide kernels (one workgroup per CU): their own occupancy
     const int f = xdot_flash_wide_splits(0, dt_code(rows.scalar_type()), (int)g.D, sb != nullptr, NB, (g.T + 31) / 32);

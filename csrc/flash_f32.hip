@@ -199,14 +199,35 @@ __global__ __launch_bounds__(256, SD && D <= 96 ? 3 : 2) void fwd_kernel(FwdArgs
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nrb = (a.R + 127) / 128;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb = lin % nrb, bhs = lin / nrb;
-  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H);
+  int rbl, sp, ns, tail = -1;  // linear row block (bh * nrb + rb), column piece, pieces of this block
+  if (a.xrbs > 0) {
+    // head-heavy grid (as the 16-bit forward): XCD x = blockIdx % 8 runs its row blocks whole,
+    // then splits only its last xrem blocks in nsplit column pieces (compact partials `tail`,
+    // merged by combine_tail_kernel), so no uniform split pays partial writes and a full combine
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    if (k < a.xwhole) {
+      rbl = x * a.xrbs + k;
+      sp = 0;
+      ns = 1;
+    } else {
+      const int p = k - a.xwhole, j = p / a.nsplit;
+      rbl = x * a.xrbs + a.xwhole + j;
+      sp = p - j * a.nsplit;
+      ns = a.nsplit;
+      tail = x * a.xrem + j;
+    }
+  } else {
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    rbl = lin % (nrb * a.B * a.H);
+    sp = lin / (nrb * a.B * a.H);
+    ns = a.nsplit;
+  }
+  const int rb = rbl % nrb, bh = rbl / nrb;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int NKT64 = (a.T + 63) / 64, NKT32 = (a.T + 31) / 32;
-  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / a.nsplit);
-  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / a.nsplit));
+  const int kt_beg = 2 * (int)((int64_t)sp * NKT64 / ns);
+  const int kt_end = min(NKT32, 2 * (int)((int64_t)(sp + 1) * NKT64 / ns));
   const int r0 = rb * 128 + wave * 32, row = r0 + (lane & 31);
   const bool row_ok = row < a.R;
   const int NKT4 = (NKT64 + 3) & ~3, NRB32 = (a.R + 31) / 32;
@@ -305,9 +326,13 @@ __global__ __launch_bounds__(256, SD && D <= 96 ? 3 : 2) void fwd_kernel(FwdArgs
   if (!row_ok) return;
   const float lse = (m_run + __log2f(l_tot)) * LN2;
   float* op;
-  if (a.nsplit == 1 && !a.force_partial) {
+  if (ns == 1 && !a.force_partial) {
     op = reinterpret_cast<float*>(a.out) + ((int64_t)b * a.R + row) * C + h * D;
     if (hf == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = lse;
+  } else if (tail >= 0) {  // head-heavy tail piece: compact partial
+    const int64_t pi = ((int64_t)sp * 8 * a.xrem + tail) * 128 + (row - rb * 128);
+    op = a.opart + pi * D;
+    if (hf == 0) a.lpart[pi] = lse;
   } else {
     op = a.opart + (((int64_t)(a.sp0 + sp) * a.B + b) * a.R + row) * C + h * D;
     if (hf == 0) a.lpart[(((int64_t)(a.sp0 + sp) * a.B + b) * a.H + h) * a.R + row] = lse;
@@ -318,6 +343,39 @@ __global__ __launch_bounds__(256, SD && D <= 96 ? 3 : 2) void fwd_kernel(FwdArgs
     for (int g = 0; g < 4; ++g)
       *reinterpret_cast<f32x4*>(op + db * 32 + 8 * g + 4 * hf) =
           f32x4{o[db][4 * g] * inv, o[db][4 * g + 1] * inv, o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv};
+}
+
+// merge the head-heavy grid's split tail blocks (compact partials, fp32 out); see
+// flash_fwd_combine_tail.  One thread per (tail row, 4 output columns).
+__global__ __launch_bounds__(256) void combine_tail_kernel(FwdArgs a, int D) {
+  const int ntail = 8 * a.xrem;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)ntail * 128 * (D / 4)) return;
+  const int c4 = (int)(idx % (D / 4));
+  const int tr = (int)(idx / (D / 4));
+  const int rloc = tr & 127, t = tr >> 7;
+  const int nrb = (a.R + 127) / 128;
+  const int rbl = (t / a.xrem) * a.xrbs + a.xwhole + t % a.xrem;
+  const int rb = rbl % nrb, bh = rbl / nrb, b = bh / a.H, h = bh % a.H;
+  const int row = rb * 128 + rloc;
+  if (row >= a.R) return;
+  const int64_t pstride = (int64_t)ntail * 128, p0 = (int64_t)t * 128 + rloc;
+  float mx = -__builtin_inff(), sum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < a.nsplit; ++s) mx = fmaxf(mx, a.lpart[s * pstride + p0]);
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float l = a.lpart[s * pstride + p0];
+    if (l == -__builtin_inff()) continue;  // a piece that saw only masked columns (0 / 0 output)
+    const float wgt = __expf(l - mx);
+    sum += wgt;
+    acc += wgt * *reinterpret_cast<const f32x4*>(a.opart + (s * pstride + p0) * D + 4 * c4);
+  }
+  const float inv = 1.f / sum;  // fully masked row: NaN output, -inf lse
+  float* op = reinterpret_cast<float*>(a.out) + ((int64_t)b * a.R + row) * (a.H * D) + h * D + 4 * c4;
+  *reinterpret_cast<f32x4*>(op) = sum == 0.f ? f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                                                     __builtin_nanf("")}
+                                             : acc * inv;
+  if (c4 == 0) a.lse[((int64_t)b * a.H + h) * a.R + row] = mx + __logf(sum);
 }
 
 // merge split partials (fp32 out); see flash_fwd_combine
@@ -872,7 +930,7 @@ extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipS
   using namespace xdot::fa32;
   if (a->R == 0 || a->B == 0 || a->H == 0 || a->prescaled) return a->prescaled ? -1 : 0;
   const int nrb = (a->R + 127) / 128;
-  const dim3 grid(nrb * a->B * a->H * a->nsplit);
+  const dim3 grid(a->xrbs > 0 ? 8 * (a->xwhole + a->xrem * a->nsplit) : nrb * a->B * a->H * a->nsplit);
   if (a->sbuf) {
     if (fwd_direct_store()) {
 #define L(DV) hipLaunchKernelGGL((fwd_kernel<DV, true, true>), grid, dim3(256), lds_bytes<DV>(), st, *a)
@@ -890,6 +948,12 @@ extern "C" int xdot_flash_fwd_f32_launch(const xdot::fa::FwdArgs* a, int D, hipS
 
 extern "C" int xdot_flash_combine_f32_launch(const xdot::fa::FwdArgs* a, int D, hipStream_t st) {
   if (a->R == 0 || a->B == 0 || a->H == 0) return 0;
+  if (a->xrbs > 0) {  // head-heavy grid: only the tail blocks' compact partials
+    if (a->xrem <= 0) return 0;
+    const int64_t n = (int64_t)8 * a->xrem * 128 * (D / 4);
+    hipLaunchKernelGGL(xdot::fa32::combine_tail_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a, D);
+    return 0;
+  }
   const int64_t n = (int64_t)a->B * a->R * (a->H * D / 4);
   hipLaunchKernelGGL(xdot::fa32::combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a, D);
   return 0;
@@ -1046,6 +1110,28 @@ extern "C" int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D,
 }
 
 // column splits of the exact-fp32 forward (kernel 0) / row-side backward (1), see kernels.h
+extern "C" int xdot_flash_f32_heavy() {
+  static const int v = [] {
+    const char* e = std::getenv("XDOT_F32_HEAVY");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+// resident forward workgroups per CU of the exact-fp32 forward the launcher would pick (0: none)
+extern "C" int xdot_flash_f32_fwd_occ(int D, bool sbuf) {
+  using namespace xdot::fa32;
+  int occ = 0;
+#define OC(DV)                                                                                               \
+  if (D == DV)                                                                                               \
+    occ = sbuf ? (fwd_direct_store() ? xdot::fa::wg_per_cu(fwd_kernel<DV, true, true>, lds_bytes<DV>())      \
+                                     : xdot::fa::wg_per_cu(fwd_kernel<DV, true>, lds_bytes_sb<DV>()))        \
+               : xdot::fa::wg_per_cu(fwd_kernel<DV, false>, lds_bytes<DV>());
+  OC(32) OC(64) OC(96) OC(128)
+#undef OC
+  return occ;
+}
+
 extern "C" int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int64_t W, int64_t T) {
   using namespace xdot::fa32;
   int occ = 0;

@@ -240,6 +240,10 @@ int xdot_prescale_rows_launch(const void* x, void* out, int64_t n, float scale, 
 int xdot_flash_fwd_rows_per_wg();
 // one AdamW step over a->nt tensors of dtype dt (params/grads), fp32 moments
 int xdot_adamw_launch(const xdot::AdamArgs* a, int dt, hipStream_t st);
+// resident workgroups per CU of the exact-fp32 forward (head-heavy grid planning), 0: no kernel
+int xdot_flash_f32_fwd_occ(int D, bool sbuf);
+// XDOT_F32_HEAVY (default 1): the exact-fp32 forward may take the head-heavy grid
+int xdot_flash_f32_heavy();
 // a->nt conversions in one launch (DT_F32 / DT_BF16 / DT_F16 each side)
 int xdot_cast_multi_launch(const xdot::CastArgs* a, hipStream_t st);
 int xdot_mse_fwd_launch(const void* y, const void* t, void* dy, float* part, int nparts, void* loss, int64_t n, int dt,

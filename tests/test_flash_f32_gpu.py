@@ -518,3 +518,40 @@ def test_module_fp32_ds_only_mode(gpu, monkeypatch, mode):
                 m.zero_grad()
     finally:
         FLAGS.fp32_ds_only, FLAGS.fp32_mode = old
+
+
+@pytest.mark.parametrize("mask_kind", ["none", "random"])
+def test_flash_f32_head_heavy_forward(gpu, mask_kind):
+    """Exact-fp32 forward on the head-heavy grid (R = 97 row blocks x 8 heads = 776 blocks: each
+    XCD's 96 resident slots run its first 96 blocks whole, its last block in column pieces merged
+    by the tail combine): vs fp64 (<= 2e-6) and vs a forced uniform column split (<= 1e-6); a
+    fully masked row inside a tail block gives NaN output and -inf LSE like the reference."""
+    from xdot.ops import flash
+
+    B, R, H, D, T = 1, 97 * 128, 8, 96, 1024
+    C = H * D
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rows = torch.randn(B, R, C, generator=g).to(gpu)
+    kc = torch.randn(1, B, T, C, generator=g).to(gpu)
+    vc = torch.randn(1, B, T, C, generator=g).to(gpu)
+    mask = None
+    if mask_kind == "random":
+        mask = torch.rand(B, R, T, generator=g) < 0.1
+        mask[..., 0] = False
+        mask[:, R - 16, :] = True  # a fully masked row in the last (tail) row block of every head
+        mask = mask.to(gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)
+    o, lse = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=0, sbuf=sb)
+    ou, lu = flash.fwd(rows, kb, vb, mk, H, scale, nsplit=2, fp32_mode=0)
+    _, _, _, o64, l64 = _ref64(rows, kc, vc, mask, H, scale)
+    ok = torch.ones(R, dtype=torch.bool, device=gpu)
+    if mask is not None:
+        ok[R - 16] = False
+        assert torch.isnan(o[:, R - 16]).all() and torch.isneginf(lse[:, :, R - 16]).all()
+        assert torch.isnan(ou[:, R - 16]).all()
+    assert _rel(o[:, ok], o64[:, ok]) <= 2e-6
+    assert _rel(lse[:, :, ok], l64[:, :, ok]) <= 2e-6
+    assert _rel(o[:, ok], ou[:, ok]) <= 1e-6
