@@ -766,12 +766,25 @@ std::tuple<at::Tensor, at::Tensor> flash_bwd_cols(const at::Tensor& dout, const 
     int sq = 1, sv = 1;  // (the single-pass recompute kernels use sq for both halves: sv == sq there)
     TORCH_CHECK(xdot_flash_cols_splits(&a, dt, (int)g.D, &sq, &sv) == 0, "xdot.flash_bwd_cols: split config");
     const bool run_q = !sb || passes == 4 || (passes & 2), run_v = !sb || passes == 4 || (passes & 1);
-    if (run_q && sq > 1) {
+    int hw = 0, hr = 0, hs = 0;
+    if (dt == xdot::DT_F32 && xdot_flash_f32_cols_heavy(&a, (int)g.D, sq, &hw, &hr, &hs)) {
+      // head-heavy fused column pass: compact partials of the XCDs' tail blocks only
+      const int64_t W = ((g.T + 127) / 128) * g.B * H;
+      cpq = at::empty({(int64_t)hs * 8 * hr * 128 * g.D}, rows.options().dtype(at::kFloat));
+      cpv = at::empty({(int64_t)hs * 8 * hr * 128 * g.D}, rows.options().dtype(at::kFloat));
+      a.cpq = cpq.data_ptr<float>();
+      a.cpv = cpv.data_ptr<float>();
+      a.csq = a.csv = hs;
+      a.xcb = (int)(W / 8);
+      a.xwhole = hw;
+      a.xrem = hr;
+    }
+    if (a.xcb == 0 && run_q && sq > 1) {
       cpq = at::empty({sq, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
       a.cpq = cpq.data_ptr<float>();
       a.csq = sq;
     }
-    if (run_v && sv > 1) {
+    if (a.xcb == 0 && run_v && sv > 1) {
       cpv = at::empty({sv, g.B, g.T, g.C}, rows.options().dtype(at::kFloat));
       a.cpv = cpv.data_ptr<float>();
       a.csv = sv;

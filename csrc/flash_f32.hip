@@ -575,9 +575,27 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ncb = (a.T + 127) / 128;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int cb = lin % ncb, bhs = lin / ncb;
-  const int bh = bhs % (a.B * a.H), sp = bhs / (a.B * a.H), ns = a.csq > 1 ? a.csq : 1;
+  int cbl, sp, ns, tail = -1;  // linear column block (bh * ncb + cb), row piece, pieces of this block
+  if (a.xcb > 0) {  // head-heavy grid (BwdArgs::xcb): whole blocks first, the XCD's last ones split
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    if (k < a.xwhole) {
+      cbl = x * a.xcb + k;
+      sp = 0;
+      ns = 1;
+    } else {
+      const int p = k - a.xwhole, j = p / a.csq;
+      cbl = x * a.xcb + a.xwhole + j;
+      sp = p - j * a.csq;
+      ns = a.csq;
+      tail = x * a.xrem + j;
+    }
+  } else {
+    const int lin = xcd_remap(blockIdx.x, gridDim.x);
+    cbl = lin % (ncb * a.B * a.H);
+    sp = lin / (ncb * a.B * a.H);
+    ns = a.csq > 1 ? a.csq : 1;
+  }
+  const int cb = cbl % ncb, bh = cbl / ncb;
   const int b = bh / a.H, h = bh % a.H;
   const int C = a.H * D;
   const int c0 = cb * 128 + wave * 32, col = c0 + (lane & 31);
@@ -703,6 +721,11 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
   const int64_t prow = ((int64_t)sp * a.B + b) * a.T + col;  // row of the split partials
   float* pq = ns > 1 ? a.cpq + prow * C + h * D : reinterpret_cast<float*>(a.dkc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
   float* pv = ns > 1 ? a.cpv + prow * C + h * D : reinterpret_cast<float*>(a.dvc) + ((int64_t)b * a.T + col) * a.ldg + h * D;
+  if (tail >= 0) {  // head-heavy tail piece: compact partials
+    const int64_t pi = ((int64_t)sp * 8 * a.xrem + tail) * 128 + (col - cb * 128);
+    pq = a.cpq + pi * D;
+    pv = a.cpv + pi * D;
+  }
   const float sc = a.scale;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
@@ -714,6 +737,26 @@ __global__ __launch_bounds__(256, LS && D <= 96 ? 2 : 1) void bwd_cols_kernel(Bw
         *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g + 4 * hf) =
             f32x4{dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
     }
+}
+
+// head-heavy column pass: the tail blocks' compact row-piece partials summed in piece order into
+// the gathered-side gradient (fp32, row stride ldg).  One thread per (tail column, 4 values).
+__global__ __launch_bounds__(256) void cols_sum_tail_kernel(BwdArgs a, const float* part, float* out, int D) {
+  const int ntail = 8 * a.xrem;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)ntail * 128 * (D / 4)) return;
+  const int c4 = (int)(idx % (D / 4));
+  const int tc = (int)(idx / (D / 4));
+  const int cloc = tc & 127, t = tc >> 7;
+  const int ncb = (a.T + 127) / 128;
+  const int cbl = (t / a.xrem) * a.xcb + a.xwhole + t % a.xrem;
+  const int cb = cbl % ncb, bh = cbl / ncb, b = bh / a.H, h = bh % a.H;
+  const int col = cb * 128 + cloc;
+  if (col >= a.T) return;
+  const int64_t pstride = (int64_t)ntail * 128 * D, p0 = ((int64_t)t * 128 + cloc) * D + 4 * c4;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(part + p0);
+  for (int s = 1; s < a.csq; ++s) acc += *reinterpret_cast<const f32x4*>(part + s * pstride + p0);
+  *reinterpret_cast<f32x4*>(out + ((int64_t)b * a.T + col) * a.ldg + h * D + 4 * c4) = acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1010,6 +1053,22 @@ extern "C" int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D,
   auto sum_v = [&](int s) {
     if (s > 1) xdot_flash_cols_sum_launch(a->cpv, a->dvc, s, rows, C, a->ldg, xdot::DT_F32, st);
   };
+  if (a->sbuf && a->sb_passes == 4 && a->xcb > 0) {  // fused pass on the head-heavy grid
+    if (sq < 2 || !a->cpq || !a->cpv || 8 * a->xcb != W) return -1;
+    const dim3 grid(8 * (a->xwhole + a->xrem * sq));
+    const int64_t nt = (int64_t)8 * a->xrem * 128 * (D / 4);
+#define L(DV)                                                                                                  \
+  hipLaunchKernelGGL((bwd_cols_kernel<DV, true, true, true>), grid, dim3(256), lds_bytes_ds<DV>(), st, *a);     \
+  if (nt > 0) {                                                                                                  \
+    hipLaunchKernelGGL(cols_sum_tail_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, *a, a->cpq,   \
+                       reinterpret_cast<float*>(a->dkc), DV);                                                    \
+    hipLaunchKernelGGL(cols_sum_tail_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, *a, a->cpv,   \
+                       reinterpret_cast<float*>(a->dvc), DV);                                                    \
+  }                                                                                                              \
+  return 0;
+    XF32_DISPATCH(L)
+#undef L
+  }
   if (a->sbuf && a->sb_passes == 4) {  // fused: dP, dQ and dV in one pass (S -> dS)
 #define L(DV)                                                                                                  \
   hipLaunchKernelGGL((bwd_cols_kernel<DV, true, true, true>), dim3(W * sq), dim3(256), lds_bytes_ds<DV>(), st, *a); \
@@ -1110,6 +1169,35 @@ extern "C" int xdot_flash_rows_sum_f32_launch(const xdot::fa::BwdArgs* a, int D,
 }
 
 // column splits of the exact-fp32 forward (kernel 0) / row-side backward (1), see kernels.h
+extern "C" int xdot_flash_f32_cols_heavy(const xdot::fa::BwdArgs* a, int D, int sq, int* whole, int* rem, int* split) {
+  using namespace xdot::fa32;
+  if (!xdot_flash_f32_heavy() || !a->sbuf || a->sb_passes != 4 || a->fp32_mode || D > 128) return 0;
+  int occ = 0;
+#define OC(DV) \
+  if (D == DV) occ = xdot::fa::wg_per_cu(bwd_cols_kernel<DV, true, true, true>, lds_bytes_ds<DV>());
+  OC(32) OC(64) OC(96) OC(128)
+#undef OC
+  const int64_t W = (int64_t)((a->T + 127) / 128) * a->B * a->H, S = (int64_t)occ * (xdot_num_cus() / 8);
+  if (occ <= 0 || S <= 0 || W % 8) return 0;
+  // the forward's round model (bindings.cpp head_heavy_plan) over 64-row tiles of the row sweep
+  const int64_t m = W / 8, n = (a->R + 63) / 64, full = m / S, r = m % S;
+  if (r == 0 || full == 0) return 0;
+  const int su = sq > 1 ? sq : 1;
+  const double cu = (double)((W * su + 8 * S - 1) / (8 * S)) * ((double)n / su + 8.0);
+  double best = 1e300;
+  int bs = 0;
+  for (int s = 1; s <= 16; ++s) {
+    if (s > 1 && n / s < 8) break;
+    const double c = (double)full * ((double)n + 8.0) + (double)((r * s + S - 1) / S) * ((double)n / s + 8.0);
+    if (c < best * 0.985) { best = c; bs = s; }
+  }
+  if (bs < 2 || best >= cu * 0.97) return 0;
+  *whole = (int)(full * S);
+  *rem = (int)r;
+  *split = bs;
+  return 1;
+}
+
 extern "C" int xdot_flash_f32_heavy() {
   static const int v = [] {
     const char* e = std::getenv("XDOT_F32_HEAVY");

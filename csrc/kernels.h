@@ -107,6 +107,11 @@ struct BwdArgs {
   int csq, csv;
   float* cpq;
   float* cpv;
+  // head-heavy grid of the exact-fp32 fused column pass (xcb > 0): XCD x = blockIdx % 8 owns column
+  // blocks [x*xcb, (x+1)*xcb) (linear index bh*ncb + cb); the first xwhole sweep all rows and write
+  // the gradients directly, the last xrem run in csq row pieces whose partials are compact:
+  // cpq/cpv[((piece * 8*xrem + tail) * 128 + column-in-block) * D]
+  int xcb, xwhole, xrem;
 };
 
 }  // namespace fa
@@ -262,6 +267,9 @@ int xdot_flash_bwd_cols_f32_launch(const xdot::fa::BwdArgs* a, int D, hipStream_
 // recompute pass, *sv for the dV pass (score-buffer mode); both 1 for other families
 int xdot_flash_cols_splits(const xdot::fa::BwdArgs* a, int dt, int D, int* sq, int* sv);
 int xdot_flash_cols_splits_f32(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
+// head-heavy plan of the exact-fp32 fused column pass (sbuf, 4 passes, D <= 128): 1 and
+// (whole, rem, split) per XCD when the round model prefers it over the uniform split sq, else 0
+int xdot_flash_f32_cols_heavy(const xdot::fa::BwdArgs* a, int D, int sq, int* whole, int* rem, int* split);
 int xdot_flash_cols_splits_x3(const xdot::fa::BwdArgs* a, int D, int* sq, int* sv);
 // out[r * ldo + c] = Σ_s part[(s * rows + r) * C + c] for r < rows, c < C (C % 4 == 0): fp32
 // partials, output in dtype `dt` (DT_F32 / DT_BF16 / DT_F16)

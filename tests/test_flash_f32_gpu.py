@@ -555,3 +555,39 @@ def test_flash_f32_head_heavy_forward(gpu, mask_kind):
     assert _rel(o[:, ok], o64[:, ok]) <= 2e-6
     assert _rel(lse[:, :, ok], l64[:, :, ok]) <= 2e-6
     assert _rel(o[:, ok], ou[:, ok]) <= 1e-6
+
+
+@pytest.mark.parametrize("mask_kind", ["none", "random"])
+def test_flash_f32_fused_cols_head_heavy(gpu, mask_kind):
+    """The fused exact-fp32 column pass on its head-heavy grid (T = 65 column blocks x 8 heads =
+    520 blocks: each XCD's 64 resident slots sweep 64 blocks whole, its last block in row pieces
+    whose compact partials the tail sum adds) == the two-pass score-buffer path (uniform splits)
+    to fp32 summation order, and the row side that reads its dS likewise."""
+    from xdot.ops import flash
+
+    B, R, H, D, T = 1, 2048, 8, 96, 65 * 128
+    C = H * D
+    g = torch.Generator(device="cpu").manual_seed(13)
+    rows = torch.randn(B, R, C, generator=g).to(gpu)
+    kc = torch.randn(1, B, T, C, generator=g).to(gpu)
+    vc = torch.randn(1, B, T, C, generator=g).to(gpu)
+    do = torch.randn(B, R, C, generator=g).to(gpu)
+    mask = None
+    if mask_kind == "random":
+        mask = torch.rand(B, R, T, generator=g) < 0.1
+        mask[..., 0] = False
+        mask = mask.to(gpu)
+    scale = 1.0 / math.sqrt(D)
+    mk = flash.prepare_mask(mask, B, R, T)
+    kb, vb = flash.gathered_to_btc(kc), flash.gathered_to_btc(vc)
+    res = []
+    for passes in (4, 3):
+        sb = torch.full((flash.score_buffer_numel(B, H, R, T),), float("nan"), device=gpu)
+        o, l = flash.fwd(rows, kb, vb, mk, H, scale, fp32_mode=0, sbuf=sb)
+        dkv, dl = flash.bwd_cols(do, rows, kb, vb, o, l, mk, H, scale, fp32_mode=0, sbuf=sb, passes=passes)
+        dr = flash.bwd_rows(do, rows, kb, vb, l, dl, mk, H, scale, fp32_mode=0, sbuf=sb)
+        res.append((dkv, dr))
+    (a1, r1), (a0, r0) = res
+    assert torch.isfinite(a1).all()
+    assert _rel(a1, a0) <= 1e-6, f"cols {_rel(a1, a0):.2e}"
+    assert _rel(r1, r0) <= 1e-6, f"rows {_rel(r1, r0):.2e}"
