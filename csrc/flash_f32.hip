@@ -1233,5 +1233,9 @@ extern "C" int xdot_flash_f32_row_splits_exact(int kernel, int D, bool sbuf, int
   OC(32) OC(64) OC(96) OC(128)
 #undef OC
   if (!occ) return 0;
+  // the forward's workgroups are long (a 32-column fp32 tile is ~16x a 16-bit one), so a split
+  // costs little beside a part-full last round: up to 32 splits at 0.1 % each (the N=8 rank's 200
+  // row blocks: 23 splits fill six rounds of 768 slots instead of 7 splits in two part-full ones)
+  if (kernel == 0) return xdot::fa::pick_csplit(W, (int)((T + 31) / 32), occ * xdot_num_cus(), 32, 0.001);
   return xdot::fa::pick_csplit(W, (int)((T + 31) / 32), occ * xdot_num_cus(), 8, 0.004);
 }
